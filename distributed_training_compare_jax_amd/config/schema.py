@@ -1,0 +1,166 @@
+"""Configuration schema.
+
+Mirrors the three frozen dataclasses of the reference (``config/schema.py:7-38``):
+``ModelConfig``, ``OptimConfig`` and ``TrainConfig`` keep every reference field with
+the same name and meaning, so the reference YAML files load unchanged.  New fields
+are optional and default to the reference behaviour:
+
+* ``ModelConfig.vocab_pad_multiple`` — the vocab is padded (masked pad logits) to a
+  multiple of this so TP works at 4 and 8 GPUs (reference quirk: 50258 = 2*13*1933,
+  ``parallel/sharding.py:35``).
+* ``TrainConfig.dtype`` — ``bf16`` (MFMA bf16, fp32 master/accum) or ``fp32``.
+* ``TrainConfig.dp/tp/pp`` — explicit mesh degrees for hybrid runs (reference: one
+  1-D axis, ``train/train.py:29``).
+* ``TrainConfig.pp_schedule`` (``gpipe`` | ``1f1b``), ``pp_clip`` (``local`` is the
+  reference's stage-local global-norm clip, ``create_train_step.py:190``; ``global``
+  all-reduces the norm across stages).
+* ``TrainConfig.data`` (``synthetic`` | ``fineweb``), ``use_graph``, ``profile``,
+  ``dp_bucket_mb``, ``warmup_steps`` (reference hard-codes 5, ``train/train.py:64``),
+  ``grad_reduce_dtype``, ``ckpt_every``/``resume``.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field, replace
+from typing import Any, Dict, Optional
+
+PyTree = Any
+
+# GPT-2 BPE (50257) + the added <pad> token (reference data/fineweb_edu.py:8-12, main.py:17-18).
+REFERENCE_VOCAB_SIZE = 50258
+
+
+@dataclass(frozen=True)
+class ModelConfig:
+    vocab_size: int
+    d_model: int
+    n_layers: int
+    n_heads: int
+    d_ff: int
+    max_seq_len: int
+    dropout: float
+    parallel: str = "none"
+    # --- extensions (defaults = reference behaviour) ---
+    vocab_pad_multiple: int = 128
+    layernorm_eps: float = 1e-6  # flax nn.LayerNorm default
+    name: str = "gpt-ref-89M"
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.n_heads
+
+    @property
+    def padded_vocab(self) -> int:
+        m = max(1, int(self.vocab_pad_multiple))
+        return ((self.vocab_size + m - 1) // m) * m
+
+    def num_params(self) -> int:
+        """Parameter count of the reference architecture (unpadded vocab)."""
+        D, F, V, T, L = self.d_model, self.d_ff, self.vocab_size, self.max_seq_len, self.n_layers
+        per_layer = 4 * D * D + 4 * D + D * F + F + F * D + D + 4 * D
+        return V * D + T * D + L * per_layer + 2 * D + D * V + V
+
+    def flops_per_token(self) -> float:
+        """Matmul FLOPs per token, fwd+bwd (6*N_matmul + attention), as SURVEY §2.4."""
+        D, F, V, T, L = self.d_model, self.d_ff, self.vocab_size, self.max_seq_len, self.n_layers
+        mm = L * (4 * D * D + 2 * D * F) + D * V
+        attn = L * 2 * T * D  # QK^T + PV per token (full, non-causal count as the survey)
+        return 6.0 * mm + 3.0 * 2.0 * attn
+
+
+@dataclass(frozen=True)
+class OptimConfig:
+    lr: float
+    weight_decay: float
+    grad_clip: float
+    # optax.adamw defaults (optax 0.2.6)
+    b1: float = 0.9
+    b2: float = 0.999
+    eps: float = 1e-8
+
+
+@dataclass(frozen=True)
+class TrainConfig:
+    seed: int
+    parallel: str
+    # batching
+    batch: int
+    # steps
+    steps: int
+    log_every: int
+    # output
+    output_dir: str
+    # pipeline parallelism
+    pp_microbatches: int = 1
+    # --- extensions ---
+    dtype: str = "bf16"
+    dp: Optional[int] = None
+    tp: Optional[int] = None
+    pp: Optional[int] = None
+    pp_schedule: str = "gpipe"
+    pp_clip: str = "local"
+    data: str = "synthetic"
+    use_graph: bool = True
+    profile: bool = False
+    dp_bucket_mb: float = 64.0
+    grad_reduce_dtype: str = "fp32"
+    warmup_steps: int = 5
+    ckpt_every: int = 0
+    resume: bool = False
+    deterministic: bool = False
+    device: str = "auto"  # auto | cuda | cpu
+    batch_is_global: bool = True  # reference: `batch` is the global batch
+
+
+# Named model presets.  "ref" is the reference's configs/model_config.yaml.
+MODEL_PRESETS: Dict[str, Dict[str, Any]] = {
+    "ref": dict(d_model=512, n_layers=12, n_heads=16, d_ff=2048, max_seq_len=512, dropout=0.1,
+                name="gpt-ref-89M"),
+    "gpt2-small": dict(d_model=768, n_layers=12, n_heads=12, d_ff=3072, max_seq_len=1024, dropout=0.1,
+                       name="gpt2-small-124M"),
+    "gpt2-medium": dict(d_model=1024, n_layers=24, n_heads=16, d_ff=4096, max_seq_len=1024, dropout=0.1,
+                        name="gpt2-medium-355M"),
+    "tiny": dict(d_model=64, n_layers=2, n_heads=4, d_ff=256, max_seq_len=32, dropout=0.1, name="tiny"),
+}
+
+
+def model_config_from_preset(preset: str, vocab_size: int = REFERENCE_VOCAB_SIZE, **overrides) -> ModelConfig:
+    d = dict(MODEL_PRESETS[preset])
+    d.update(overrides)
+    return ModelConfig(vocab_size=vocab_size, **d)
+
+
+def _filter_fields(cls, d: Dict[str, Any]) -> Dict[str, Any]:
+    names = {f.name for f in dataclasses.fields(cls)}
+    unknown = set(d) - names
+    if unknown:
+        raise TypeError(f"{cls.__name__}: unknown config keys {sorted(unknown)}")
+    return d
+
+
+def load_yaml(path: str) -> Dict[str, Any]:
+    import yaml
+
+    with open(path) as f:
+        return yaml.safe_load(f) or {}
+
+
+def build_configs(train_config_path: str, model_config_path: str = "configs/model_config.yaml",
+                  optim_config_path: str = "configs/optim_config.yaml",
+                  vocab_size: int = REFERENCE_VOCAB_SIZE):
+    """Same assembly as reference main.py:14-30: vocab injected, parallel copied into ModelConfig."""
+    mdict = load_yaml(model_config_path)
+    mdict["vocab_size"] = vocab_size
+    tdict = load_yaml(train_config_path)
+    train_config = TrainConfig(**_filter_fields(TrainConfig, tdict))
+    mdict["parallel"] = train_config.parallel
+    model_config = ModelConfig(**_filter_fields(ModelConfig, mdict))
+    opt_config = OptimConfig(**_filter_fields(OptimConfig, load_yaml(optim_config_path)))
+    return train_config, model_config, opt_config
+
+
+__all__ = [
+    "PyTree", "ModelConfig", "OptimConfig", "TrainConfig", "MODEL_PRESETS", "REFERENCE_VOCAB_SIZE",
+    "model_config_from_preset", "build_configs", "load_yaml", "replace", "field",
+]

@@ -1,0 +1,195 @@
+"""GPT decoder with explicit forward/backward (no autograd on the hot path).
+
+Same architecture as the reference ``model/GPTModel.py`` (pre-LN blocks of
+``TransformerBlock.py:13-26``: ``x += out(attn(LN1 x))``, ``x += fc2(gelu(fc1(LN2 x)))``;
+learned absolute positions; untied ``lm_head`` with bias) and the same three callable
+partitions the reference exposes for pipelining (``embed_forward`` / ``stage_forward`` /
+``head_forward``, ``GPTModel.py:24-74``).
+
+Why explicit backward instead of autograd: every backward op is a fused HIP kernel that
+writes its gradient straight into the flat fp32 grad buffer (``parallel/buffers.py``),
+activations are kept exactly as the kernels need them (bf16 GEMM operands, fp32
+residual stream, LN mean/rstd, attention LSE), TP collectives sit at exactly the four
+points per block Megatron-style TP needs, and the whole step is a static sequence of
+kernel launches that can be captured into hipGraphs.  Numerical equivalence to the
+autograd oracle (``models/reference.py``) is tested in ``tests/test_model.py``.
+
+Dtypes: residual stream fp32; GEMM operands in the compute dtype (bf16 on MI355X, fp32
+on the CPU oracle path); all accumulation fp32; grads fp32.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from ..config.schema import ModelConfig
+from ..ops import attention as A
+from ..ops import embedding as E
+from ..ops import gemm as G
+from ..ops import layernorm as LN
+from ..ops import xent as X
+from ..parallel.buffers import FlatParams
+
+
+class NoComm:
+    """TP communicator stub for tp_size == 1."""
+
+    size = 1
+    rank = 0
+
+    def all_reduce_(self, t):
+        return t
+
+    def all_gather_stack(self, t):
+        return t.unsqueeze(0)
+
+
+@dataclass
+class StageLayout:
+    layers: range
+    has_embed: bool
+    has_head: bool
+
+
+class GPTStage:
+    """The slice of the GPT owned by one rank (all of it, a TP shard, or a PP stage)."""
+
+    def __init__(self, cfg: ModelConfig, flat: FlatParams, layout: StageLayout, tp=None,
+                 dropout_seed: int = 0, act_dtype: torch.dtype = torch.bfloat16):
+        self.cfg = cfg
+        self.flat = flat
+        self.layout = layout
+        self.tp = tp if tp is not None else NoComm()
+        self.seed = int(dropout_seed)
+        self.act_dtype = act_dtype
+        D, H = cfg.d_model, cfg.n_heads
+        assert D % H == 0
+        assert H % self.tp.size == 0, f"n_heads {H} not divisible by tp {self.tp.size}"
+        self.heads_local = H // self.tp.size
+        self.v_local = cfg.padded_vocab // self.tp.size
+        self.v_start = self.tp.rank * self.v_local
+        self.v_valid = max(0, min(self.v_local, cfg.vocab_size - self.v_start))
+        self.eps = cfg.layernorm_eps
+
+    # ------------------------------------------------------------------ embed
+    def embed_forward(self, ids: torch.Tensor, step: torch.Tensor, row0: int, ctx: Dict) -> torch.Tensor:
+        """ids int32 [b, T] → h fp32 [b*T, D]  (wte gather + wpe + dropout, GPTModel.py:30-38)."""
+        f = self.flat
+        ctx["embed"] = (ids, row0)
+        return E.embed_fwd(ids, f.p("wte"), f.p("wpe"), self.cfg.dropout, self.seed, step, row0)
+
+    def embed_backward(self, ctx: Dict, dh: torch.Tensor, step: torch.Tensor, beta: float):
+        ids, row0 = ctx.pop("embed")
+        f = self.flat
+        E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta)
+
+    # ------------------------------------------------------------------ block
+    def block_forward(self, l: int, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
+        f, p = self.flat, f"h.{l}."
+        tp = self.tp
+        lead = tp.rank == 0  # row-parallel bias + residual are added by exactly one TP rank
+        T = x.shape[0] // batch
+        y1, mu1, rs1 = LN.layernorm_fwd(x, f.p(p + "ln1.g"), f.p(p + "ln1.b"), self.eps, self.act_dtype)
+        qkv = G.linear(y1, f.w(p + "qkv.w"), f.p(p + "qkv.b"))
+        o, lse = A.attn_fwd(qkv.view(batch, T, -1), self.heads_local)
+        o = o.view(batch * T, -1)
+        x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
+        tp.all_reduce_(x2)
+        y2, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
+        u, gact = G.linear_gelu(y2, f.w(p + "fc1.w"), f.p(p + "fc1.b"))
+        x3 = G.linear_resid(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b") if lead else None, x2 if lead else None)
+        tp.all_reduce_(x3)
+        ctx[l] = (x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch)
+        return x3
+
+    def block_backward(self, l: int, ctx: Dict, dx3: torch.Tensor, dx3_c: torch.Tensor, beta: float):
+        """dx3 fp32 (and its compute-dtype copy) → (dx, dx_c) wrt the block input."""
+        f, p = self.flat, f"h.{l}."
+        tp = self.tp
+        x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch = ctx.pop(l)
+        T = x.shape[0] // batch
+        # MLP
+        du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
+        G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta)
+        G.colsum(dx3, f.g(p + "fc2.b"), beta)
+        dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
+        G.wgrad(du, y2, f.g(p + "fc1.w"), beta)
+        G.colsum(du, f.g(p + "fc1.b"), beta)
+        tp.all_reduce_(dy2)
+        dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta)
+        # attention
+        do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
+        G.wgrad(dx2_c, o, f.g(p + "out.w"), beta)
+        G.colsum(dx2, f.g(p + "out.b"), beta)
+        dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
+                          self.heads_local).view(batch * T, -1)
+        dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
+        G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta)
+        G.colsum(dqkv, f.g(p + "qkv.b"), beta)
+        tp.all_reduce_(dy1)
+        return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta)
+
+    def _ln_bwd(self, dy, x, ln: str, mu, rs, dres, beta):
+        f = self.flat
+        dx_c = None if self.act_dtype == torch.float32 else torch.empty(dy.shape, dtype=self.act_dtype,
+                                                                        device=dy.device)
+        dx = LN.layernorm_bwd(dy, x, f.p(ln + ".g"), mu, rs, dres, f.g(ln + ".g"), f.g(ln + ".b"), beta,
+                              out_c=dx_c)
+        return dx, (dx if dx_c is None else dx_c)
+
+    def stage_forward(self, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
+        for l in self.layout.layers:
+            x = self.block_forward(l, x, batch, ctx)
+        return x
+
+    # ------------------------------------------------------------------ head
+    def head_forward(self, x: torch.Tensor, labels: torch.Tensor, loss_scale: float, ctx: Dict,
+                     loss_out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+        """Final LN + lm_head + CE (GPTModel.py:69-74; create_train_step.py:32-34).
+
+        Returns a device scalar ``loss_scale · Σ_tokens CE`` (1-element fp32 tensor)."""
+        f = self.flat
+        yf, muf, rsf = LN.layernorm_fwd(x, f.p("lnf.g"), f.p("lnf.b"), self.eps, self.act_dtype)
+        lab = labels.reshape(-1)
+        logits, rowstat, lab_logit = X.lmhead_logits_partials(yf, f.w("lm_head.w"), f.p("lm_head.b"), lab,
+                                                              self.v_start, self.v_valid)
+        if self.tp.size > 1:
+            rowstats = self.tp.all_gather_stack(rowstat)  # [tp, M, 2]
+            self.tp.all_reduce_(lab_logit)
+        else:
+            rowstats = rowstat.unsqueeze(0)
+        lse, loss = X.ce_finalize(rowstats, lab_logit, loss_scale, loss_out, accumulate)
+        ctx["head"] = (x, yf, muf, rsf, logits, lse, lab)
+        return loss
+
+    def head_backward(self, ctx: Dict, grad_scale: float, beta: float):
+        f = self.flat
+        x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
+        dlogits = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale)
+        dyf = G.matmul_nn(dlogits, f.w("lm_head.w"))
+        G.wgrad(dlogits, yf, f.g("lm_head.w"), beta)
+        G.colsum(dlogits, f.g("lm_head.b"), beta)
+        del logits, dlogits
+        self.tp.all_reduce_(dyf)
+        return self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta)
+
+    def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None):
+        """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist."""
+        for l in reversed(list(self.layout.layers)):
+            dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta)
+            if hook is not None:
+                hook(l)
+        return dx, dx_c
+
+
+def full_forward_loss(stage: GPTStage, ids, labels, step, row0: int = 0, ctx: Optional[Dict] = None):
+    """Convenience: embed → all layers → head (single-stage layout), returns (loss, ctx)."""
+    ctx = {} if ctx is None else ctx
+    b, T = ids.shape
+    h = stage.embed_forward(ids, step, row0, ctx)
+    h = stage.stage_forward(h, b, ctx)
+    loss = stage.head_forward(h, labels, 1.0 / (b * T), ctx)
+    return loss, ctx

@@ -1,0 +1,126 @@
+"""Loader for the in-tree HIP kernel library ``_dtc_kernels.so`` (gfx950).
+
+The kernels are plain HIP C++ (``csrc/*.hip``) compiled by ``hipcc --offload-arch=gfx950``
+into one shared object with a C ABI; Python calls it through ctypes with raw device
+pointers and the current HIP stream, so every launch is stream-ordered and
+hipGraph-capturable.  torch is imported first so the library binds to the same
+``libamdhip64.so.7`` instance torch already loaded (same SONAME).
+
+On a GPU tensor there is NO silent fallback: if the library is missing or fails to
+load, :func:`lib` raises.  CPU tensors use the pure-torch reference implementations in
+the op modules (the test oracle and the gloo plumbing path).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_LIB = None
+_LOCK = threading.Lock()
+LIB_NAME = "_dtc_kernels.so"
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+
+c_int = ctypes.c_int
+c_long = ctypes.c_long
+c_float = ctypes.c_float
+c_vp = ctypes.c_void_p
+
+
+class GemmArgs(ctypes.Structure):
+    """Mirror of ``struct GemmArgs`` in csrc/common.h (keep in sync)."""
+
+    _fields_ = [
+        ("layout", c_int),       # 0: C=A.B^T (nt)  1: C=A.B (nn)  2: C=A^T.B (tn)
+        ("M", c_int), ("N", c_int), ("K", c_int),
+        ("A", c_vp), ("lda", c_long),
+        ("B", c_vp), ("ldb", c_long),
+        ("C", c_vp), ("ldc", c_long),
+        ("c_f32", c_int),        # C dtype: 0 bf16, 1 fp32
+        ("epi", c_int),          # epilogue id (EPI_*)
+        ("bias", c_vp),          # fp32 [N] or null
+        ("aux", c_vp), ("ldaux", c_long),   # epi-specific input (residual fp32 / gelu pre-act bf16)
+        ("aux_out", c_vp),       # epi-specific second output (gelu output bf16)
+        ("alpha", c_float), ("beta", c_float),
+        ("labels", c_vp),        # int32 [M] (lm-head CE epilogue)
+        ("vocab_start", c_int), ("n_valid", c_int),
+        ("part", c_vp),          # float2 [M][nparts]
+        ("label_out", c_vp),     # fp32 [M]
+        ("workspace", c_vp), ("ws_bytes", c_long),
+        ("split_k", c_int),      # 0 = auto
+    ]
+
+
+EPI_STORE = 0       # C = alpha*acc (+bias) (+beta*C if fp32)
+EPI_RESID = 1       # C(f32) = aux(f32) + acc + bias
+EPI_GELU = 2        # C(bf16) = u = acc+bias ; aux_out(bf16) = gelu_tanh(u)
+EPI_DGELU = 3       # C(bf16) = acc * gelu_tanh'(aux)
+EPI_LMHEAD = 4      # C(bf16) = acc+bias, pad cols -inf; per-row partial (max,sumexp); label logit
+
+
+def _declare(lib):
+    vp, i, l, f = c_vp, c_int, c_long, c_float
+    sigs = {
+        "dtc_version": ([], i),
+        "dtc_gemm": ([ctypes.POINTER(GemmArgs), vp], i),
+        "dtc_gemm_workspace_bytes": ([i, i, i, i], l),
+        "dtc_lmhead_nparts": ([i], i),
+        "dtc_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
+        "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, vp], i),
+        "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
+        "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, vp], i),
+        "dtc_colsum_workspace_bytes": ([i, i], l),
+        "dtc_embed_fwd": ([vp, vp, vp, vp, i, i, i, i, f, l, vp, l, vp], i),
+        "dtc_embed_bwd": ([vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),
+        "dtc_attn_fwd": ([vp, vp, vp, i, i, i, i, l, f, vp], i),
+        "dtc_attn_bwd": ([vp, vp, vp, vp, vp, vp, i, i, i, i, l, f, vp, l, vp], i),
+        "dtc_attn_bwd_workspace_bytes": ([i, i, i, i], l),
+        "dtc_ce_combine": ([vp, i, i, l, l, vp, vp, vp, f, vp, i, vp], i),
+        "dtc_ce_bwd": ([vp, l, vp, vp, i, i, i, i, f, vp], i),
+        "dtc_sumsq_segments": ([vp, vp, i, vp, vp, vp, l, vp], i),
+        "dtc_sumsq_workspace_bytes": ([], l),
+        "dtc_adamw": ([vp, vp, vp, vp, vp, l, l, vp, vp, f, f, f, f, f, f, f, vp], i),
+        "dtc_cast_f32_bf16": ([vp, vp, l, vp], i),
+        "dtc_fill_f32": ([vp, f, l, vp], i),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+def available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+def lib():
+    """The loaded kernel library; raises (never falls back) if it is unavailable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"HIP kernel library {LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(or python -m distributed_training_compare_jax_amd.csrc.build)")
+            _LIB = _declare(ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL))
+    return _LIB
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error code {rc}")

@@ -1,0 +1,213 @@
+"""GEMM-shaped ops: every Dense of the reference model, forward and backward.
+
+Reference sites: q/k/v/out Dense (``model/CausalSelfAttention.py:18-20,46``), fc1/fc2
+(``model/MLP.py:13,20``), lm_head (``model/GPTModel.py:72``).  Weights are stored
+``[out, in]`` (the transpose of Flax's ``[in, out]`` kernel) so the forward GEMM has both
+operands K-contiguous.  On GPU all three GEMM forms run on the hand-written MFMA kernel
+in ``csrc/gemm.hip`` (bf16 in, fp32 accumulate) with fused epilogues:
+
+* ``linear``         y = x·Wᵀ + b                       (bf16 out)
+* ``linear_resid``   x_out = resid + x·Wᵀ + b           (fp32 residual stream)
+* ``linear_gelu``    u = x·Wᵀ + b ; g = gelu_tanh(u)     (fc1 + ``nn.gelu``, MLP.py:14)
+* ``matmul_nn``      dX = dY·W                           (dgrad, fp32 out)
+* ``matmul_nn_dgelu`` dU = (dY·W) ⊙ gelu'(u)             (fc2 dgrad fused with GELU bwd)
+* ``wgrad``          dW = β·dW + dYᵀ·X                    (fp32, written straight into the flat grad buffer)
+* ``colsum``         db = β·db + Σ_rows dY                (bias grads)
+
+CPU tensors take the pure-torch fp32 path below (the oracle / gloo path).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _native as N
+
+_SQRT_2_OVER_PI = math.sqrt(2.0 / math.pi)
+
+
+def gelu_tanh(u: torch.Tensor) -> torch.Tensor:
+    """``jax.nn.gelu(approximate=True)`` (flax ``nn.gelu`` default)."""
+    return 0.5 * u * (1.0 + torch.tanh(_SQRT_2_OVER_PI * (u + 0.044715 * u * u * u)))
+
+
+def gelu_tanh_grad(u: torch.Tensor) -> torch.Tensor:
+    inner = _SQRT_2_OVER_PI * (u + 0.044715 * u * u * u)
+    t = torch.tanh(inner)
+    dinner = _SQRT_2_OVER_PI * (1.0 + 3.0 * 0.044715 * u * u)
+    return 0.5 * (1.0 + t) + 0.5 * u * (1.0 - t * t) * dinner
+
+
+# ----------------------------------------------------------------------------- native glue
+_WS = {}
+
+
+def _workspace(device, nbytes: int) -> torch.Tensor:
+    """Persistent per-device scratch (split-K slabs etc.).  Grows, never shrinks; stream-ordered reuse."""
+    key = (device.type, device.index)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("GEMM workspace must be reserved before graph capture (call ops.reserve_workspace)")
+        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws
+
+
+def reserve_workspace(device, nbytes: int):
+    _workspace(torch.device(device), nbytes)
+
+
+def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, *,
+                 epi: int = N.EPI_STORE, bias=None, aux=None, ldaux: int = 0, aux_out=None,
+                 alpha: float = 1.0, beta: float = 0.0, labels=None, vocab_start: int = 0,
+                 n_valid: int = 0, part=None, label_out=None):
+    L = N.lib()
+    ws_need = int(L.dtc_gemm_workspace_bytes(layout, M, N_, K))
+    ws = _workspace(c.device, ws_need) if ws_need > 0 else None
+    args = N.GemmArgs(
+        layout=layout, M=M, N=N_, K=K,
+        A=a.data_ptr(), lda=lda, B=b.data_ptr(), ldb=ldb, C=c.data_ptr(), ldc=ldc,
+        c_f32=1 if c.dtype == torch.float32 else 0, epi=epi,
+        bias=N.ptr(bias), aux=N.ptr(aux), ldaux=ldaux, aux_out=N.ptr(aux_out),
+        alpha=alpha, beta=beta, labels=N.ptr(labels), vocab_start=vocab_start, n_valid=n_valid,
+        part=N.ptr(part), label_out=N.ptr(label_out),
+        workspace=N.ptr(ws), ws_bytes=0 if ws is None else ws.numel(), split_k=0)
+    N.check(L.dtc_gemm(args, N.stream_ptr(c.device)), "dtc_gemm")
+
+
+def _check2d(t: torch.Tensor, name: str):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a row-major 2-D tensor, got shape {tuple(t.shape)} strides {t.stride()}")
+    if t.is_cuda and t.dtype not in (torch.bfloat16,):
+        raise TypeError(f"{name}: GPU GEMM operands are bf16, got {t.dtype}")
+
+
+def _f32(t):
+    return None if t is None else t.float()
+
+
+# ----------------------------------------------------------------------------- forward
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    M, K = x.shape
+    Nn = w.shape[0]
+    assert w.shape[1] == K
+    out_dtype = out_dtype or x.dtype
+    if not x.is_cuda:
+        y = _f32(x) @ _f32(w).t()
+        if bias is not None:
+            y = y + bias.float()
+        return y.to(out_dtype)
+    _check2d(x, "x"); _check2d(w, "w")
+    y = torch.empty(M, Nn, dtype=out_dtype, device=x.device)
+    _gemm_native(0, M, Nn, K, x, x.stride(0), w, w.stride(0), y, Nn, bias=bias)
+    return y
+
+
+def linear_resid(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
+                 resid: Optional[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 ``out = resid + x·Wᵀ + bias`` (resid/bias optional; ``out`` may alias ``resid``)."""
+    M, K = x.shape
+    Nn = w.shape[0]
+    if not x.is_cuda:
+        y = _f32(x) @ _f32(w).t()
+        if bias is not None:
+            y = y + bias.float()
+        if resid is not None:
+            y = y + resid
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _check2d(x, "x"); _check2d(w, "w")
+    if out is None:
+        out = torch.empty(M, Nn, dtype=torch.float32, device=x.device)
+    if resid is not None:
+        assert resid.dtype == torch.float32 and resid.is_contiguous()
+        _gemm_native(0, M, Nn, K, x, x.stride(0), w, w.stride(0), out, Nn, epi=N.EPI_RESID, bias=bias,
+                     aux=resid, ldaux=Nn)
+    else:
+        _gemm_native(0, M, Nn, K, x, x.stride(0), w, w.stride(0), out, Nn, bias=bias)
+    return out
+
+
+def linear_gelu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]):
+    """Returns ``(u, g)``: pre-activation and ``gelu_tanh(u)`` (both activation dtype)."""
+    M, K = x.shape
+    Nn = w.shape[0]
+    if not x.is_cuda:
+        u = _f32(x) @ _f32(w).t()
+        if bias is not None:
+            u = u + bias.float()
+        return u.to(x.dtype), gelu_tanh(u).to(x.dtype)
+    _check2d(x, "x"); _check2d(w, "w")
+    u = torch.empty(M, Nn, dtype=torch.bfloat16, device=x.device)
+    g = torch.empty_like(u)
+    _gemm_native(0, M, Nn, K, x, x.stride(0), w, w.stride(0), u, Nn, epi=N.EPI_GELU, bias=bias, aux_out=g)
+    return u, g
+
+
+# ----------------------------------------------------------------------------- backward
+def matmul_nn(dy: torch.Tensor, w: torch.Tensor, out_dtype=torch.float32) -> torch.Tensor:
+    """dX[M,K] = dY[M,N]·W[N,K]."""
+    M, Nn = dy.shape
+    K = w.shape[1]
+    assert w.shape[0] == Nn
+    if not dy.is_cuda:
+        return (_f32(dy) @ _f32(w)).to(out_dtype)
+    _check2d(dy, "dy"); _check2d(w, "w")
+    dx = torch.empty(M, K, dtype=out_dtype, device=dy.device)
+    _gemm_native(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), dx, K)
+    return dx
+
+
+def matmul_nn_dgelu(dy: torch.Tensor, w: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """dU = (dY·W) ⊙ gelu_tanh'(u)   (fc2 dgrad fused with the GELU backward)."""
+    M, Nn = dy.shape
+    K = w.shape[1]
+    if not dy.is_cuda:
+        return ((_f32(dy) @ _f32(w)) * gelu_tanh_grad(_f32(u))).to(u.dtype)
+    _check2d(dy, "dy"); _check2d(w, "w")
+    du = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    _gemm_native(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), du, K, epi=N.EPI_DGELU, aux=u, ldaux=K)
+    return du
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
+    """dW[N,K] = β·dW + dY[M,N]ᵀ·X[M,K]  (fp32 ``dw`` is a view into the flat grad buffer)."""
+    M, Nn = dy.shape
+    K = x.shape[1]
+    assert x.shape[0] == M and tuple(dw.shape) == (Nn, K)
+    if not dy.is_cuda:
+        g = _f32(dy).t() @ _f32(x)
+        if beta != 0.0:
+            dw.mul_(beta).add_(g)
+        else:
+            dw.copy_(g)
+        return dw
+    _check2d(dy, "dy"); _check2d(x, "x")
+    assert dw.dtype == torch.float32 and dw.is_contiguous()
+    _gemm_native(2, Nn, K, M, dy, dy.stride(0), x, x.stride(0), dw, K, beta=beta)
+    return dw
+
+
+def colsum(dy: torch.Tensor, db: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
+    """db[N] = β·db + Σ_m dY[m, :]  (deterministic two-stage reduction on GPU)."""
+    M, Nn = dy.shape
+    if not dy.is_cuda:
+        s = _f32(dy).sum(0)
+        if beta != 0.0:
+            db.mul_(beta).add_(s)
+        else:
+            db.copy_(s)
+        return db
+    L = N.lib()
+    ws = _workspace(dy.device, int(L.dtc_colsum_workspace_bytes(M, Nn)))
+    is_f32 = 1 if dy.dtype == torch.float32 else 0
+    N.check(L.dtc_colsum(dy.data_ptr(), is_f32, M, Nn, dy.stride(0), db.data_ptr(), beta,
+                         ws.data_ptr(), ws.numel(), N.stream_ptr(dy.device)), "dtc_colsum")
+    return db

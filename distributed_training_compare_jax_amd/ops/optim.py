@@ -1,0 +1,95 @@
+"""Fused clip-by-global-norm + AdamW over flat fp32 buffers.
+
+Reference: ``train/create_optimizer.py:8-12`` —
+``optax.chain(clip_by_global_norm(1.0), adamw(lr=3e-4, weight_decay=0.1))`` with optax
+defaults (b1 0.9, b2 0.999, eps 1e-8, eps_root 0, bias correction, decoupled decay on
+ALL params, no mask):
+
+    g ← g·min(1, max_norm/‖g‖)         (optax: where(‖g‖ < max, g, g/‖g‖·max))
+    m ← b1·m + (1−b1)·g ;  v ← b2·v + (1−b2)·g²
+    p ← p − lr·( m/(1−b1ᵗ) / (√(v/(1−b2ᵗ)) + eps) + wd·p )
+
+GPU path (``csrc/optim.hip``): (1) a deterministic two-stage Σg² over a segment table
+(each segment carries a weight so TP-replicated params are counted once across ranks),
+whose finalize kernel also bumps the device step counter; (2) ONE streaming kernel over
+the whole flat buffer that applies clip+AdamW and writes the bf16 compute mirror of the
+weights — no per-parameter launches, no host sync (graph-capturable).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _native as N
+from .gemm import _workspace
+
+
+def make_segments(segments, device) -> torch.Tensor:
+    """segments: list of (offset, length, weight) → packed float64 tensor [S, 3] for the kernel."""
+    t = torch.tensor([[float(o), float(n), float(w)] for (o, n, w) in segments], dtype=torch.float64)
+    return t.to(device)
+
+
+def sumsq_segments(flat: torch.Tensor, segments: torch.Tensor, out: torch.Tensor,
+                   step: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[0] = Σ_s w_s·Σ_{i∈s} flat[i]²  (fp32).  If ``step`` is given it is incremented by 1."""
+    if not flat.is_cuda:
+        acc = torch.zeros((), dtype=torch.float64)
+        for o, n, w in segments.tolist():
+            seg = flat[int(o):int(o) + int(n)].double()
+            acc += w * (seg * seg).sum()
+        out.fill_(float(acc))
+        if step is not None:
+            step.add_(1)
+        return out
+    L = N.lib()
+    ws = _workspace(flat.device, int(L.dtc_sumsq_workspace_bytes()))
+    N.check(L.dtc_sumsq_segments(flat.data_ptr(), segments.data_ptr(), segments.shape[0], out.data_ptr(),
+                                 N.ptr(step), ws.data_ptr(), ws.numel(), N.stream_ptr(flat.device)),
+            "dtc_sumsq_segments")
+    return out
+
+
+def adamw_flat(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+               mirror: Optional[torch.Tensor], n_mirror: int, step: torch.Tensor, sumsq: torch.Tensor,
+               lr: float, b1: float, b2: float, eps: float, wd: float, max_norm: float):
+    """In-place AdamW on flat fp32 buffers; ``mirror[:n_mirror] = bf16(p[:n_mirror])``.
+
+    ``step`` (int64 [1], already incremented) gives t for the bias correction; ``sumsq``
+    (fp32 [1]) is the global Σg² for the clip."""
+    n = p.numel()
+    if not p.is_cuda:
+        t = float(step.item())
+        norm = float(sumsq.item()) ** 0.5
+        scale = 1.0 if (max_norm <= 0 or norm < max_norm) else max_norm / norm
+        gg = g * scale
+        m.mul_(b1).add_(gg, alpha=1 - b1)
+        v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+        mhat = m / (1 - b1 ** t)
+        vhat = v / (1 - b2 ** t)
+        p.sub_(lr * (mhat / (vhat.sqrt() + eps) + wd * p))
+        if mirror is not None and n_mirror > 0:
+            mirror[:n_mirror].copy_(p[:n_mirror])
+        return
+    N.check(N.lib().dtc_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), N.ptr(mirror), n, n_mirror,
+                              step.data_ptr(), sumsq.data_ptr(), lr, b1, b2, eps, wd, max_norm, 0.0,
+                              N.stream_ptr(p.device)), "dtc_adamw")
+
+
+def cast_to_bf16(src: torch.Tensor, dst: torch.Tensor):
+    if not src.is_cuda:
+        dst.copy_(src)
+        return
+    N.check(N.lib().dtc_cast_f32_bf16(src.data_ptr(), dst.data_ptr(), src.numel(), N.stream_ptr(src.device)),
+            "dtc_cast_f32_bf16")
+
+
+def fill_(t: torch.Tensor, value: float):
+    """t[:] = value (fp32; graph-capturable on GPU)."""
+    if not t.is_cuda:
+        t.fill_(value)
+        return t
+    N.check(N.lib().dtc_fill_f32(t.data_ptr(), value, t.numel(), N.stream_ptr(t.device)), "dtc_fill_f32")
+    return t

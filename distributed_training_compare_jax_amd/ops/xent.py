@@ -1,0 +1,99 @@
+"""Fused lm_head + softmax cross-entropy (reference ``model/GPTModel.py:71-72`` and
+``train/create_train_step.py:32-34``: ``softmax_cross_entropy_with_integer_labels(...).mean()``).
+
+Forward (GPU): ONE MFMA GEMM ``logits = h·Wᵀ + b`` whose epilogue also emits, per row and
+per 128-column tile, the partial ``(max, Σexp)`` of the fp32 accumulators and captures the
+label logit — the 4096×50304 fp32 logits (823 MB in the reference) are never re-read for
+the forward loss.  Logits are kept only as bf16 (412 MB, trivially resident in 288 GB
+HBM) for the backward, which is one streaming pass ``dlogits = (softmax − onehot)·scale``
+written in place, followed by the two GEMMs of the Dense backward.
+
+The vocab is padded (``ModelConfig.padded_vocab``); pad columns get ``-inf`` logits, so
+their probability and gradient are exactly 0 — identical loss to the unpadded reference.
+Vocab-parallel TP: each rank owns columns ``[vocab_start, vocab_start+V_local)``; rows'
+``(max, Σexp)`` and label logits are combined across ranks (``parallel/tp.py``).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+
+def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, labels: torch.Tensor,
+                           vocab_start: int, n_valid: int):
+    """Returns ``(logits [M,Vl], rowstat [M,2] (max,Σexp), label_logit [M])`` for the local vocab shard.
+
+    ``n_valid`` = number of real (non-pad) columns in this shard; ``label_logit`` is 0 for rows
+    whose label is outside the shard."""
+    M, D = h.shape
+    Vl = w.shape[0]
+    if not h.is_cuda:
+        logits = h.float() @ w.float().t() + b.float()
+        if n_valid < Vl:
+            logits[:, n_valid:] = float("-inf")
+        mx = logits.max(-1).values
+        se = torch.exp(logits - mx[:, None]).sum(-1)
+        loc = labels.long() - vocab_start
+        inside = (loc >= 0) & (loc < n_valid)
+        lab = torch.where(inside, logits.gather(1, loc.clamp(0, Vl - 1)[:, None])[:, 0], torch.zeros(M))
+        return logits.to(h.dtype), torch.stack([mx, se], -1), lab
+    L = N.lib()
+    P = int(L.dtc_lmhead_nparts(Vl))
+    logits = torch.empty(M, Vl, dtype=torch.bfloat16, device=h.device)
+    part = torch.empty(M, P, 2, dtype=torch.float32, device=h.device)
+    lab = torch.zeros(M, dtype=torch.float32, device=h.device)
+    from .gemm import _gemm_native
+
+    _gemm_native(0, M, Vl, D, h, h.stride(0), w, w.stride(0), logits, Vl, epi=N.EPI_LMHEAD, bias=b,
+                 labels=labels, vocab_start=vocab_start, n_valid=n_valid, part=part, label_out=lab)
+    rowstat = torch.empty(M, 2, dtype=torch.float32, device=h.device)
+    N.check(L.dtc_ce_combine(part.data_ptr(), M, P, P, 1, None, None, rowstat.data_ptr(), 0.0, None, 0,
+                             N.stream_ptr(h.device)), "dtc_ce_combine")
+    return logits, rowstat, lab
+
+
+def ce_finalize(rowstats: torch.Tensor, label_logit: torch.Tensor, loss_scale: float,
+                loss_out: torch.Tensor | None = None, accumulate: bool = False):
+    """rowstats [R, M, 2] (R vocab shards) + label_logit [M] → (lse [M], loss).
+
+    ``loss = scale·Σ(lse − label)`` (1-element fp32), written to / accumulated into ``loss_out``."""
+    R, M, _ = rowstats.shape
+    if loss_out is None:
+        loss_out = torch.zeros(1, dtype=torch.float32, device=rowstats.device)
+    if not rowstats.is_cuda:
+        mx = rowstats[..., 0].max(0).values
+        s = (rowstats[..., 1] * torch.exp(rowstats[..., 0] - mx[None])).sum(0)
+        lse = mx + torch.log(s)
+        loss = (lse - label_logit).sum() * loss_scale
+        if accumulate:
+            loss_out.add_(loss)
+        else:
+            loss_out.fill_(float(loss))
+        return lse, loss_out
+    lse = torch.empty(M, dtype=torch.float32, device=rowstats.device)
+    assert rowstats.is_contiguous()
+    N.check(N.lib().dtc_ce_combine(rowstats.data_ptr(), M, R, 1, M, label_logit.data_ptr(), lse.data_ptr(), None,
+                                   loss_scale, loss_out.data_ptr(), 1 if accumulate else 0,
+                                   N.stream_ptr(rowstats.device)), "dtc_ce_combine")
+    return lse, loss_out
+
+
+def ce_backward_inplace(logits: torch.Tensor, lse: torch.Tensor, labels: torch.Tensor, vocab_start: int,
+                        n_valid: int, grad_scale: float) -> torch.Tensor:
+    """logits → dlogits = (exp(logits − lse) − onehot)·grad_scale (pad columns 0), in place."""
+    M, Vl = logits.shape
+    if not logits.is_cuda:
+        p = torch.exp(logits.float() - lse[:, None])
+        if n_valid < Vl:
+            p[:, n_valid:] = 0.0
+        loc = labels.long() - vocab_start
+        inside = (loc >= 0) & (loc < n_valid)
+        rows = torch.nonzero(inside)[:, 0]
+        p[rows, loc[rows]] -= 1.0
+        logits.copy_((p * grad_scale).to(logits.dtype))
+        return logits
+    N.check(N.lib().dtc_ce_bwd(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), M, Vl,
+                               vocab_start, n_valid, grad_scale, N.stream_ptr(logits.device)), "dtc_ce_bwd")
+    return logits

@@ -1,0 +1,120 @@
+"""Flat per-rank parameter / gradient / optimizer-state buffers.
+
+One contiguous fp32 buffer each for master params, grads, Adam m and v (+ a bf16 mirror
+of the GEMM-side params) replaces the reference's pytree of 22 leaves.  This is what
+makes the MI355X step cheap:
+
+* the fused clip+AdamW (``ops/optim.py``) is ONE launch over the whole buffer;
+* DP gradient buckets are plain contiguous slices (grads are laid out in backward
+  order), so each RCCL all-reduce / reduce-scatter is one large message;
+* wgrad GEMM epilogues write straight into their slice (no autograd accumulation copy);
+* checkpoints are a handful of tensors plus an index.
+
+Offsets are 64-element (256-B) aligned for 16-byte vector access.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Tuple
+
+import torch
+
+from ..models.params import ParamSpec, init_full, local_shape, shard
+
+ALIGN = 64
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+@dataclass
+class Slot:
+    spec: ParamSpec
+    offset: int
+    shape: Tuple[int, ...]
+
+    @property
+    def numel(self) -> int:
+        n = 1
+        for s in self.shape:
+            n *= s
+        return n
+
+
+class FlatParams:
+    def __init__(self, specs: List[ParamSpec], tp_rank: int, tp_size: int, device, compute_dtype=torch.bfloat16):
+        self.specs = specs
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        self.slots: Dict[str, Slot] = {}
+        off = 0
+        n_mirror = 0
+        seen_nonmirror = False
+        for s in specs:
+            shp = local_shape(s, tp_size)
+            slot = Slot(s, off, shp)
+            self.slots[s.name] = slot
+            off = _align(off + slot.numel)
+            if s.mirror:
+                assert not seen_nonmirror, "mirrored params must precede non-mirrored ones"
+                n_mirror = off
+            else:
+                seen_nonmirror = True
+        self.numel = max(off, ALIGN)
+        self.n_mirror = n_mirror
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.params = torch.zeros(self.numel, **f32)
+        self.grads = torch.zeros(self.numel, **f32)
+        self.exp_avg = torch.zeros(self.numel, **f32)
+        self.exp_avg_sq = torch.zeros(self.numel, **f32)
+        self.use_mirror = compute_dtype != torch.float32
+        self.mirror = (torch.zeros(max(n_mirror, ALIGN), dtype=compute_dtype, device=self.device)
+                       if self.use_mirror else None)
+
+    # -- init -----------------------------------------------------------------
+    def init_canonical(self, seed: int):
+        for name, slot in self.slots.items():
+            full = init_full(slot.spec, seed)
+            loc = shard(slot.spec, full, self.tp_rank, self.tp_size)
+            self.p(name).copy_(loc.to(self.device))
+        self.refresh_mirror()
+
+    def refresh_mirror(self):
+        if self.use_mirror and self.n_mirror > 0:
+            from ..ops.optim import cast_to_bf16
+
+            cast_to_bf16(self.params[: self.n_mirror], self.mirror[: self.n_mirror])
+
+    # -- views ----------------------------------------------------------------
+    def _view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        s = self.slots[name]
+        return buf[s.offset: s.offset + s.numel].view(s.shape)
+
+    def p(self, name: str) -> torch.Tensor:
+        return self._view(self.params, name)
+
+    def g(self, name: str) -> torch.Tensor:
+        return self._view(self.grads, name)
+
+    def w(self, name: str) -> torch.Tensor:
+        """Compute-dtype view (bf16 mirror on GPU, fp32 master otherwise)."""
+        if self.use_mirror and self.slots[name].spec.mirror:
+            return self._view(self.mirror, name)
+        return self.p(name)
+
+    def has(self, name: str) -> bool:
+        return name in self.slots
+
+    def range_of(self, names: List[str]) -> Tuple[int, int]:
+        lo = min(self.slots[n].offset for n in names)
+        hi = max(_align(self.slots[n].offset + self.slots[n].numel) for n in names)
+        return lo, hi
+
+    def segments(self, weight_fn) -> List[Tuple[int, int, float]]:
+        return [(s.offset, s.numel, float(weight_fn(s.spec))) for s in self.slots.values()]
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {"params": self.params, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}

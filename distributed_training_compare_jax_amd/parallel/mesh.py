@@ -1,0 +1,118 @@
+"""DP × TP × PP process mesh.
+
+The reference has a single 1-D device axis ``"data"`` used by both DP and TP
+(``train/train.py:29``) and a separate ``pmap`` axis ``"pipe"`` for PP
+(``create_train_step.py:70``).  Here the three axes are explicit process groups:
+
+    rank = (pp_idx · dp + dp_idx) · tp + tp_idx
+
+TP is innermost so a TP group is a block of adjacent GPUs (on an 8×MI355X xGMI mesh every
+pair is one hop, but adjacency keeps a TP group inside one socket on multi-node
+layouts), DP next, PP outermost.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch.distributed as dist
+
+
+@dataclass
+class Mesh:
+    dp: int
+    tp: int
+    pp: int
+    rank: int
+    dp_idx: int
+    tp_idx: int
+    pp_idx: int
+    dp_group: Optional[object] = None
+    tp_group: Optional[object] = None
+    pp_group: Optional[object] = None
+    # ranks of neighbours inside the pp group (global ranks)
+    pp_prev: Optional[int] = None
+    pp_next: Optional[int] = None
+
+    @property
+    def world(self) -> int:
+        return self.dp * self.tp * self.pp
+
+    def rank_of(self, dp_idx: int, tp_idx: int, pp_idx: int) -> int:
+        return (pp_idx * self.dp + dp_idx) * self.tp + tp_idx
+
+
+def resolve_degrees(parallel: str, world: int, dp: Optional[int], tp: Optional[int], pp: Optional[int]):
+    """Map the reference's single ``parallel`` string (+ optional explicit degrees) onto (dp, tp, pp)."""
+    if dp or tp or pp:
+        dp, tp, pp = dp or 1, tp or 1, pp or 1
+        if dp * tp * pp != world:
+            # fill the unspecified axis implied by the strategy
+            rest = world // (dp * tp * pp) if world % (dp * tp * pp) == 0 else None
+            if rest is None:
+                raise ValueError(f"dp*tp*pp = {dp * tp * pp} does not divide world size {world}")
+            if parallel == "tp":
+                tp *= rest
+            elif parallel == "pp":
+                pp *= rest
+            else:
+                dp *= rest
+        return dp, tp, pp
+    if parallel == "dp":
+        return world, 1, 1
+    if parallel == "tp":
+        return 1, world, 1
+    if parallel == "pp":
+        return 1, 1, world
+    if parallel in ("none", "single"):
+        if world != 1:
+            raise ValueError("parallel=none needs world size 1")
+        return 1, 1, 1
+    raise ValueError(f"Unsupported strategy `{parallel}`")
+
+
+def build_mesh(rank: int, world: int, dp: int, tp: int, pp: int) -> Mesh:
+    assert dp * tp * pp == world, (dp, tp, pp, world)
+    tp_idx = rank % tp
+    dp_idx = (rank // tp) % dp
+    pp_idx = rank // (tp * dp)
+    m = Mesh(dp, tp, pp, rank, dp_idx, tp_idx, pp_idx)
+    if world > 1 and dist.is_initialized():
+        # every rank must create every group, in the same order
+        for p in range(pp):
+            for d in range(dp):
+                ranks = [m.rank_of(d, t, p) for t in range(tp)]
+                g = dist.new_group(ranks) if tp > 1 else None
+                if p == pp_idx and d == dp_idx:
+                    m.tp_group = g
+        for p in range(pp):
+            for t in range(tp):
+                ranks = [m.rank_of(d, t, p) for d in range(dp)]
+                g = dist.new_group(ranks) if dp > 1 else None
+                if p == pp_idx and t == tp_idx:
+                    m.dp_group = g
+        for d in range(dp):
+            for t in range(tp):
+                ranks = [m.rank_of(d, t, p) for p in range(pp)]
+                g = dist.new_group(ranks) if pp > 1 else None
+                if d == dp_idx and t == tp_idx:
+                    m.pp_group = g
+    if pp_idx > 0:
+        m.pp_prev = m.rank_of(dp_idx, tp_idx, pp_idx - 1)
+    if pp_idx < pp - 1:
+        m.pp_next = m.rank_of(dp_idx, tp_idx, pp_idx + 1)
+    return m
+
+
+def split_layers(n_layers: int, pp: int, weights=None):
+    """Contiguous layer ranges per stage.  Fixes the reference quirk ``layers_per_stage =
+    n_layers // N`` (``train/train.py:118``) that silently drops layers when N ∤ L: the
+    remainder goes to the EARLIEST stages (the last stage also carries lm_head+CE)."""
+    base, rem = divmod(n_layers, pp)
+    out, start = [], 0
+    for s in range(pp):
+        n = base + (1 if s < rem else 0)
+        out.append(range(start, start + n))
+        start += n
+    return out

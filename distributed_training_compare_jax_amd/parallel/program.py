@@ -1,0 +1,129 @@
+"""Step programs: a training step as a static sequence of hipGraph segments and collectives.
+
+The reference jit-compiles the whole step into one XLA program
+(``train/create_train_step.py:28-50``) so the host issues one call per step.  The MI355X
+analog is to capture the step's kernel stream into hipGraphs.  Collectives are kept OUT
+of the graphs on purpose: RCCL calls are issued eagerly between graph segments on the
+same stream order, which
+
+* lets a DP gradient bucket's all-reduce run on RCCL's own stream while the NEXT backward
+  segment replays (overlap without capturing RCCL),
+* keeps PP send/recv and TP all-reduces on the well-trodden eager RCCL path.
+
+``record(step_fn)`` runs ``step_fn`` once with capture on; every ``comm(fn)`` call the
+step makes cuts the current graph, runs the collective for real (on whatever stale data
+the buffers hold — the recording pass computes nothing) and opens the next graph.
+``replay()`` then issues [graph, comm, graph, comm, ...] with one host call each.  With
+``mode="eager"`` the same step code just executes (CPU/gloo path, first warmup steps).
+All segments share one memory pool and are replayed in capture order, so activations
+produced in one segment and consumed in a later one stay valid.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import torch
+
+
+class StepProgram:
+    def __init__(self, device: torch.device, use_graph: bool):
+        self.device = torch.device(device)
+        self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        self.items: List[Tuple[str, Any, Optional[str]]] = []
+        self.recording = False
+        self.recorded = False
+        self._graph = None
+        self._pool = None
+        self._handles: Dict[str, Any] = {}
+        self._stream = torch.cuda.Stream(self.device) if self.use_graph else None
+
+    # -------------------------------------------------------------- step-code API
+    def comm(self, fn: Callable[[], Any], name: Optional[str] = None):
+        """Issue a collective.  ``fn`` may return an async Work handle, retrievable by ``wait(name)``."""
+        if self.recording:
+            self._cut()
+            self.items.append(("comm", fn, name))
+            res = fn()
+            if name is not None:
+                self._handles[name] = res
+            self._begin()
+            return res
+        res = fn()
+        if name is not None:
+            self._handles[name] = res
+        return res
+
+    def wait(self, name: str):
+        if self.recording:
+            self._cut()
+            self.items.append(("wait", None, name))
+            self._wait(name)
+            self._begin()
+        else:
+            self._wait(name)
+
+    def _wait(self, name):
+        h = self._handles.pop(name, None)
+        if h is not None:
+            if isinstance(h, (list, tuple)):
+                for x in h:
+                    x.wait()
+            else:
+                h.wait()
+
+    # -------------------------------------------------------------- capture / replay
+    def _begin(self):
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+        if self._pool is None:
+            self._pool = g.pool()
+        self._graph = g
+
+    def _cut(self):
+        g, self._graph = self._graph, None
+        g.capture_end()
+        self.items.append(("graph", g, None))
+
+    def record(self, step_fn: Callable[[], Any]) -> Any:
+        assert self.use_graph
+        self.items = []
+        torch.cuda.synchronize(self.device)
+        cur = torch.cuda.current_stream(self.device)
+        self._stream.wait_stream(cur)
+        self.recording = True
+        try:
+            with torch.cuda.stream(self._stream):
+                self._begin()
+                out = step_fn()
+                self._cut()
+        finally:
+            self.recording = False
+        cur.wait_stream(self._stream)
+        torch.cuda.synchronize(self.device)
+        self.recorded = True
+        return out
+
+    def replay(self):
+        for kind, obj, name in self.items:
+            if kind == "graph":
+                obj.replay()
+            elif kind == "comm":
+                res = obj()
+                if name is not None:
+                    self._handles[name] = res
+            else:
+                self._wait(name)
+
+    @property
+    def n_graphs(self) -> int:
+        return sum(1 for k, _, _ in self.items if k == "graph")
+
+    @property
+    def n_comms(self) -> int:
+        return sum(1 for k, _, _ in self.items if k != "graph")
+
+
+class EagerProgram(StepProgram):
+    def __init__(self, device):
+        super().__init__(device, use_graph=False)

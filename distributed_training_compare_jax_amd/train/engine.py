@@ -1,0 +1,179 @@
+"""Training engine: one rank's model shard, flat buffers, optimizer and the step program.
+
+Reference counterparts: the DP/TP jitted step (``train/create_train_step.py:24-52``), the
+PP pmap/scan step (``:55-195``) and the state plumbing of ``train/train.py:22-233``.
+One class serves every layout (DP, TP, PP and their products): the mesh decides which
+layers/params this rank owns and which collectives run; the step itself is a static
+sequence of HIP kernels + RCCL calls that :class:`StepProgram` captures into hipGraph
+segments after the first eager warmup step.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..config.schema import ModelConfig, OptimConfig, TrainConfig
+from ..models.gpt import GPTStage, StageLayout
+from ..models.params import stage_param_specs
+from ..ops import optim as O
+from ..parallel.buffers import FlatParams
+from ..parallel.dist import DistInfo
+from ..parallel.dp import GradBuckets
+from ..parallel.mesh import Mesh, build_mesh, resolve_degrees, split_layers
+from ..parallel.program import StepProgram
+from ..parallel.tp import TPComm
+from .optimizer import FusedAdamW
+
+
+class Engine:
+    def __init__(self, model_cfg: ModelConfig, train_cfg: TrainConfig, opt_cfg: OptimConfig, dinfo: DistInfo):
+        self.mcfg, self.tcfg, self.ocfg = model_cfg, train_cfg, opt_cfg
+        self.dinfo = dinfo
+        self.device = dinfo.device
+        dp, tp, pp = resolve_degrees(train_cfg.parallel, dinfo.world, train_cfg.dp, train_cfg.tp, train_cfg.pp)
+        self.mesh: Mesh = build_mesh(dinfo.rank, dinfo.world, dp, tp, pp)
+        m = self.mesh
+        on_gpu = self.device.type == "cuda"
+        self.act_dtype = torch.bfloat16 if (on_gpu and train_cfg.dtype == "bf16") else torch.float32
+        if on_gpu and self.act_dtype == torch.float32:
+            raise NotImplementedError("fp32 compute on GPU: use dtype: bf16 (fp32 parity mode runs on the CPU path)")
+
+        # ---- batch geometry (reference: `batch` is the global batch, train_config_*.yaml:1)
+        T = model_cfg.max_seq_len
+        self.T = T
+        self.global_batch = train_cfg.batch
+        if self.global_batch % dp:
+            raise ValueError(f"global batch {self.global_batch} not divisible by dp={dp}")
+        self.b_local = self.global_batch // dp
+        self.n_micro = max(1, train_cfg.pp_microbatches) if pp > 1 else 1
+        if self.b_local % self.n_micro:
+            raise ValueError(f"local batch {self.b_local} not divisible by pp_microbatches={self.n_micro}")
+        self.mb_rows = self.b_local // self.n_micro
+        self.row0 = m.dp_idx * self.b_local
+
+        # ---- ownership
+        layer_ranges = split_layers(model_cfg.n_layers, pp)
+        self.layout = StageLayout(layer_ranges[m.pp_idx], has_embed=m.pp_idx == 0, has_head=m.pp_idx == pp - 1)
+        specs = stage_param_specs(model_cfg, self.layout.layers, self.layout.has_embed, self.layout.has_head)
+        self.flat = FlatParams(specs, m.tp_idx, tp, self.device, compute_dtype=self.act_dtype)
+        self.flat.init_canonical(train_cfg.seed)
+
+        # ---- step program, comms, model, optimizer
+        self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu)
+        self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program)
+        self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
+                              act_dtype=self.act_dtype)
+        self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb)
+        self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,
+                              pp_global_clip=(train_cfg.pp_clip == "global"))
+
+        # ---- static device-side inputs/outputs (graph replay reads/writes these)
+        self.ids = torch.zeros(self.b_local, T, dtype=torch.int32, device=self.device)
+        self.labels = torch.zeros(self.b_local, T, dtype=torch.int32, device=self.device)
+        pin = on_gpu
+        self._host = [torch.zeros(2, self.b_local, T, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._host_i = 0
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        D = model_cfg.d_model
+        if pp > 1:
+            self.recv_x = [torch.zeros(self.mb_rows * T, D, dtype=torch.float32, device=self.device)
+                           for _ in range(self.n_micro)]
+            self.recv_dx = [torch.zeros(self.mb_rows * T, D, dtype=torch.float32, device=self.device)
+                            for _ in range(self.n_micro)]
+            self.recv_dx_c = [torch.zeros(self.mb_rows * T, D, dtype=self.act_dtype, device=self.device)
+                              for _ in range(self.n_micro)] if self.act_dtype != torch.float32 else self.recv_dx
+        self.steps_done = 0
+        if on_gpu:
+            self._reserve_workspaces()
+
+    # ------------------------------------------------------------------ helpers
+    def _reserve_workspaces(self):
+        from ..ops.gemm import reserve_workspace
+
+        reserve_workspace(self.device, 64 << 20)
+
+    @property
+    def tokens_per_step(self) -> int:
+        return self.global_batch * self.T
+
+    def set_batch(self, batch_np: np.ndarray):
+        """batch_np int32 [b_local, T+1] (this rank's rows) → static device ids/labels."""
+        h = self._host[self._host_i]
+        self._host_i ^= 1
+        h[0].copy_(torch.from_numpy(batch_np[:, :-1]))
+        h[1].copy_(torch.from_numpy(batch_np[:, 1:]))
+        self.ids.copy_(h[0], non_blocking=True)
+        self.labels.copy_(h[1], non_blocking=True)
+
+    # ------------------------------------------------------------------ step bodies
+    def _step_fn_dp_tp(self):
+        st, T, b = self.stage, self.T, self.b_local
+        dp = self.mesh.dp
+        ctx: Dict = {}
+        step = self.opt.step_t
+        h = st.embed_forward(self.ids, step, self.row0, ctx)
+        h = st.stage_forward(h, b, ctx)
+        st.head_forward(h, self.labels, 1.0 / (b * T), ctx, loss_out=self.loss)
+        dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
+        self.buckets.ready_upto(self.buckets.head_end_offset())
+        bk = self.buckets
+        dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=lambda l: bk.ready_upto(bk.layer_end_offset(l)))
+        st.embed_backward(ctx, dx, step, 0.0)
+        self.buckets.ready_all()
+        self.buckets.wait_all()
+        self._loss_allreduce()
+        self.opt.step()
+        return self.loss
+
+    def _loss_allreduce(self):
+        m = self.mesh
+        groups = []
+        if m.dp > 1:
+            groups.append(m.dp_group)
+        if m.pp > 1:
+            groups.append(m.pp_group)
+        for g in groups:
+            t = self.loss
+            self.program.comm(lambda g=g, t=t: dist.all_reduce(t, group=g))
+
+    def _step_fn_pp(self):
+        from ..parallel.pp import run_pipeline
+
+        run_pipeline(self)
+        self.buckets.ready_all()
+        self.buckets.wait_all()
+        self._loss_allreduce()
+        self.opt.step()
+        return self.loss
+
+    def _step_fn(self):
+        return self._step_fn_pp() if self.mesh.pp > 1 else self._step_fn_dp_tp()
+
+    # ------------------------------------------------------------------ public
+    def run_step(self) -> torch.Tensor:
+        """Enqueue one full training step on the static inputs; returns the (device) loss."""
+        p = self.program
+        if not p.use_graph:
+            self._step_fn()
+        elif not p.recorded:
+            if self.steps_done == 0:
+                self._step_fn()  # eager first step: lazy RCCL init, workspace sizing
+            else:
+                p.record(self._step_fn)
+                p.replay()
+        else:
+            p.replay()
+        self.steps_done += 1
+        return self.loss
+
+    def loss_value(self) -> float:
+        """Blocking read of the global mean loss (reference: float(np.asarray(loss)), train.py:82)."""
+        v = float(self.loss.item())
+        return v / self.mesh.dp
+
+    def grad_norm(self) -> float:
+        return self.opt.grad_norm()

@@ -1,0 +1,53 @@
+"""Optimizer: clip-by-global-norm(1.0) + AdamW(3e-4, wd 0.1) over the flat buffers.
+
+Reference: ``train/create_optimizer.py:8-12`` (optax chain).  The global norm is computed
+over exactly the reference's set of gradients:
+
+* DP: grads are identical after the all-reduce → local Σg² is the global one.
+* TP: sharded params' Σg² is summed over the TP group, replicated params (identical on
+  every TP rank) are weighted 1/tp so the all-reduce counts them once.
+* PP: ``pp_clip: local`` (default) clips with the stage-local norm exactly like the
+  reference's per-stage ``tx.update`` (``create_train_step.py:189-191``);
+  ``pp_clip: global`` all-reduces Σg² over the pipeline (what a single-device run does).
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..config.schema import OptimConfig
+from ..ops import optim as O
+from ..parallel.buffers import FlatParams
+
+
+class FusedAdamW:
+    def __init__(self, flat: FlatParams, cfg: OptimConfig, program, tp_size: int = 1, tp_group=None,
+                 pp_group=None, pp_global_clip: bool = False):
+        self.flat = flat
+        self.cfg = cfg
+        self.program = program
+        self.tp_size, self.tp_group = tp_size, tp_group
+        self.pp_group = pp_group if pp_global_clip else None
+        dev = flat.device
+        w = (lambda spec: 1.0 if spec.tp != "rep" else 1.0 / tp_size)
+        self.segments = O.make_segments(flat.segments(w), dev)
+        self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step(self):
+        f, c = self.flat, self.cfg
+        O.sumsq_segments(f.grads, self.segments, self.sumsq, step=self.step_t)
+        if self.tp_size > 1:
+            g = self.tp_group
+            s = self.sumsq
+            self.program.comm(lambda: dist.all_reduce(s, group=g))
+        if self.pp_group is not None:
+            g = self.pp_group
+            s = self.sumsq
+            self.program.comm(lambda: dist.all_reduce(s, group=g))
+        O.adamw_flat(f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.mirror, f.n_mirror if f.use_mirror else 0,
+                     self.step_t, self.sumsq, c.lr, c.b1, c.b2, c.eps, c.weight_decay, c.grad_clip)
+
+    def grad_norm(self) -> float:
+        return float(self.sumsq.item()) ** 0.5

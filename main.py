@@ -1,0 +1,76 @@
+"""CLI entry point — same interface as the reference ``main.py:10-57``.
+
+    python main.py --train_config_path configs/train_config_{dp,tp,pp}.yaml
+
+Loads ``configs/model_config.yaml`` and ``configs/optim_config.yaml`` (paths relative to the
+CWD, as in the reference), injects ``vocab_size`` (50258 = GPT-2 + <pad>) and
+``parallel``, prints ``Running `<strategy>` on N devices.`` and trains.
+
+Process model: one rank per GPU.  Under ``torchrun`` the ranks already exist; started as
+a plain script it spawns one process per visible GPU itself (the reference uses every
+visible device, ``main.py:34``).  ``--nproc`` overrides the count (e.g. gloo ranks on CPU).
+"""
+
+from __future__ import annotations
+
+import os
+
+import click
+
+
+def _run(train_config_path: str, model_config_path: str, optim_config_path: str, overrides: dict):
+    from distributed_training_compare_jax_amd.config.schema import build_configs, replace
+    from distributed_training_compare_jax_amd.data.synthetic import get_tokenizer
+    from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
+    from distributed_training_compare_jax_amd.train.loop import train
+
+    train_config, model_config, opt_config = build_configs(train_config_path, model_config_path, optim_config_path,
+                                                           vocab_size=len(get_tokenizer()))
+    if overrides:
+        train_config = replace(train_config, **overrides)
+    if train_config.parallel not in ("dp", "tp", "pp"):
+        raise ValueError(f"Unsupported strategy `{train_config.parallel}`")
+    dinfo = init_distributed(train_config.device)
+    if dinfo.rank == 0:
+        print(f"Running `{train_config.parallel}` on {dinfo.world} devices.", flush=True)
+    try:
+        train(train_config, model_config, opt_config, dinfo)
+    finally:
+        destroy()
+
+
+def _spawn_target(args):
+    _run(*args)
+
+
+@click.command()
+@click.option("--train_config_path", default="configs/train_config_dp.yaml")
+@click.option("--model_config_path", default="configs/model_config.yaml", show_default=True)
+@click.option("--optim_config_path", default="configs/optim_config.yaml", show_default=True)
+@click.option("--nproc", type=int, default=None, help="ranks to spawn (default: all visible GPUs, else 1)")
+@click.option("--steps", type=int, default=None, help="override train_config.steps")
+@click.option("--device", type=click.Choice(["auto", "cuda", "cpu"]), default=None)
+def main(train_config_path: str, model_config_path: str, optim_config_path: str, nproc, steps, device):
+    overrides = {}
+    if steps is not None:
+        overrides["steps"] = steps
+    if device is not None:
+        overrides["device"] = device
+    args = (train_config_path, model_config_path, optim_config_path, overrides)
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        _run(*args)
+        return
+    import torch
+
+    if nproc is None:
+        nproc = torch.cuda.device_count() if (device != "cpu" and torch.cuda.device_count() > 0) else 1
+    if nproc <= 1:
+        _run(*args)
+        return
+    from distributed_training_compare_jax_amd.parallel.dist import spawn
+
+    spawn(_spawn_target, nproc, args=(args,))
+
+
+if __name__ == "__main__":
+    main()
