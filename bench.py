@@ -1,0 +1,121 @@
+"""Headline benchmark: training throughput of the reference GPT on N MI355X GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--parallel dp|tp|pp] [--model ref|gpt2-small|gpt2-medium]
+
+Metric (BASELINE.json): avg step time (ms) + tokens/sec of the reference model
+(``configs/model_config.yaml``: d_model 512, 12 layers, 16 heads, d_ff 2048, seq 512,
+vocab 50258, 89.6 M params — the model BASELINE.json calls "GPT-2 small") trained with
+AdamW + global-norm clip, bf16 MFMA compute / fp32 master weights, synthetic
+FineWeb-shaped tokens (no network) and random-init weights.
+
+Each timed step does exactly what the reference's timed loop does (``train/train.py:75-85``):
+next host batch → H2D → full forward + backward + gradient all-reduce + clip + AdamW →
+blocking loss read.  W untimed warmup steps first (the first one eager, then hipGraph
+capture), then K steps bracketed by barrier + device sync on both sides; the MAX over
+ranks is reported.  ``value`` is whole-job tokens/s.
+
+Scaling: ``dp`` keeps 8 sequences per GPU (weak scaling, global batch 8·N); ``tp`` and
+``pp`` keep the reference global batch of 8 (strong scaling; pp uses 2·N microbatches).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_TOKENS_PER_S = {"dp": 27887.0, "tp": 27919.0, "pp": 19978.0}  # BASELINE.md (4096 tok/step)
+METRIC = "avg step time (ms) + tokens/sec, GPT-2-small DP/TP/PP at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--parallel", default="dp", choices=["dp", "tp", "pp"])
+    ap.add_argument("--model", default="ref")
+    ap.add_argument("--batch_per_gpu", type=int, default=8)
+    ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--pp_schedule", default="1f1b")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from distributed_training_compare_jax_amd.config.schema import (OptimConfig, TrainConfig,
+                                                                     model_config_from_preset)
+    from distributed_training_compare_jax_amd.data.synthetic import get_batch_iterator
+    from distributed_training_compare_jax_amd.parallel.dist import barrier, init_distributed
+    from distributed_training_compare_jax_amd.train.engine import Engine
+
+    if "RANK" not in os.environ and args.gpus > 1:
+        raise SystemExit("multi-GPU: launch with python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
+    dinfo = init_distributed("cuda")
+    world = dinfo.world
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    mc = model_config_from_preset(args.model)
+    if args.parallel == "dp":
+        global_batch, micro, scaling = args.batch_per_gpu * world, 1, "weak"
+    elif args.parallel == "tp":
+        global_batch, micro, scaling = args.batch_per_gpu, 1, "strong"
+    else:
+        global_batch, micro, scaling = args.batch_per_gpu, max(2, min(args.batch_per_gpu, 2 * world)), "strong"
+    tc = TrainConfig(seed=0, parallel=args.parallel, batch=global_batch, steps=args.steps, log_every=10 ** 9,
+                     output_dir="/tmp/bench", pp_microbatches=micro, use_graph=not args.no_graph,
+                     pp_schedule=args.pp_schedule)
+    oc = OptimConfig(lr=3e-4, weight_decay=0.1, grad_clip=1.0)
+    eng = Engine(mc, tc, oc, dinfo)
+    data = get_batch_iterator(global_batch, mc.max_seq_len + 1, seed=0, row0=eng.row0, nrows=eng.b_local)
+
+    for _ in range(args.warmup):
+        eng.set_batch(next(data))
+        eng.run_step()
+        eng.loss_value()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    batch = next(data)
+    loss = float("nan")
+    for i in range(args.steps):
+        eng.set_batch(batch)
+        eng.run_step()
+        batch = next(data)
+        loss = eng.loss_value()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dinfo.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = 1e3 * dt / args.steps
+    tokens = global_batch * mc.max_seq_len
+    value = tokens / (ms / 1e3)
+    if dinfo.rank == 0:
+        base = BASELINE_TOKENS_PER_S.get(args.parallel) if args.model == "ref" else None
+        par = {"dp": f"dp{world}", "tp": f"tp{world}", "pp": f"pp{world}"}[args.parallel]
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": scaling,
+            "vs_baseline": round(value / base, 3) if base else None, "dtype": "bf16",
+            "data": "synthetic (FineWeb-shaped token stream, random-init weights)",
+            "config": {"model": f"{mc.name} (d{mc.d_model} L{mc.n_layers} H{mc.n_heads} F{mc.d_ff} "
+                                f"T{mc.max_seq_len} V{mc.vocab_size})",
+                       "global_batch": global_batch, "seq_len": mc.max_seq_len, "parallelism": par,
+                       "pp_microbatches": micro if args.parallel == "pp" else None,
+                       "hipgraph": eng.program.use_graph, "final_loss": round(loss, 4)},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -121,7 +121,7 @@ MODEL_PRESETS: Dict[str, Dict[str, Any]] = {
                        name="gpt2-small-124M"),
     "gpt2-medium": dict(d_model=1024, n_layers=24, n_heads=16, d_ff=4096, max_seq_len=1024, dropout=0.1,
                         name="gpt2-medium-355M"),
-    "tiny": dict(d_model=64, n_layers=2, n_heads=4, d_ff=256, max_seq_len=32, dropout=0.1, name="tiny"),
+    "tiny": dict(d_model=64, n_layers=2, n_heads=2, d_ff=256, max_seq_len=64, dropout=0.1, name="tiny"),
 }
 
 

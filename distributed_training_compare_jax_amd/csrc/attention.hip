@@ -1,0 +1,354 @@
+// Causal flash attention for gfx950 (reference: model/CausalSelfAttention.py:34-44).
+//
+// Layout: qkv [B, T, 3, H, HD] bf16 straight out of the fused QKV GEMM (row stride 3*H*HD),
+// o [B, T, H, HD] bf16 (= out_proj input), lse [B, H, T] fp32 (natural log).
+//
+// All products use v_mfma_f32_16x16x32_bf16 (K = 32 = the reference head_dim).  The trick
+// that keeps softmax in registers (cdna_hip_programming.md §3 "accumulator tile as the next
+// MFMA's operand", T10): compute the score tile TRANSPOSED so the query sits on the lane:
+//     S^T[key][q] = K · Q^T   ->  lane (g, j) holds keys 4g..4g+3 of query j
+// Two such 16-key tiles give exactly the 8 k-values (keys 4g+r and 16+4g+r) that the next
+// MFMA's B operand needs in the same permuted k order the GEMM uses, so P never leaves
+// registers; V (and Q/K/dO in backward) is read k-major from LDS with ds_read_b64_tr_b16.
+//
+// Backward = 3 kernels, no atomics (bitwise deterministic): delta = rowsum(dO*O); dK/dV with
+// one workgroup per 64-key block sweeping the queries; dQ with one workgroup per 64-query
+// block sweeping the keys.  P is recomputed from the saved LSE.
+#include "common.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+template <int HD>
+struct AttnLds {
+  static constexpr int KLD = HD + 8;   // row-read image (ds_read_b128 of 8 contiguous hd)
+  static constexpr int VLD = HD + 16;  // tr-read image (rows = keys/queries, cols = hd)
+};
+
+// A/B fragment from a row-major [row][ld] LDS tile: lane (g, i) gets row r0+i, cols c0+8g..+7
+__device__ __forceinline__ bf16x8 row_frag(const bf16* lds, int ld, int r0, int c0, int lane) {
+  return *(const bf16x8*)(lds + (r0 + (lane & 15)) * ld + c0 + 8 * (lane >> 4));
+}
+// transposed fragment: element j of lane (g, i) = tile[row k(j)][col c0+i] with
+// k(j) = r0 + 4g + j (j<4), r0 + 16 + 4g + (j-4) (j>=4)   (the permuted k order)
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* lds, int ld, int r0, int c0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const bf16* p0 = lds + (r0 + 4 * g + q) * ld + c0 + 4 * p;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0 + 16 * ld));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+__device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
+  return bf16x8{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+}
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// stage a [rows][HD] tile (rows starting at token t0) of slot `which` (0 q, 1 k, 2 v) into LDS [rows][ld]
+template <int HD, int ROWS>
+__device__ __forceinline__ void stage_tile(bf16* lds, int ld, const bf16* __restrict__ base, long tok_stride, int t0,
+                                           int T, int tid, int nthreads) {
+  constexpr int CH = ROWS * HD / 8;
+  for (int c = tid; c < CH; c += nthreads) {
+    int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
+    int t = t0 + r;
+    u32x4 v = t < T ? *(const u32x4*)(base + (long)t * tok_stride + col) : u32x4{0, 0, 0, 0};
+    *(u32x4*)(lds + r * ld + col) = v;
+  }
+}
+
+// ============================================================================ forward
+template <int HD>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+                                                       float* __restrict__ lse, int B, int T, int H, float scale) {
+  constexpr int KC = HD / 32;  // k-chunks of the QK^T product
+  constexpr int HT = HD / 16;  // 16-wide hd tiles of the output
+  using L = AttnLds<HD>;
+  __shared__ __attribute__((aligned(16))) bf16 sK[64 * L::KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sV[64 * L::VLD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int nqb = (T + 63) / 64;
+  const int qb = nqb - 1 - (int)(blockIdx.x % nqb);  // heavy (late) query blocks first
+  const int bh = blockIdx.x / nqb, b = bh / H, h = bh % H;
+  const long ts = 3L * H * HD;  // token stride
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const int q = qb * 64 + 16 * w + j;  // this lane's query row
+  bf16x8 qf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc)
+    qf[kc] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + kc * 32 + 8 * g) : bf16x8{};
+  const float c = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 acc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt <= qb; ++kt) {
+    __syncthreads();
+    stage_tile<HD, 64>(sK, L::KLD, Kb, ts, kt * 64, T, tid, 256);
+    stage_tile<HD, 64>(sV, L::VLD, Vb, ts, kt * 64, T, tid, 256);
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      s[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) s[st] = mfma(row_frag(sK, L::KLD, st * 16, kc * 32, lane), qf[kc], s[st]);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int key = kt * 64 + st * 16 + 4 * g + r;
+        float x = s[st][r] * c;
+        x = (key <= q && key < T) ? x : -INFINITY;
+        s[st][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);  // m = -inf on the first tile -> 0
+    m = mn;
+    float ls = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pv = exp2f(s[st][r] - mn);
+        s[st][r] = pv;
+        ls += pv;
+      }
+    l = l * alpha + ls;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) acc[t] *= alpha;
+    bf16x8 pf0 = pack_p(s[0], s[1]), pf1 = pack_p(s[2], s[3]);
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      acc[t] = mfma(tr_frag(sV, L::VLD, 0, t * 16, lane), pf0, acc[t]);
+      acc[t] = mfma(tr_frag(sV, L::VLD, 32, t * 16, lane), pf1, acc[t]);
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (q < T) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long)b * T + q) * H * HD + h * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+      *(bf16x4*)(orow + t * 16 + 4 * g) =
+          bf16x4{f2bf(acc[t][0] * inv), f2bf(acc[t][1] * inv), f2bf(acc[t][2] * inv), f2bf(acc[t][3] * inv)};
+    if (g == 0) lse[((long)b * H + h) * T + q] = (m + __log2f(l)) * LN2;
+  }
+}
+
+// ============================================================================ backward
+// delta[b,h,t] = sum_d dO*O
+template <int HD>
+__global__ void attn_delta_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout, float* __restrict__ delta,
+                                  int B, int T, int H) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (b, t, h)
+  if (i >= (long)B * T * H) return;
+  int h = (int)(i % H);
+  long bt = i / H;
+  int t = (int)(bt % T), b = (int)(bt / T);
+  const bf16* po = o + i * HD;
+  const bf16* pd = dout + i * HD;
+  float s = 0.f;
+#pragma unroll
+  for (int d = 0; d < HD; d += 8) {
+    bf16x8 a = *(const bf16x8*)(po + d), c = *(const bf16x8*)(pd + d);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s += (float)a[r] * (float)c[r];
+  }
+  delta[((long)b * H + h) * T + t] = s;
+}
+
+// dK, dV: workgroup = (b, h, 64-key block); wave w owns keys kb*64+16w..+15 (key on the lane).
+template <int HD>
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                            const float* __restrict__ lse, const float* __restrict__ delta,
+                                                            bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  __shared__ __attribute__((aligned(16))) bf16 sQ[32 * L::VLD];
+  __shared__ __attribute__((aligned(16))) bf16 sD[32 * L::VLD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int nkb = (T + 63) / 64;
+  const int kb = (int)(blockIdx.x % nkb);  // light first: kb 0 sweeps all queries
+  const int bh = blockIdx.x / nkb, b = bh / H, h = bh % H;
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const float* lseb = lse + ((long)b * H + h) * T;
+  const float* delb = delta + ((long)b * H + h) * T;
+  const int key = kb * 64 + 16 * w + j;
+  bf16x8 kf[KC], vf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    kf[kc] = key < T ? *(const bf16x8*)(Kb + (long)key * ts + kc * 32 + 8 * g) : bf16x8{};
+    vf[kc] = key < T ? *(const bf16x8*)(Vb + (long)key * ts + kc * 32 + 8 * g) : bf16x8{};
+  }
+  const float c = scale * LOG2E;
+  f32x4 dk[HT], dv[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) { dk[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
+
+  for (int q0 = kb * 64; q0 < T; q0 += 32) {
+    __syncthreads();
+    stage_tile<HD, 32>(sQ, L::VLD, Qb, ts, q0, T, tid, 256);
+    stage_tile<HD, 32>(sD, L::VLD, dOb, dts, q0, T, tid, 256);
+    __syncthreads();
+    f32x4 p[2], ds[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        s = mfma(row_frag(sQ, L::VLD, qt * 16, kc * 32, lane), kf[kc], s);    // S[q][key]
+        dp = mfma(row_frag(sD, L::VLD, qt * 16, kc * 32, lane), vf[kc], dp);  // dP[q][key]
+      }
+      const int qr = q0 + qt * 16 + 4 * g;  // rows of this lane's 4 registers
+      f32x4 l4 = {0.f, 0.f, 0.f, 0.f}, d4 = {0.f, 0.f, 0.f, 0.f};
+      if (qr + 4 <= T) { l4 = *(const f32x4*)(lseb + qr); d4 = *(const f32x4*)(delb + qr); }
+      else for (int r = 0; r < 4; ++r) if (qr + r < T) { l4[r] = lseb[qr + r]; d4[r] = delb[qr + r]; }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qr + r;
+        float pv = (key <= qq && qq < T && key < T) ? exp2f(s[r] * c - l4[r] * LOG2E) : 0.f;
+        p[qt][r] = pv;
+        ds[qt][r] = pv * (dp[r] - d4[r]);
+      }
+    }
+    const bf16x8 pb = pack_p(p[0], p[1]), dsb = pack_p(ds[0], ds[1]);
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      dv[t] = mfma(tr_frag(sD, L::VLD, 0, t * 16, lane), pb, dv[t]);   // dV^T[hd][key] += dO^T P
+      dk[t] = mfma(tr_frag(sQ, L::VLD, 0, t * 16, lane), dsb, dk[t]);  // dK^T[hd][key] += Q^T dS
+    }
+  }
+  if (key < T) {
+    bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
+    bf16* pv = dqkv + ((long)b * T + key) * ts + (2 * H + h) * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      *(bf16x4*)(pk + t * 16 + 4 * g) = bf16x4{f2bf(dk[t][0] * scale), f2bf(dk[t][1] * scale), f2bf(dk[t][2] * scale),
+                                               f2bf(dk[t][3] * scale)};
+      *(bf16x4*)(pv + t * 16 + 4 * g) = bf16x4{f2bf(dv[t][0]), f2bf(dv[t][1]), f2bf(dv[t][2]), f2bf(dv[t][3])};
+    }
+  }
+}
+
+// dQ: workgroup = (b, h, 64-query block); wave w owns queries qb*64+16w..+15 (query on the lane).
+template <int HD>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                                          bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  __shared__ __attribute__((aligned(16))) bf16 sK[32 * L::VLD];
+  __shared__ __attribute__((aligned(16))) bf16 sV[32 * L::VLD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int nqb = (T + 63) / 64;
+  const int qb = nqb - 1 - (int)(blockIdx.x % nqb);
+  const int bh = blockIdx.x / nqb, b = bh / H, h = bh % H;
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const int q = qb * 64 + 16 * w + j;
+  bf16x8 qf[KC], df[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    qf[kc] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + kc * 32 + 8 * g) : bf16x8{};
+    df[kc] = q < T ? *(const bf16x8*)(dOb + (long)q * dts + kc * 32 + 8 * g) : bf16x8{};
+  }
+  const float lq = q < T ? lse[((long)b * H + h) * T + q] * LOG2E : 0.f;
+  const float dq_ = q < T ? delta[((long)b * H + h) * T + q] : 0.f;
+  const float c = scale * LOG2E;
+  f32x4 acc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kend = min(T, qb * 64 + 64);
+  for (int k0 = 0; k0 < kend; k0 += 32) {
+    __syncthreads();
+    stage_tile<HD, 32>(sK, L::VLD, Kb, ts, k0, T, tid, 256);
+    stage_tile<HD, 32>(sV, L::VLD, Vb, ts, k0, T, tid, 256);
+    __syncthreads();
+    f32x4 ds[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        s = mfma(row_frag(sK, L::VLD, kt * 16, kc * 32, lane), qf[kc], s);   // S^T[key][q]
+        dp = mfma(row_frag(sV, L::VLD, kt * 16, kc * 32, lane), df[kc], dp); // dP^T[key][q]
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = k0 + kt * 16 + 4 * g + r;
+        float pv = (kk <= q && kk < T && q < T) ? exp2f(s[r] * c - lq) : 0.f;
+        ds[kt][r] = pv * (dp[r] - dq_);
+      }
+    }
+    const bf16x8 dsb = pack_p(ds[0], ds[1]);
+#pragma unroll
+    for (int t = 0; t < HT; ++t) acc[t] = mfma(tr_frag(sK, L::VLD, 0, t * 16, lane), dsb, acc[t]);  // dQ^T += K^T dS^T
+  }
+  if (q < T) {
+    bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+      *(bf16x4*)(pq + t * 16 + 4 * g) = bf16x4{f2bf(acc[t][0] * scale), f2bf(acc[t][1] * scale),
+                                               f2bf(acc[t][2] * scale), f2bf(acc[t][3] * scale)};
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int HD, long flags, float scale,
+                 hipStream_t st) {
+  int nqb = (T + 63) / 64;
+  dim3 grid(B * H * nqb);
+  if (HD == 32) hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, st, qkv, o, lse, B, T, H, scale);
+  else if (HD == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, st, qkv, o, lse, B, T, H, scale);
+  else return 4001;
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+long dtc_attn_bwd_workspace_bytes(int B, int T, int H, int HD) { return (long)B * H * T * 4; }
+
+int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* dout, bf16* dqkv, int flags, int B,
+                 int T, int H, int HD, long unused, float scale, float* ws, long ws_bytes, hipStream_t st) {
+  if (ws_bytes < dtc_attn_bwd_workspace_bytes(B, T, H, HD)) return 4002;
+  long n = (long)B * T * H;
+  int nb = (T + 63) / 64;
+  dim3 grid(B * H * nb);
+  if (HD == 32) {
+    hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<32>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
+  } else if (HD == 64) {
+    hipLaunchKernelGGL(attn_delta_kernel<64>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<64>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
+  } else {
+    return 4001;
+  }
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

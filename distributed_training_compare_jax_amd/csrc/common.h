@@ -1,0 +1,79 @@
+// Shared definitions for the gfx950 (MI355X / CDNA4) kernels of this framework.
+// Wave64 everywhere; MFMA operands are bf16x8 fragments; accumulators f32x4.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define DTC_WAVE 64
+#define DTC_LDS __attribute__((address_space(3)))
+
+// Mirror of ops/_native.py GemmArgs (keep field order and types identical).
+struct GemmArgs {
+  int layout;  // 0: C = A.B^T (nt) 1: C = A.B (nn) 2: C = A^T.B (tn)
+  int M, N, K;
+  const void* A; long lda;
+  const void* B; long ldb;
+  void* C; long ldc;
+  int c_f32;
+  int epi;
+  const float* bias;
+  const void* aux; long ldaux;
+  void* aux_out;
+  float alpha, beta;
+  const int* labels;
+  int vocab_start, n_valid;
+  float* part;
+  float* label_out;
+  void* workspace; long ws_bytes;
+  int split_k;
+};
+
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_LMHEAD = 4 };
+
+#define DTC_CHECK_LAUNCH() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// gelu (tanh approximation, jax.nn.gelu(approximate=True) = flax nn.gelu default)
+__device__ __forceinline__ float gelu_tanh_f(float u) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float t = tanhf(k0 * (u + k1 * u * u * u));
+  return 0.5f * u * (1.f + t);
+}
+__device__ __forceinline__ float gelu_tanh_grad_f(float u) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float t = tanhf(k0 * (u + k1 * u * u * u));
+  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
+}
+
+// Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5 "XCD swizzle must
+// be bijective"): blocks that the dispatcher deals to the same XCD (b % 8) get a contiguous
+// range of logical tile ids, so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int NX = 8;
+  if (nwg <= NX) return b;
+  int q = nwg / NX, r = nwg % NX;
+  int x = b % NX, i = b / NX;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}

@@ -1,0 +1,313 @@
+// Streaming kernels: embedding+dropout fwd/bwd, cross-entropy combine/backward, fused
+// clip+AdamW, global-norm reduction, casts.  All memory-bound: 16-byte vector accesses,
+// grid-stride, no host sync, stream-ordered (graph-capturable).
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- Philox4x32-10 (dropout)
+// Counter = (group lo, group hi, 0, 0) with group = global_element_index / 4; key = (seed, step).
+// Bit-identical to ops/embedding.py:philox4x32 (tested).
+__device__ __forceinline__ u32x4 philox(uint64_t group, uint32_t k0, uint32_t k1) {
+  uint32_t c0 = (uint32_t)group, c1 = (uint32_t)(group >> 32), c2 = 0, c3 = 0;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+  }
+  return u32x4{c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ uint32_t drop_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+// h[tok, d..d+3] = dropout(wte[id] + wpe[t])  — one thread per 4 channels (one Philox call)
+__global__ void embed_fwd_kernel(const int* __restrict__ ids, const float* __restrict__ wte, const float* __restrict__ wpe,
+                                 float* __restrict__ h, int B, int T, int D, float p, uint32_t seed,
+                                 const int64_t* __restrict__ step, long row0) {
+  const int D4 = D / 4;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * T * D4) return;
+  long tok = i / D4;
+  int d = (int)(i % D4) * 4;
+  int t = (int)(tok % T);
+  int id = ids[tok];
+  f32x4 v = *(const f32x4*)(wte + (long)id * D + d) + *(const f32x4*)(wpe + (long)t * D + d);
+  if (p > 0.f) {
+    long gtok = (row0 + tok / T) * T + t;
+    uint64_t grp = ((uint64_t)gtok * D + d) >> 2;
+    u32x4 u = philox(grp, seed, (uint32_t)step[0]);
+    uint32_t thr = drop_threshold(p);
+    float sc = 1.f / (1.f - p);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = u[r] >= thr ? v[r] * sc : 0.f;
+  }
+  *(f32x4*)(h + tok * D + d) = v;
+}
+
+// One thread per (t, 4 channels): loops over the batch — dwpe is a deterministic sum, dwte rows
+// get fp32 atomics (rows repeat only for repeated tokens).
+__global__ void embed_bwd_kernel(const int* __restrict__ ids, const float* __restrict__ dh, float* __restrict__ dwte,
+                                 float* __restrict__ dwpe, int B, int T, int D, float p, uint32_t seed,
+                                 const int64_t* __restrict__ step, long row0, int accumulate) {
+  const int D4 = D / 4;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)T * D4) return;
+  int t = (int)(i / D4);
+  int d = (int)(i % D4) * 4;
+  uint32_t thr = drop_threshold(p);
+  float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < B; ++b) {
+    long tok = (long)b * T + t;
+    f32x4 g = *(const f32x4*)(dh + tok * D + d);
+    if (p > 0.f) {
+      uint64_t grp = ((uint64_t)((row0 + b) * T + t) * D + d) >> 2;
+      u32x4 u = philox(grp, seed, (uint32_t)step[0]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g[r] = u[r] >= thr ? g[r] * sc : 0.f;
+    }
+    acc += g;
+    float* w = dwte + (long)ids[tok] * D + d;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) atomicAdd(w + r, g[r]);
+  }
+  float* o = dwpe + (long)t * D + d;
+  if (accumulate) acc += *(f32x4*)o;
+  *(f32x4*)o = acc;
+}
+
+// ---------------------------------------------------------------- cross-entropy
+// per row: (max, sum exp) over P partials (strided), optional lse, rowstat outputs.
+__global__ void ce_combine_rows(const float* __restrict__ part, int M, int P, long srow, long spart,
+                                float* __restrict__ lse_out, float* __restrict__ rowstat) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float mx = -INFINITY;
+  for (int p = lane; p < P; p += 64) mx = fmaxf(mx, part[(row * srow + p * spart) * 2]);
+  mx = warp_max(mx);
+  float s = 0.f;
+  for (int p = lane; p < P; p += 64) {
+    const float* q = part + (row * srow + p * spart) * 2;
+    if (q[1] > 0.f) s += q[1] * __expf(q[0] - mx);
+  }
+  s = warp_sum(s);
+  if (lane == 0) {
+    if (lse_out) lse_out[row] = mx + __logf(s);
+    if (rowstat) { rowstat[2 * row] = mx; rowstat[2 * row + 1] = s; }
+  }
+}
+
+// loss = scale * sum_m (lse[m] - label_logit[m])  (one block, fixed reduction order)
+__global__ void ce_loss_reduce(const float* __restrict__ lse, const float* __restrict__ lab, int M, float scale,
+                               float* __restrict__ loss, int accumulate) {
+  __shared__ float red[1024 / 64];
+  float s = 0.f;
+  for (int m = threadIdx.x; m < M; m += blockDim.x) s += lse[m] - lab[m];
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    loss[0] = (accumulate ? loss[0] : 0.f) + scale * t;
+  }
+}
+
+// dlogits = (exp(l - lse) - onehot) * scale, in place, 8 bf16 per thread
+__global__ void ce_bwd_kernel(bf16* __restrict__ logits, long ld, const float* __restrict__ lse,
+                              const int* __restrict__ labels, int M, int V, int vstart, int n_valid, float scale) {
+  const int V8 = V / 8;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * V8) return;
+  int m = (int)(i / V8);
+  int n = (int)(i % V8) * 8;
+  bf16x8* p = (bf16x8*)(logits + (long)m * ld + n);
+  bf16x8 v = *p;
+  const float l = lse[m];
+  const int lab = labels[m] - vstart;
+  bf16x8 o;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    int c = n + r;
+    float g = c < n_valid ? __expf((float)v[r] - l) : 0.f;
+    if (c == lab) g -= 1.f;
+    o[r] = f2bf(g * scale);
+  }
+  *p = o;
+}
+
+// ---------------------------------------------------------------- optimizer
+constexpr int SS_BLOCKS = 1024;
+
+// stage 1: per-block partial of sum_s w_s * sum x^2 over the segment table (float64 [S][3])
+__global__ void __launch_bounds__(256) sumsq_stage1(const float* __restrict__ x, const double* __restrict__ seg, int S,
+                                                    float* __restrict__ part) {
+  float acc = 0.f;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int s = 0; s < S; ++s) {
+    const long off = (long)seg[3 * s], len = (long)seg[3 * s + 1];
+    const float w = (float)seg[3 * s + 2];
+    float a = 0.f;
+    for (long i = tid; i < len; i += stride) { float v = x[off + i]; a += v * v; }
+    acc += w * a;
+  }
+  __shared__ float red[4];
+  acc = warp_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void sumsq_stage2(const float* __restrict__ part, int P, float* __restrict__ out, int64_t* __restrict__ step) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) a += part[i];
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    out[0] = (float)t;
+    if (step) step[0] += 1;
+  }
+}
+
+// clip-by-global-norm + AdamW (optax semantics), 4 elements per thread; bf16 mirror for i < n_mirror
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, bf16* __restrict__ mirror, long n, long n_mirror,
+                             const int64_t* __restrict__ step, const float* __restrict__ sumsq, float lr, float b1,
+                             float b2, float eps, float wd, float max_norm) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  const float norm = sqrtf(sumsq[0]);
+  const float clip = (max_norm > 0.f && !(norm < max_norm)) ? max_norm / norm : 1.f;
+  const float t = (float)step[0];
+  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+  f32x4 pp = *(f32x4*)(p + i), gg = *(const f32x4*)(g + i) * clip, mm = *(f32x4*)(m + i), vv = *(f32x4*)(v + i);
+  mm = b1 * mm + (1.f - b1) * gg;
+  vv = b2 * vv + (1.f - b2) * gg * gg;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float mh = mm[r] / bc1, vh = vv[r] / bc2;
+    pp[r] -= lr * (mh / (sqrtf(vh) + eps) + wd * pp[r]);
+  }
+  *(f32x4*)(p + i) = pp;
+  *(f32x4*)(m + i) = mm;
+  *(f32x4*)(v + i) = vv;
+  if (i < n_mirror) *(bf16x4*)(mirror + i) = bf16x4{f2bf(pp[0]), f2bf(pp[1]), f2bf(pp[2]), f2bf(pp[3])};
+}
+
+__global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, long n) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    f32x4 v = *(const f32x4*)(x + i);
+    *(bf16x4*)(y + i) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  } else {
+    for (long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+  }
+}
+
+__global__ void fill_kernel(float* __restrict__ x, float v, long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = v;
+}
+
+inline int blocks_for(long n, int per_block) { return (int)((n + per_block - 1) / per_block); }
+
+}  // namespace
+
+extern "C" {
+
+int dtc_version() { return 1; }
+
+int dtc_embed_fwd(const int* ids, const float* wte, const float* wpe, float* h, int B, int T, int D, int V, float p,
+                  long seed, const int64_t* step, long row0, hipStream_t st) {
+  if (D % 4) return 3001;
+  long n = (long)B * T * (D / 4);
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ids, wte, wpe, h, B, T, D, p,
+                     (uint32_t)seed, step, row0);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_embed_bwd(const int* ids, const float* dh, float* dwte, float* dwpe, int B, int T, int D, int V, float p,
+                  long seed, const int64_t* step, long row0, int accumulate, hipStream_t st) {
+  if (D % 4) return 3001;
+  if (!accumulate) {
+    hipError_t e = hipMemsetAsync(dwte, 0, (size_t)V * D * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+  }
+  long n = (long)T * (D / 4);
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ids, dh, dwte, dwpe, B, T, D, p,
+                     (uint32_t)seed, step, row0, accumulate);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_ce_combine(const float* part, int M, int P, long srow, long spart, const float* label_logit, float* lse_out,
+                   float* rowstat_out, float loss_scale, float* loss_out, int accumulate, hipStream_t st) {
+  float* lse = lse_out;
+  if (loss_out && !lse) return 3002;
+  hipLaunchKernelGGL(ce_combine_rows, dim3((M + 3) / 4), dim3(256), 0, st, part, M, P, srow, spart, lse, rowstat_out);
+  DTC_CHECK_LAUNCH();
+  if (loss_out) {
+    hipLaunchKernelGGL(ce_loss_reduce, dim3(1), dim3(1024), 0, st, lse, label_logit, M, loss_scale, loss_out, accumulate);
+    DTC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+int dtc_ce_bwd(bf16* logits, long ld, const float* lse, const int* labels, int M, int V, int vstart, int n_valid,
+               float scale, hipStream_t st) {
+  if (V % 8 || ld % 8) return 3003;
+  long n = (long)M * (V / 8);
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, logits, ld, lse, labels, M, V, vstart,
+                     n_valid, scale);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+long dtc_sumsq_workspace_bytes() { return SS_BLOCKS * 4; }
+
+int dtc_sumsq_segments(const float* x, const double* seg, int S, float* out, int64_t* step, float* ws, long ws_bytes,
+                       hipStream_t st) {
+  if (ws_bytes < SS_BLOCKS * 4) return 3004;
+  hipLaunchKernelGGL(sumsq_stage1, dim3(SS_BLOCKS), dim3(256), 0, st, x, seg, S, ws);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sumsq_stage2, dim3(1), dim3(1024), 0, st, ws, SS_BLOCKS, out, step);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_adamw(float* p, const float* g, float* m, float* v, bf16* mirror, long n, long n_mirror, const int64_t* step,
+              const float* sumsq, float lr, float b1, float b2, float eps, float wd, float max_norm, float unused,
+              hipStream_t st) {
+  if (n % 4 || n_mirror % 4) return 3005;
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks_for(n / 4, 256)), dim3(256), 0, st, p, g, m, v, mirror, n, n_mirror,
+                     step, sumsq, lr, b1, b2, eps, wd, max_norm);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_kernel, dim3(blocks_for((n + 3) / 4, 256)), dim3(256), 0, st, x, y, n);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_fill_f32(float* x, float v, long n, hipStream_t st) {
+  hipLaunchKernelGGL(fill_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, x, v, n);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

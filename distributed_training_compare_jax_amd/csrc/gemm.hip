@@ -1,0 +1,386 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues — every Dense of the GPT, fwd and bwd.
+//
+//   C[m,n] = epi( sum_k A(m,k) * B(n,k) )      fp32 accumulation
+//   layout 0 (nt): A[m*lda+k], B[n*ldb+k]        forward   y  = x W^T       (W stored [out,in])
+//   layout 1 (nn): A[m*lda+k], B[k*ldb+n]        dgrad     dX = dY W
+//   layout 2 (tn): A[k*lda+m], B[k*ldb+n]        wgrad     dW = dY^T X
+//
+// CDNA4 design (see cdna_hip_programming.md §3, §5, T10, T14):
+//  * 256 threads = 4 waves (2x2); each wave owns a (BM/2)x(BN/2) sub-tile of 16x16 MFMA tiles
+//    (v_mfma_f32_16x16x32_bf16: measured ~1.15x the FLOP/s of 32x32x16 on random data).
+//  * The MFMA's A operand is the GEMM's B side and vice versa, so the accumulator puts the
+//    GEMM's m on the lane (lane&15) and 4 CONSECUTIVE n in a lane's 4 registers: epilogue
+//    stores are 8-byte (bf16x4) / 16-byte (f32x4) vectors, bias is one float4.
+//  * Register-staged, double-buffered LDS (T14: issue the global loads of tile k+1 before the
+//    MFMAs of tile k, write LDS after them, one barrier per k-tile).
+//  * K-contiguous operands: LDS rows padded to BK+8 (144 B rows) and read with two
+//    ds_read_b64 per fragment (conflict-free: 144/4 = 36 spreads the 16 rows over all banks).
+//  * M/N-contiguous operands (dgrad's W, wgrad's dY and X): stored k-major in LDS
+//    ([BK][R+16], 288 B rows) and read with ds_read_b64_tr_b16, the gfx950 hardware
+//    transpose read — no transposed copies of any tensor exist anywhere.
+//  * Both operands use the same permuted k order inside an MFMA (element j of lane group g
+//    holds k = 4g+j for j<4, 16+4g+(j-4) for j>=4), which makes both read kinds conflict-free.
+//  * XCD-aware block remap (each XCD gets a contiguous run of tiles; M-tiles fastest so the
+//    blocks sharing a weight panel share an L2).
+//  * Split-K (fp32 slabs + deterministic reduce) for the small wgrad grids.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+template <int R, int BK, bool KMAJ>
+struct Tile {
+  static constexpr int LD = KMAJ ? (BK + 8) : (R + 16);  // LDS row length (elements)
+  static constexpr int ROWS = KMAJ ? R : BK;
+  static constexpr int ELEMS = ROWS * LD;
+  static constexpr int CHUNKS = R * BK / 8;  // 16-byte chunks in the tile
+  static constexpr int PER_THREAD = CHUNKS / NT;
+  static_assert(CHUNKS % NT == 0, "tile too small for 256 threads");
+
+  // global -> registers.  rows: extent of the R dimension (M or N); r0/k0 tile origin.
+  __device__ __forceinline__ static void load(u32x4 (&reg)[PER_THREAD], const bf16* __restrict__ g, long ld,
+                                              int r0, int k0, int rows, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i) {
+      int c = tid + i * NT;
+      if (KMAJ) {
+        int row = c / (BK / 8), col = (c % (BK / 8)) * 8;
+        int gr = r0 + row;
+        reg[i] = gr < rows ? *(const u32x4*)(g + (long)gr * ld + k0 + col) : u32x4{0, 0, 0, 0};
+      } else {
+        int krow = c / (R / 8), col = (c % (R / 8)) * 8;
+        int gc = r0 + col;
+        reg[i] = gc < rows ? *(const u32x4*)(g + (long)(k0 + krow) * ld + gc) : u32x4{0, 0, 0, 0};
+      }
+    }
+  }
+  __device__ __forceinline__ static void store(const u32x4 (&reg)[PER_THREAD], bf16* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i) {
+      int c = tid + i * NT;
+      if (KMAJ) {
+        int row = c / (BK / 8), col = (c % (BK / 8)) * 8;
+        *(u32x4*)(lds + row * LD + col) = reg[i];
+      } else {
+        int krow = c / (R / 8), col = (c % (R / 8)) * 8;
+        *(u32x4*)(lds + krow * LD + col) = reg[i];
+      }
+    }
+  }
+  // MFMA fragment of 16-row tile t at k-chunk kk (32 k) in the permuted k order.
+  __device__ __forceinline__ static bf16x8 frag(const bf16* lds, int t, int kk, int lane) {
+    const int g = lane >> 4;
+    if (KMAJ) {
+      const bf16* p = lds + (t * 16 + (lane & 15)) * LD + kk * 32 + 4 * g;
+      bf16x4 lo = *(const bf16x4*)p;
+      bf16x4 hi = *(const bf16x4*)(p + 16);
+      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    } else {
+      const int li = lane & 15, q = li >> 2, pp = li & 3;
+      const bf16* p0 = lds + (kk * 32 + 4 * g + q) * LD + t * 16 + 4 * pp;
+      const bf16* p1 = p0 + 16 * LD;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p1));
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+  }
+};
+
+struct Epi {
+  int M, N;
+  void* C; long ldc;
+  const float* bias;
+  const void* aux; long ldaux;
+  void* aux_out;
+  float alpha, beta;
+  const int* labels; int vocab_start, n_valid;
+  float* part; int nparts;
+  float* label_out;
+};
+
+template <int EPI, bool OUTF32>
+__device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4 v) {
+  const bool full = (n + 4 <= e.N);
+  float b[4] = {0.f, 0.f, 0.f, 0.f};
+  if (e.bias) {
+    if (full) { f32x4 bb = *(const f32x4*)(e.bias + n); b[0] = bb[0]; b[1] = bb[1]; b[2] = bb[2]; b[3] = bb[3]; }
+    else { for (int r = 0; r < 4; ++r) if (n + r < e.N) b[r] = e.bias[n + r]; }
+  }
+  float o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = e.alpha * v[r] + b[r];
+  if (EPI == EPI_RESID) {
+    const float* res = (const float*)e.aux + (long)m * e.ldaux + n;
+    if (full) { f32x4 rr = *(const f32x4*)res; for (int r = 0; r < 4; ++r) o[r] += rr[r]; }
+    else { for (int r = 0; r < 4; ++r) if (n + r < e.N) o[r] += res[r]; }
+  }
+  if (EPI == EPI_DGELU) {
+    const bf16* u = (const bf16*)e.aux + (long)m * e.ldaux + n;
+    if (full) { bf16x4 uu = *(const bf16x4*)u; for (int r = 0; r < 4; ++r) o[r] *= gelu_tanh_grad_f((float)uu[r]); }
+    else { for (int r = 0; r < 4; ++r) if (n + r < e.N) o[r] *= gelu_tanh_grad_f((float)u[r]); }
+  }
+  if (EPI == EPI_STORE && OUTF32 && e.beta != 0.f) {
+    const float* c = (const float*)e.C + (long)m * e.ldc + n;
+    for (int r = 0; r < 4; ++r) if (n + r < e.N) o[r] += e.beta * c[r];
+  }
+  if (OUTF32) {
+    float* c = (float*)e.C + (long)m * e.ldc + n;
+    if (full) *(f32x4*)c = f32x4{o[0], o[1], o[2], o[3]};
+    else for (int r = 0; r < 4; ++r) if (n + r < e.N) c[r] = o[r];
+  } else {
+    bf16* c = (bf16*)e.C + (long)m * e.ldc + n;
+    bf16x4 ob = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+    if (full) *(bf16x4*)c = ob;
+    else for (int r = 0; r < 4; ++r) if (n + r < e.N) c[r] = ob[r];
+    if (EPI == EPI_GELU) {
+      bf16* g = (bf16*)e.aux_out + (long)m * e.ldc + n;
+      bf16x4 gb = {f2bf(gelu_tanh_f(o[0])), f2bf(gelu_tanh_f(o[1])), f2bf(gelu_tanh_f(o[2])), f2bf(gelu_tanh_f(o[3]))};
+      if (full) *(bf16x4*)g = gb;
+      else for (int r = 0; r < 4; ++r) if (n + r < e.N) g[r] = gb[r];
+    }
+  }
+}
+
+template <int BM, int BN, int BK, bool AK, bool BKM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(NT, 2)
+gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+            int tiles_m, int tiles_n, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+  using TA = Tile<BM, BK, AK>;
+  using TB = Tile<BN, BK, BKM>;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (TA::ELEMS + TB::ELEMS)];
+  constexpr int BUF = TA::ELEMS + TB::ELEMS;  // one stage: A tile then B tile
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, ntiles * split);
+  const int tile = lid % ntiles, z = lid / ntiles;
+  const int m0 = (tile % tiles_m) * BM, n0 = (tile / tiles_m) * BN;
+  const int kbeg = z * k_per_split;
+  const int nk = k_per_split / BK;
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[TA::PER_THREAD], rb[TB::PER_THREAD];
+  TA::load(ra, A, lda, m0, kbeg, M, tid);
+  TB::load(rb, B, ldb, n0, kbeg, N, tid);
+  TA::store(ra, smem, tid);
+  TB::store(rb, smem + TA::ELEMS, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    const bf16* sAc = smem + cur * BUF;
+    const bf16* sBc = sAc + TA::ELEMS;
+    if (more) {
+      TA::load(ra, A, lda, m0, kbeg + (kt + 1) * BK, M, tid);
+      TB::load(rb, B, ldb, n0, kbeg + (kt + 1) * BK, N, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = TA::frag(sAc, wm * TM + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = TB::frag(sBc, wn * TN + i, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      TA::store(ra, smem + (cur ^ 1) * BUF, tid);
+      TB::store(rb, smem + (cur ^ 1) * BUF + TA::ELEMS, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + r]
+  const int g4 = 4 * (lane >> 4);
+  if (split > 1) {
+    float* s = slab + (long)z * M * N;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        int m = m0 + wm * WM + j * 16 + (lane & 15);
+        int n = n0 + wn * WN + i * 16 + g4;
+        if (m < M) {
+          float* c = s + (long)m * N + n;
+          if (n + 4 <= N) *(f32x4*)c = acc[i][j];
+          else for (int r = 0; r < 4; ++r) if (n + r < N) c[r] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if (EPI == EPI_LMHEAD) {
+    // logits (bf16) + per-row partial (max, sum exp) over this wave's WN columns + label logit.
+    const int part_idx = (tile / tiles_m) * 2 + wn;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + (lane & 15);
+      const bool mvalid = m < M;
+      const int lab = mvalid ? e.labels[m] - e.vocab_start : -1;
+      float v[TN][4];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + g4;
+        f32x4 bb = (n + 4 <= e.N) ? *(const f32x4*)(e.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = (float)f2bf(acc[i][j][r] + bb[r]);
+          bool ok = (n + r) < e.n_valid && (n + r) < e.N;
+          v[i][r] = ok ? x : -INFINITY;
+          mx = fmaxf(mx, v[i][r]);
+        }
+        if (mvalid && n + 4 <= e.N) {
+          bf16x4 ob = {f2bf(v[i][0]), f2bf(v[i][1]), f2bf(v[i][2]), f2bf(v[i][3])};
+          *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
+        }
+        if (lab >= n && lab < n + 4 && lab < e.n_valid) e.label_out[m] = v[i][lab - n];
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float s = 0.f;
+      if (mx != -INFINITY) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s += __expf(v[i][r] - mx);
+      }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (mvalid && lane < 16) *(f32x2*)(e.part + ((long)m * e.nparts + part_idx) * 2) = f32x2{mx, s};
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      int m = m0 + wm * WM + j * 16 + (lane & 15);
+      int n = n0 + wn * WN + i * 16 + g4;
+      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+    }
+}
+
+// C = beta*C + sum_z slab[z]   (fp32, deterministic order)
+__global__ void splitk_reduce(const float* __restrict__ slab, int split, long MN, float* __restrict__ C, long ldc,
+                              int N, float beta) {
+  long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= MN) return;
+  long m = i4 / N;
+  int n = (int)(i4 % N);
+  f32x4 s = *(const f32x4*)(slab + i4);
+  for (int z = 1; z < split; ++z) {
+    f32x4 t = *(const f32x4*)(slab + z * MN + i4);
+    s += t;
+  }
+  float* c = C + m * ldc + n;
+  if (beta != 0.f) {
+    f32x4 old = *(const f32x4*)c;
+    s += beta * old;
+  }
+  *(f32x4*)c = s;
+}
+
+struct Plan {
+  int bm, bn, bk, split;
+};
+
+Plan make_plan(int M, int N, int K, bool allow_split) {
+  Plan p{128, 128, 64, 1};
+  long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  if (t128 < 256) {
+    p.bm = p.bn = 64;
+    long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
+    if (allow_split) {
+      while (t64 * p.split < 512 && K % (p.split * 2 * p.bk) == 0 && K / (p.split * 2) >= 256) p.split *= 2;
+    }
+  }
+  return p;
+}
+
+template <int BM, int BN, bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
+  Epi e;
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
+  e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
+  int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  e.nparts = tiles_n * 2;
+  int kps = a.K / p.split;
+  dim3 grid(tiles_m * tiles_n * p.split);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st,
+                     (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, p.split, kps,
+                     (float*)a.workspace, e);
+  DTC_CHECK_LAUNCH();
+  if (p.split > 1) {
+    long MN = (long)a.M * a.N;
+    int blocks = (int)((MN / 4 + 255) / 256);
+    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, p.split, MN,
+                       (float*)a.C, a.ldc, a.N, a.beta);
+    DTC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_sz(const GemmArgs& a, const Plan& p, hipStream_t st) {
+  if (p.bm == 128) return launch_t<128, 128, AK, BKM, EPI, OUTF32>(a, p, st);
+  return launch_t<64, 64, AK, BKM, EPI, OUTF32>(a, p, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dtc_lmhead_nparts(int N) { return ((N + 127) / 128) * 2; }
+
+long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
+  Plan p = make_plan(M, N, K, layout == 2);
+  return p.split > 1 ? (long)p.split * M * N * 4 : 0;
+}
+
+int dtc_gemm(const GemmArgs* a, hipStream_t st) {
+  if (a->K % 64 != 0) return 1001;               // K must be a multiple of BK=64
+  if (a->lda % 8 || a->ldb % 8 || a->ldc % 4) return 1002;  // 16-B row alignment
+  if (a->M <= 0 || a->N <= 0) return 0;
+  const int epi = a->epi;
+  const bool f32 = a->c_f32 != 0;
+  if (a->layout == 0) {
+    Plan p = make_plan(a->M, a->N, a->K, false);
+    if (epi == EPI_LMHEAD) { p.bm = p.bn = 128; return launch_t<128, 128, true, true, EPI_LMHEAD, false>(*a, p, st); }
+    if (epi == EPI_GELU) return launch_sz<true, true, EPI_GELU, false>(*a, p, st);
+    if (epi == EPI_RESID) return launch_sz<true, true, EPI_RESID, true>(*a, p, st);
+    if (epi == EPI_STORE) return f32 ? launch_sz<true, true, EPI_STORE, true>(*a, p, st)
+                                     : launch_sz<true, true, EPI_STORE, false>(*a, p, st);
+    return 1003;
+  }
+  if (a->layout == 1) {
+    if (a->N % 8) return 1004;
+    Plan p = make_plan(a->M, a->N, a->K, false);
+    if (epi == EPI_DGELU) return launch_sz<true, false, EPI_DGELU, false>(*a, p, st);
+    if (epi == EPI_STORE) return f32 ? launch_sz<true, false, EPI_STORE, true>(*a, p, st)
+                                     : launch_sz<true, false, EPI_STORE, false>(*a, p, st);
+    return 1003;
+  }
+  if (a->layout == 2) {
+    if (a->M % 8 || a->N % 8) return 1004;
+    if (epi != EPI_STORE || !f32 || a->bias) return 1003;
+    Plan p = make_plan(a->M, a->N, a->K, true);
+    if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;
+    return launch_sz<false, false, EPI_STORE, true>(*a, p, st);
+  }
+  return 1006;
+}
+
+}  // extern "C"

@@ -1,0 +1,229 @@
+// LayerNorm fwd/bwd and deterministic column reductions (bias grads, dgamma/dbeta).
+//
+// LayerNorm (flax nn.LayerNorm, eps 1e-6): one wave64 per row, the row held in registers as
+// float4 chunks (16-byte loads), two-pass mean/variance in fp32, output in the GEMM operand
+// dtype.  Backward fuses the residual-gradient add and writes a bf16 copy of dx for the next
+// dgrad/wgrad GEMM; dgamma/dbeta go through per-block partial slabs + an ordered reduce (no
+// float atomics -> bitwise reproducible).
+#include "common.h"
+
+namespace {
+
+template <int NV>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                     const float* __restrict__ b, void* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int M, int D, float eps, int out_f32) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int D4 = D / 4;
+  const f32x4* xr = (const f32x4*)(x + (long)row * D);
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    int c = lane + 64 * i;
+    v[i] = c < D4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mean = warp_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    int c = lane + 64 * i;
+    if (c < D4) {
+      f32x4 d = v[i] - mean;
+      q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+  }
+  const float rstd = rsqrtf(warp_sum(q) / D + eps);
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    int c = lane + 64 * i;
+    if (c < D4) {
+      f32x4 gg = ((const f32x4*)g)[c], bb = ((const f32x4*)b)[c];
+      f32x4 o = (v[i] - mean) * rstd * gg + bb;
+      if (out_f32) ((f32x4*)((float*)y + (long)row * D))[c] = o;
+      else ((bf16x4*)((bf16*)y + (long)row * D))[c] = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+    }
+  }
+}
+
+constexpr int LN_BWD_ROWS = 16;  // rows per block (4 waves x 4 rows)
+
+template <int NV>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy, int dy_f32, const float* __restrict__ x,
+                                                     const float* __restrict__ g, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const float* __restrict__ dres,
+                                                     float* __restrict__ dx, bf16* __restrict__ dx_c,
+                                                     float* __restrict__ part, int M, int D) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int D4 = D / 4;
+  f32x4 ag[NV], ab[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) { ag[i] = f32x4{0.f, 0.f, 0.f, 0.f}; ab[i] = ag[i]; }
+  for (int rr = wave; rr < LN_BWD_ROWS; rr += 4) {
+    const int row = blockIdx.x * LN_BWD_ROWS + rr;
+    if (row >= M) break;
+    const float mu = mean[row], rs = rstd[row];
+    f32x4 xh[NV], d[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int c = lane + 64 * i;
+      if (c < D4) {
+        f32x4 xv = ((const f32x4*)(x + (long)row * D))[c];
+        f32x4 dv;
+        if (dy_f32) dv = ((const f32x4*)((const float*)dy + (long)row * D))[c];
+        else { bf16x4 t = ((const bf16x4*)((const bf16*)dy + (long)row * D))[c]; dv = f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]}; }
+        xh[i] = (xv - mu) * rs;
+        d[i] = dv;
+        f32x4 gd = dv * ((const f32x4*)g)[c];
+        s1 += gd[0] + gd[1] + gd[2] + gd[3];
+        f32x4 t2 = gd * xh[i];
+        s2 += t2[0] + t2[1] + t2[2] + t2[3];
+        ag[i] += dv * xh[i];
+        ab[i] += dv;
+      }
+    }
+    const float c1 = warp_sum(s1) / D, c2 = warp_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int c = lane + 64 * i;
+      if (c < D4) {
+        f32x4 gd = d[i] * ((const f32x4*)g)[c];
+        f32x4 o = (gd - c1 - xh[i] * c2) * rs;
+        if (dres) o += ((const f32x4*)(dres + (long)row * D))[c];
+        ((f32x4*)(dx + (long)row * D))[c] = o;
+        if (dx_c) ((bf16x4*)(dx_c + (long)row * D))[c] = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+      }
+    }
+  }
+  // block reduce of the dgamma/dbeta partials over the 4 waves (fixed order)
+  __shared__ __attribute__((aligned(16))) float red[4][2][1024];
+  float* mine = &red[wave][0][0];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    int c = lane + 64 * i;
+    if (c < D4 && c < 256) { ((f32x4*)mine)[c] = ag[i]; ((f32x4*)(mine + 1024))[c] = ab[i]; }
+  }
+  __syncthreads();
+  // partial layout: part[block][2][D]
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float sg = 0.f, sb = 0.f;
+    if (c < 1024) {
+      for (int w = 0; w < 4; ++w) { sg += red[w][0][c]; sb += red[w][1][c]; }
+    }
+    part[((long)blockIdx.x * 2 + 0) * D + c] = sg;
+    part[((long)blockIdx.x * 2 + 1) * D + c] = sb;
+  }
+}
+
+// out[c] (+)= sum_p part[p*stride + c]   for the two slabs of ln bwd (dgamma, dbeta)
+__global__ void slab_reduce2(const float* __restrict__ part, int P, int D, float* __restrict__ o0,
+                             float* __restrict__ o1, int accumulate) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * D) return;
+  int which = c / D, col = c % D;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[((long)p * 2 + which) * D + col];
+  float* o = which ? o1 : o0;
+  o[col] = accumulate ? o[col] + s : s;
+}
+
+constexpr int CS_ROWS = 64;
+
+// stage 1: part[slab][n] = sum over rows of the slab (4 columns per thread, vector loads)
+__global__ void __launch_bounds__(256) colsum_stage1(const void* __restrict__ dy, int is_f32, int M, int N, long ld,
+                                                     float* __restrict__ part) {
+  const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int r0 = blockIdx.y * CS_ROWS;
+  if (n >= N) return;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  const int r1 = min(M, r0 + CS_ROWS);
+  if (n + 4 <= N) {
+    for (int r = r0; r < r1; ++r) {
+      if (is_f32) s += *(const f32x4*)((const float*)dy + (long)r * ld + n);
+      else { bf16x4 t = *(const bf16x4*)((const bf16*)dy + (long)r * ld + n); s += f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]}; }
+    }
+    *(f32x4*)(part + (long)blockIdx.y * N + n) = s;
+  } else {
+    for (int j = 0; j < 4 && n + j < N; ++j) {
+      float a = 0.f;
+      for (int r = r0; r < r1; ++r) a += is_f32 ? ((const float*)dy)[(long)r * ld + n + j] : (float)((const bf16*)dy)[(long)r * ld + n + j];
+      part[(long)blockIdx.y * N + n + j] = a;
+    }
+  }
+}
+
+__global__ void colsum_stage2(const float* __restrict__ part, int P, int N, float* __restrict__ out, float beta) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(long)p * N + n];
+  out[n] = beta != 0.f ? beta * out[n] + s : s;
+}
+
+}  // namespace
+
+#define DTC_NV_SWITCH(NV_, ...)                                              \
+  switch (NV_) {                                                             \
+    case 1: { constexpr int NVC = 1; __VA_ARGS__; } break;                   \
+    case 2: { constexpr int NVC = 2; __VA_ARGS__; } break;                   \
+    case 3: { constexpr int NVC = 3; __VA_ARGS__; } break;                   \
+    case 4: { constexpr int NVC = 4; __VA_ARGS__; } break;                   \
+    case 5: case 6: { constexpr int NVC = 6; __VA_ARGS__; } break;           \
+    case 7: case 8: { constexpr int NVC = 8; __VA_ARGS__; } break;           \
+    default: return 2001;                                                    \
+  }
+
+extern "C" {
+
+int dtc_layernorm_fwd(const float* x, const float* g, const float* b, void* y, float* mean, float* rstd, int M, int D,
+                      float eps, int out_f32, hipStream_t st) {
+  if (D % 4) return 2002;
+  int nv = (D / 4 + 63) / 64;
+  dim3 grid((M + 3) / 4);
+  DTC_NV_SWITCH(nv, hipLaunchKernelGGL(ln_fwd_kernel<NVC>, grid, dim3(256), 0, st, x, g, b, y, mean, rstd, M, D, eps, out_f32));
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+long dtc_layernorm_bwd_workspace_bytes(int M, int D) {
+  long blocks = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  return blocks * 2 * D * 4;
+}
+
+int dtc_layernorm_bwd(const void* dy, int dy_f32, const float* x, const float* g, const float* mean, const float* rstd,
+                      const float* dres, float* dx, bf16* dx_c, float* dg, float* db, int M, int D, int accumulate,
+                      float* ws, long ws_bytes, hipStream_t st) {
+  if (D % 4 || D > 1024) return 2002;  // dgamma/dbeta block reduce holds D <= 1024 in LDS
+  int blocks = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  if (ws_bytes < dtc_layernorm_bwd_workspace_bytes(M, D)) return 2003;
+  int nv = (D / 4 + 63) / 64;
+  DTC_NV_SWITCH(nv, hipLaunchKernelGGL(ln_bwd_kernel<NVC>, dim3(blocks), dim3(256), 0, st, dy, dy_f32, x, g, mean, rstd,
+                                       dres, dx, dx_c, ws, M, D));
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(slab_reduce2, dim3((2 * D + 255) / 256), dim3(256), 0, st, ws, blocks, D, dg, db, accumulate);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+long dtc_colsum_workspace_bytes(int M, int N) { return (long)((M + CS_ROWS - 1) / CS_ROWS) * N * 4; }
+
+int dtc_colsum(const void* dy, int is_f32, int M, int N, long ld, float* out, float beta, float* ws, long ws_bytes,
+               hipStream_t st) {
+  int P = (M + CS_ROWS - 1) / CS_ROWS;
+  if (ws_bytes < dtc_colsum_workspace_bytes(M, N)) return 2004;
+  if (ld % 4) return 2005;
+  dim3 g1((N / 4 + 255) / 256 + 1, P);
+  hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, st, dy, is_f32, M, N, ld, ws);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_stage2, dim3((N + 255) / 256), dim3(256), 0, st, ws, P, N, out, beta);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -74,10 +74,10 @@ class StepProgram:
 
     # -------------------------------------------------------------- capture / replay
     def _begin(self):
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
-        if self._pool is None:
-            self._pool = g.pool()
         self._graph = g
 
     def _cut(self):
@@ -97,6 +97,16 @@ class StepProgram:
                 self._begin()
                 out = step_fn()
                 self._cut()
+        except BaseException:
+            # never leave the stream in capture mode (the process would abort at teardown)
+            if self._graph is not None:
+                try:
+                    self._graph.capture_end()
+                except Exception:
+                    pass
+                self._graph = None
+            self.items = []
+            raise
         finally:
             self.recording = False
         cur.wait_stream(self._stream)

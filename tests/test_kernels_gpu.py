@@ -1,0 +1,195 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (GPU).
+
+Inputs are bf16-rounded first, so the reference sees exactly the kernel's operands and the
+only difference is accumulation order / fp32 vs bf16 output rounding.  Operands are
+asymmetric random data (cdna_hip_programming.md §3: a symmetric operand hides transposes).
+"""
+
+import math
+
+import pytest
+import torch
+
+from distributed_training_compare_jax_amd.ops import attention as A
+from distributed_training_compare_jax_amd.ops import embedding as E
+from distributed_training_compare_jax_amd.ops import gemm as G
+from distributed_training_compare_jax_amd.ops import layernorm as LN
+from distributed_training_compare_jax_amd.ops import optim as O
+from distributed_training_compare_jax_amd.ops import xent as X
+
+pytestmark = pytest.mark.gpu
+
+
+def _r(*shape, scale=1.0, dev="cuda", seed=0, dtype=torch.bfloat16):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    t = (torch.randn(*shape, generator=g) * scale + 0.1 * torch.rand(*shape, generator=g))
+    return t.to(dev).to(dtype)
+
+
+def _close(a, b, rtol, name=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item() + 1e-6
+    assert err <= rtol * ref, f"{name}: max abs err {err:.3e} vs ref max {ref:.3e} (rel {err / ref:.2e})"
+
+
+GEMM_SHAPES = [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048), (256, 384, 128),
+               (200, 136, 64), (4096, 50304, 512)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+def test_gemm_nt_bias(cuda, M, N, K):
+    x, w = _r(M, K, seed=1), _r(N, K, scale=0.05, seed=2)
+    b = _r(N, dtype=torch.float32, seed=3)
+    y = G.linear(x, w, b)
+    ref = x.float() @ w.float().t() + b
+    _close(y, ref, 1e-2, "nt")
+
+
+def test_gemm_resid_gelu(cuda):
+    M, N, K = 512, 768, 256
+    x, w = _r(M, K, seed=1), _r(N, K, scale=0.05, seed=2)
+    b = _r(N, dtype=torch.float32, seed=3)
+    res = _r(M, N, dtype=torch.float32, seed=4)
+    y = G.linear_resid(x, w, b, res)
+    _close(y, res + x.float() @ w.float().t() + b, 2e-3, "resid")
+    y2 = G.linear_resid(x, w, None, None)
+    _close(y2, x.float() @ w.float().t(), 2e-3, "store_f32")
+    u, g = G.linear_gelu(x, w, b)
+    uref = x.float() @ w.float().t() + b
+    _close(u, uref, 1e-2, "gelu_u")
+    _close(g, G.gelu_tanh(uref), 1e-2, "gelu_g")
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 512, 1536), (4096, 2048, 512), (4096, 512, 50304), (256, 128, 64)])
+def test_gemm_nn(cuda, M, N, K):
+    dy, w = _r(M, K, seed=5), _r(K, N, scale=0.05, seed=6)
+    dx = G.matmul_nn(dy, w)
+    _close(dx, dy.float() @ w.float(), 2e-3, "nn")
+    u = _r(M, N, seed=7)
+    du = G.matmul_nn_dgelu(dy, w, u)
+    _close(du, (dy.float() @ w.float()) * G.gelu_tanh_grad(u.float()), 1e-2, "dgelu")
+
+
+@pytest.mark.parametrize("Mtok,N,K", [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048),
+                                      (4096, 50304, 512), (128, 64, 64), (512, 200, 96)])
+def test_gemm_wgrad(cuda, Mtok, N, K):
+    dy, x = _r(Mtok, N, seed=8), _r(Mtok, K, seed=9)
+    dw = torch.full((N, K), 3.0, device=cuda)
+    G.wgrad(dy, x, dw, beta=0.0)
+    ref = dy.float().t() @ x.float()
+    _close(dw, ref, 2e-3, "wgrad")
+    G.wgrad(dy, x, dw, beta=1.0)
+    _close(dw, 2 * ref, 2e-3, "wgrad_acc")
+
+
+def test_colsum(cuda):
+    dy = _r(4096, 1536, seed=10)
+    db = torch.zeros(1536, device=cuda)
+    G.colsum(dy, db)
+    _close(db, dy.float().sum(0), 1e-4, "colsum")
+    G.colsum(dy, db, beta=1.0)
+    _close(db, 2 * dy.float().sum(0), 1e-4, "colsum_acc")
+    d32 = _r(1000, 520, dtype=torch.float32, seed=11)
+    db2 = torch.zeros(520, device=cuda)
+    G.colsum(d32, db2)
+    _close(db2, d32.sum(0), 1e-5, "colsum_f32")
+
+
+@pytest.mark.parametrize("D", [512, 768, 64])
+def test_layernorm(cuda, D):
+    M = 1024
+    x = _r(M, D, dtype=torch.float32, seed=12) * 3 + 1
+    g = _r(D, dtype=torch.float32, seed=13)
+    b = _r(D, dtype=torch.float32, seed=14)
+    y, mu, rs = LN.layernorm_fwd(x, g, b, 1e-6, torch.bfloat16)
+    yc, muc, rsc = LN.layernorm_fwd(x.cpu(), g.cpu(), b.cpu(), 1e-6, torch.float32)
+    _close(y.cpu(), yc, 1e-2, "ln_fwd")
+    _close(rs.cpu(), rsc, 1e-5, "ln_rstd")
+    dy = _r(M, D, seed=15)
+    dres = _r(M, D, dtype=torch.float32, seed=16)
+    dg, db = torch.zeros(D, device=cuda), torch.zeros(D, device=cuda)
+    dxc = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
+    dx = LN.layernorm_bwd(dy, x, g, mu, rs, dres, dg, db, 0.0, out_c=dxc)
+    dgc, dbc = torch.zeros(D), torch.zeros(D)
+    dxr = LN.layernorm_bwd(dy.cpu().float(), x.cpu(), g.cpu(), muc, rsc, dres.cpu(), dgc, dbc, 0.0)
+    _close(dx.cpu(), dxr, 1e-4, "ln_dx")
+    _close(dxc.cpu(), dxr, 1e-2, "ln_dx_bf16")
+    _close(dg.cpu(), dgc, 1e-4, "ln_dg")
+    _close(db.cpu(), dbc, 1e-4, "ln_db")
+
+
+def test_embedding_dropout_bits(cuda):
+    B, T, D, V = 4, 64, 128, 1000
+    ids = torch.randint(0, V, (B, T), dtype=torch.int32)
+    wte = _r(V, D, dtype=torch.float32, seed=17)
+    wpe = _r(T, D, dtype=torch.float32, seed=18)
+    step = torch.tensor([7], dtype=torch.int64)
+    h = E.embed_fwd(ids.to(cuda), wte, wpe, 0.1, 1234, step.to(cuda), row0=3)
+    hc = E.embed_fwd(ids, wte.cpu(), wpe.cpu(), 0.1, 1234, step, row0=3)
+    assert torch.equal((h.cpu() == 0), (hc == 0)), "dropout mask differs between HIP Philox and CPU Philox"
+    _close(h.cpu(), hc, 1e-6, "embed_fwd")
+    dh = _r(B * T, D, dtype=torch.float32, seed=19)
+    dwte, dwpe = torch.full((V, D), 5.0, device=cuda), torch.zeros(T, D, device=cuda)
+    E.embed_bwd(ids.to(cuda), dh, dwte, dwpe, 0.1, 1234, step.to(cuda), 3, 0.0)
+    dwc, dpc = torch.zeros(V, D), torch.zeros(T, D)
+    E.embed_bwd(ids, dh.cpu(), dwc, dpc, 0.1, 1234, step, 3, 0.0)
+    _close(dwte.cpu(), dwc, 1e-5, "dwte")
+    _close(dwpe.cpu(), dpc, 1e-5, "dwpe")
+
+
+@pytest.mark.parametrize("B,T,H,hd", [(2, 512, 4, 32), (1, 256, 2, 64), (2, 128, 3, 32)])
+def test_attention(cuda, B, T, H, hd):
+    qkv = _r(B, T, 3 * H * hd, seed=20)
+    o, lse = A.attn_fwd(qkv, H)
+    oc, lsec = A.attn_fwd(qkv.cpu().float(), H)
+    _close(o.cpu(), oc, 2e-2, "attn_o")
+    _close(lse.cpu(), lsec, 1e-3, "attn_lse")
+    do = _r(B, T, H * hd, seed=21)
+    dqkv = A.attn_bwd(qkv, o, lse, do, H)
+    dref = A.attn_bwd(qkv.cpu().float(), o.cpu().float(), lse.cpu(), do.cpu().float(), H)
+    d3, r3 = dqkv.cpu().float().view(B, T, 3, -1), dref.view(B, T, 3, -1)
+    for i, n in enumerate("qkv"):
+        _close(d3[:, :, i], r3[:, :, i], 3e-2, f"attn_d{n}")
+
+
+def test_lmhead_ce(cuda):
+    M, D, V, Vp = 512, 128, 1000, 1024
+    h = _r(M, D, seed=22)
+    w = _r(Vp, D, scale=0.2, seed=23)
+    b = _r(Vp, dtype=torch.float32, seed=24)
+    labels = torch.randint(0, V, (M,), dtype=torch.int32)
+    logits, rowstat, lab = X.lmhead_logits_partials(h, w, b, labels.to(cuda), 0, V)
+    lse, loss = X.ce_finalize(rowstat.unsqueeze(0).contiguous(), lab, 1.0 / M)
+    ref = torch.nn.functional.cross_entropy(h.float().cpu() @ w.float().cpu()[:V].t() + b.cpu()[:V], labels.long())
+    assert abs(loss.item() - ref.item()) < 2e-2 * abs(ref.item()), (loss.item(), ref.item())
+    X.ce_backward_inplace(logits, lse, labels.to(cuda), 0, V, 1.0 / M)
+    lf = h.float().cpu() @ w.float().cpu().t() + b.cpu()
+    lf[:, V:] = float("-inf")
+    p = torch.softmax(lf, -1)
+    p[torch.arange(M), labels.long()] -= 1
+    _close(logits.cpu(), p / M, 3e-2, "dlogits")
+    assert logits[:, V:].abs().max().item() == 0.0
+
+
+def test_adamw_matches_cpu(cuda):
+    n = 10_000 * 64
+    p = _r(n, dtype=torch.float32, seed=25)
+    g = _r(n, dtype=torch.float32, seed=26) * 0.01
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    mirror = torch.zeros(n, dtype=torch.bfloat16, device=cuda)
+    segs = O.make_segments([(0, n // 2, 1.0), (n // 2, n // 2, 0.5)], cuda)
+    ss, step = torch.zeros(1, device=cuda), torch.zeros(1, dtype=torch.int64, device=cuda)
+    O.sumsq_segments(g, segs, ss, step)
+    gc = g.cpu()
+    ref_ss = (gc[: n // 2].double() ** 2).sum() + 0.5 * (gc[n // 2:].double() ** 2).sum()
+    assert abs(ss.item() - ref_ss.item()) < 1e-4 * ref_ss.item()
+    assert step.item() == 1
+    pc, mc, vc = p.cpu().clone(), torch.zeros(n), torch.zeros(n)
+    for it in range(3):
+        O.adamw_flat(p, g, m, v, mirror, n, step, ss, 3e-4, 0.9, 0.999, 1e-8, 0.1, 1.0)
+        O.adamw_flat(pc, gc, mc, vc, None, 0, step.cpu(), ss.cpu(), 3e-4, 0.9, 0.999, 1e-8, 0.1, 1.0)
+        step += 1
+    _close(p.cpu(), pc, 1e-6, "adamw_p")
+    _close(mirror.cpu(), pc, 1e-2, "adamw_mirror")
+    _close(v.cpu(), vc, 1e-5, "adamw_v")

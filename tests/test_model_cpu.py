@@ -1,0 +1,165 @@
+"""CPU tests: reference semantics of the model, data, config and optimizer (no GPU)."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_training_compare_jax_amd.config.schema import (OptimConfig, TrainConfig, build_configs,
+                                                                 model_config_from_preset)
+from distributed_training_compare_jax_amd.data.synthetic import SyntheticTokenStream, get_batch_iterator, get_tokenizer
+from distributed_training_compare_jax_amd.models.gpt import GPTStage, StageLayout
+from distributed_training_compare_jax_amd.models.params import all_param_specs, init_full, shard, unshard
+from distributed_training_compare_jax_amd.models.reference import oracle_loss
+from distributed_training_compare_jax_amd.ops import embedding as E
+from distributed_training_compare_jax_amd.ops import gemm as G
+from distributed_training_compare_jax_amd.ops import optim as O
+from distributed_training_compare_jax_amd.parallel.buffers import FlatParams
+from distributed_training_compare_jax_amd.parallel.mesh import resolve_degrees, split_layers
+
+
+def test_reference_configs_load():
+    tc, mc, oc = build_configs("configs/train_config_pp.yaml", vocab_size=len(get_tokenizer()))
+    assert (mc.vocab_size, mc.d_model, mc.n_layers, mc.n_heads, mc.d_ff, mc.max_seq_len) == (50258, 512, 12, 16, 2048, 512)
+    assert mc.dropout == 0.1 and mc.parallel == "pp" and tc.pp_microbatches == 2
+    assert (oc.lr, oc.weight_decay, oc.grad_clip) == (3e-4, 0.1, 1.0)
+    assert mc.padded_vocab % 128 == 0 and mc.padded_vocab >= 50258
+    assert abs(mc.num_params() - 89.61e6) < 0.01e6  # 89.61 M params
+    for s in ("dp", "tp"):
+        tc, _, _ = build_configs(f"configs/train_config_{s}.yaml")
+        assert tc.parallel == s and tc.batch == 8 and tc.steps == 5000 and tc.log_every == 50
+
+
+def test_unknown_key_rejected(tmp_path):
+    p = tmp_path / "t.yaml"
+    p.write_text("batch: 8\nlog_every: 1\noutput_dir: x\nparallel: dp\nseed: 0\nsteps: 1\nbogus: 3\n")
+    with pytest.raises(TypeError):
+        build_configs(str(p))
+
+
+def test_strategy_resolution():
+    assert resolve_degrees("dp", 8, None, None, None) == (8, 1, 1)
+    assert resolve_degrees("tp", 8, None, None, None) == (1, 8, 1)
+    assert resolve_degrees("pp", 4, None, None, None) == (1, 1, 4)
+    assert resolve_degrees("dp", 8, None, 2, None) == (4, 2, 1)
+    with pytest.raises(ValueError):
+        resolve_degrees("zz", 2, None, None, None)
+    # reference quirk fix: 12 layers over 8 stages keeps all 12 layers
+    r = split_layers(12, 8)
+    assert sum(len(x) for x in r) == 12 and r[0].start == 0 and r[-1].stop == 12
+
+
+def test_synthetic_data_contract():
+    it = get_batch_iterator(8, 513)
+    a = next(it)
+    assert a.shape == (8, 513) and a.dtype == np.int32
+    assert a.min() >= 0 and a.max() < 50257  # pad id never appears
+    # row-sliced iterator (a DP rank) is bit-identical to slicing the global batch
+    b = next(get_batch_iterator(8, 513, row0=2, nrows=3))
+    assert np.array_equal(a[2:5], b)
+    # deterministic and non-trivial
+    assert np.array_equal(a, next(get_batch_iterator(8, 513)))
+    assert not np.array_equal(a, next(it))
+    s = SyntheticTokenStream()
+    t = s.tokens(0, 20000)
+    follow = (s.succ[t[:-1]] == t[1:]).mean()
+    # P(e_t = succ[e_{t-1}]) = p_follow * P(e_{t-1} was not itself a follow) ~ 0.25: learnable structure
+    assert 0.2 < follow < 0.35
+
+
+def test_init_statistics():
+    mc = model_config_from_preset("ref")
+    specs = {s.name: s for s in all_param_specs(mc)}
+    wte = init_full(specs["wte"], 0)
+    assert abs(wte.std().item() - 1 / math.sqrt(512)) < 1e-3
+    w = init_full(specs["h.0.fc2.w"], 0)  # fan_in 2048, truncated normal
+    sigma = math.sqrt(1 / 2048) / 0.87962566103423978
+    assert w.abs().max().item() <= 2 * sigma + 1e-6
+    assert abs(w.std().item() - math.sqrt(1 / 2048)) < 2e-4
+    lm = init_full(specs["lm_head.w"], 0)
+    assert lm[mc.vocab_size:].abs().max().item() == 0.0
+    assert init_full(specs["h.3.ln1.g"], 0).eq(1).all() and init_full(specs["h.3.qkv.b"], 0).eq(0).all()
+    # canonical init: same tensors for the same seed, different for another
+    assert torch.equal(init_full(specs["h.0.qkv.w"], 0), init_full(specs["h.0.qkv.w"], 0))
+    assert not torch.equal(init_full(specs["h.0.qkv.w"], 0), init_full(specs["h.0.qkv.w"], 1))
+
+
+@pytest.mark.parametrize("name", ["h.0.qkv.w", "h.0.qkv.b", "h.0.fc1.w", "h.0.fc2.w", "h.0.out.w", "lm_head.w"])
+def test_tp_shard_roundtrip(name):
+    mc = model_config_from_preset("tiny", vocab_size=1000)
+    spec = {s.name: s for s in all_param_specs(mc)}[name]
+    full = init_full(spec, 3)
+    if spec.init == "zeros":
+        full = torch.randn(spec.shape)
+    parts = [shard(spec, full, r, 4) for r in range(4)]
+    assert torch.equal(unshard(spec, parts), full)
+
+
+def test_gelu_is_tanh_approx():
+    x = torch.linspace(-6, 6, 101)
+    assert torch.allclose(G.gelu_tanh(x), torch.nn.functional.gelu(x, approximate="tanh"), atol=1e-6)
+    x.requires_grad_(True)
+    torch.nn.functional.gelu(x, approximate="tanh").sum().backward()
+    assert torch.allclose(G.gelu_tanh_grad(x.detach()), x.grad, atol=1e-5)
+
+
+def test_philox_known_answer_and_rate():
+    # Philox4x32-10 known-answer vector (Random123 kat: ctr=0, key=0)
+    out = E.philox4x32(0, 0, 0, 0, 0, 0)
+    assert [int(v) for v in out] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    keep = E.dropout_keep_mask(512, 512, 0, 0.1, seed=0, step=0)
+    assert abs(keep.float().mean().item() - 0.9) < 0.005
+    # layout invariance: a token slice of the global mask equals the mask of that slice
+    sub = E.dropout_keep_mask(100, 512, 37, 0.1, seed=0, step=0)
+    assert torch.equal(sub, keep[37:137])
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_explicit_backward_matches_autograd(dropout):
+    mc = model_config_from_preset("tiny", vocab_size=1000, dropout=dropout)
+    specs = all_param_specs(mc)
+    flat = FlatParams(specs, 0, 1, "cpu", compute_dtype=torch.float32)
+    flat.init_canonical(0)
+    st = GPTStage(mc, flat, StageLayout(range(mc.n_layers), True, True), act_dtype=torch.float32, dropout_seed=5)
+    b = next(get_batch_iterator(4, mc.max_seq_len + 1, vocab=999))
+    ids, lab = torch.from_numpy(b[:, :-1]).contiguous(), torch.from_numpy(b[:, 1:]).contiguous()
+    step = torch.tensor([3])
+    ctx = {}
+    T = mc.max_seq_len
+    h = st.embed_forward(ids, step, 0, ctx)
+    h = st.stage_forward(h, 4, ctx)
+    loss = st.head_forward(h, lab, 1 / (4 * T), ctx)
+    dx, dxc = st.head_backward(ctx, 1 / (4 * T), 0.0)
+    dx, dxc = st.stage_backward(ctx, dx, dxc, 0.0)
+    st.embed_backward(ctx, dx, step, 0.0)
+    params = {n: flat.p(n).clone().requires_grad_(True) for n in flat.slots}
+    lo = oracle_loss(mc, params, ids, lab, 5, 3)
+    lo.backward()
+    assert abs(loss.item() - lo.item()) < 1e-5
+    for n in flat.slots:
+        assert torch.allclose(flat.g(n), params[n].grad, rtol=1e-4, atol=1e-6), n
+    assert not ctx  # every saved activation consumed
+
+
+def test_adamw_matches_optax_semantics():
+    n = 256
+    torch.manual_seed(0)
+    p0 = torch.randn(n)
+    grads = [torch.randn(n) * s for s in (0.01, 5.0, 0.3)]  # second step triggers clipping
+    p, m, v = p0.clone(), torch.zeros(n), torch.zeros(n)
+    step, ss = torch.zeros(1, dtype=torch.int64), torch.zeros(1)
+    segs = O.make_segments([(0, n, 1.0)], "cpu")
+    rp, rm, rv = p0.clone().double(), torch.zeros(n).double(), torch.zeros(n).double()
+    for t, g in enumerate(grads, 1):
+        O.sumsq_segments(g, segs, ss, step)
+        O.adamw_flat(p, g, m, v, None, 0, step, ss, 3e-4, 0.9, 0.999, 1e-8, 0.1, 1.0)
+        gd = g.double()
+        nrm = gd.norm()
+        gd = gd if nrm < 1.0 else gd / nrm * 1.0  # optax clip_by_global_norm
+        rm = 0.9 * rm + 0.1 * gd
+        rv = 0.999 * rv + 0.001 * gd * gd
+        mh, vh = rm / (1 - 0.9 ** t), rv / (1 - 0.999 ** t)
+        rp = rp - 3e-4 * (mh / (vh.sqrt() + 1e-8) + 0.1 * rp)
+        assert step.item() == t
+    assert torch.allclose(p.double(), rp, atol=1e-6)
