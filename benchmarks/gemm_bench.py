@@ -1,0 +1,90 @@
+"""Per-shape timing of the HIP GEMM (every Dense of the reference GPT, fwd/dgrad/wgrad) and of the
+other hot kernels, in TFLOP/s / TB/s.  torch.matmul (hipBLASLt) is timed on the same bf16 operands
+as a yardstick only — it is never used by the training path.
+
+    python benchmarks/gemm_bench.py [--reps 50] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_training_compare_jax_amd.ops import attention as A  # noqa: E402
+from distributed_training_compare_jax_amd.ops import gemm as G  # noqa: E402
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    M, D, F, V = 4096, 512, 2048, 50304
+    r = lambda *s: (torch.randn(*s, device=dev) * 0.5).to(torch.bfloat16)  # noqa: E731
+    rows = []
+
+    def rec(name, us, flops, ref_us=None):
+        tf = flops / us / 1e6
+        rows.append(dict(op=name, us=round(us, 2), tflops=round(tf, 1),
+                         hipblaslt_us=None if ref_us is None else round(ref_us, 2)))
+        print(f"{name:38s} {us:9.1f} us {tf:8.1f} TF/s" + ("" if ref_us is None else f"   (hipBLASLt {ref_us:8.1f} us)"),
+              flush=True)
+
+    for (n, k, tag) in [(3 * D, D, "qkv"), (D, D, "out"), (F, D, "fc1"), (D, F, "fc2"), (V, D, "lm_head")]:
+        x, w = r(M, k), r(n, k) * 0.05
+        b = torch.zeros(n, device=dev)
+        res = torch.zeros(M, n, device=dev)
+        if tag in ("out", "fc2"):
+            f = lambda: G.linear_resid(x, w, b, res)  # noqa: E731
+        elif tag == "fc1":
+            f = lambda: G.linear_gelu(x, w, b)  # noqa: E731
+        elif tag == "lm_head":
+            from distributed_training_compare_jax_amd.ops import xent as X
+            lab = torch.randint(0, 50257, (M,), device=dev, dtype=torch.int32)
+            f = lambda: X.lmhead_logits_partials(x, w, b, lab, 0, 50257)  # noqa: E731
+        else:
+            f = lambda: G.linear(x, w, b)  # noqa: E731
+        rec(f"fwd  {tag} [{M}x{n}x{k}]", timeit(f, a.reps), 2 * M * n * k, timeit(lambda: x @ w.t(), a.reps))
+        dy = r(M, n)
+        if tag == "fc2":
+            u = r(M, k)
+            f = lambda: G.matmul_nn_dgelu(dy, w, u)  # noqa: E731
+        else:
+            f = lambda: G.matmul_nn(dy, w)  # noqa: E731
+        rec(f"dgrad {tag} [{M}x{k}x{n}]", timeit(f, a.reps), 2 * M * n * k, timeit(lambda: dy @ w, a.reps))
+        dw = torch.zeros(n, k, device=dev)
+        rec(f"wgrad {tag} [{n}x{k}x{M}]", timeit(lambda: G.wgrad(dy, x, dw), a.reps), 2 * M * n * k,
+            timeit(lambda: dy.t() @ x, a.reps))
+        db = torch.zeros(n, device=dev)
+        us = timeit(lambda: G.colsum(dy, db), a.reps)
+        rows.append(dict(op=f"colsum {tag}", us=round(us, 2)))
+        print(f"colsum {tag:31s} {us:9.1f} us", flush=True)
+    qkv = r(8, 512, 3 * D)
+    o, lse = A.attn_fwd(qkv, 16)
+    fl = A.attn_flops(8, 512, 16, 32)
+    rec("attn fwd  B8 T512 H16 hd32", timeit(lambda: A.attn_fwd(qkv, 16), a.reps), fl)
+    do = r(8, 512, D)
+    rec("attn bwd  B8 T512 H16 hd32", timeit(lambda: A.attn_bwd(qkv, o, lse, do, 16), a.reps), 2.5 * fl)
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(rows, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -23,7 +23,10 @@ constexpr float LN2 = 0.6931471805599453f;
 
 template <int HD>
 struct AttnLds {
-  static constexpr int KLD = HD + 8;   // row-read image (ds_read_b128 of 8 contiguous hd)
+  // row-read image (ds_read_b128 of 8 contiguous hd): 160-B rows (40 dwords) make the 16 rows x
+  // 4 lane groups of a fragment read hit 64 distinct banks (80-B rows measured 35% conflicts)
+  static constexpr int KLD = 80;
+  static_assert(HD <= 64, "KLD sized for head_dim <= 64");
   static constexpr int VLD = HD + 16;  // tr-read image (rows = keys/queries, cols = hd)
 };
 
@@ -60,6 +63,65 @@ __device__ __forceinline__ void stage_tile(bf16* lds, int ld, const bf16* __rest
   }
 }
 
+// Register-staged pair of [ROWS][HD] tiles (K&V, Q&dO, ...) for a 2-deep software pipeline:
+// tile i+2 is loaded into registers while LDS holds tile i and registers hold tile i+1 (T14).
+template <int HD, int ROWS>
+struct PairStage {
+  static constexpr int CH = ROWS * HD / 8;             // 16-B chunks per tile
+  static constexpr int CPT = (CH + 255) / 256;         // per thread
+  u32x4 x[CPT], y[CPT];
+  __device__ __forceinline__ void load(const bf16* __restrict__ bx, long sx, const bf16* __restrict__ by, long sy,
+                                       int t0, int T, int tid) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / (HD / 8), col = (c % (HD / 8)) * 8, t = t0 + r;
+      const bool ok = c < CH && t < T;
+      x[i] = ok ? *(const u32x4*)(bx + (long)t * sx + col) : u32x4{0, 0, 0, 0};
+      y[i] = ok ? *(const u32x4*)(by + (long)t * sy + col) : u32x4{0, 0, 0, 0};
+    }
+  }
+  __device__ __forceinline__ void store(bf16* lx, int ldx, bf16* ly, int ldy, int tid) const {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + 256 * i;
+      if (c < CH) {
+        const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
+        *(u32x4*)(lx + r * ldx + col) = x[i];
+        *(u32x4*)(ly + r * ldy + col) = y[i];
+      }
+    }
+  }
+};
+
+// Runs body(ldsX, ldsY, it) for it = 0..n-1 over tiles starting at token t0_of(it), with the
+// tiles streamed through two LDS stages and two register stages (one barrier per tile).
+template <int HD, int ROWS, typename T0, typename Body>
+__device__ __forceinline__ void pipelined_tiles(int n, T0 t0_of, const bf16* bx, long sx, const bf16* by, long sy,
+                                                int T, bf16* lds, int ldx, int ldy, int tid, Body body) {
+  if (n <= 0) return;
+  bf16* X0 = lds;
+  bf16* Y0 = X0 + ROWS * ldx;
+  bf16* X1 = Y0 + ROWS * ldy;
+  bf16* Y1 = X1 + ROWS * ldx;
+  PairStage<HD, ROWS> p0, p1;
+  p0.load(bx, sx, by, sy, t0_of(0), T, tid);
+  if (n > 1) p1.load(bx, sx, by, sy, t0_of(1), T, tid);
+  p0.store(X0, ldx, Y0, ldy, tid);
+  __syncthreads();
+  for (int it = 0; it < n; it += 2) {
+    if (it + 2 < n) p0.load(bx, sx, by, sy, t0_of(it + 2), T, tid);
+    body(X0, Y0, it);
+    if (it + 1 < n) p1.store(X1, ldx, Y1, ldy, tid);
+    __syncthreads();
+    if (it + 1 >= n) break;
+    if (it + 3 < n) p1.load(bx, sx, by, sy, t0_of(it + 3), T, tid);
+    body(X1, Y1, it + 1);
+    if (it + 2 < n) p0.store(X0, ldx, Y0, ldy, tid);
+    __syncthreads();
+  }
+}
+
 // ============================================================================ forward
 template <int HD>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
@@ -67,8 +129,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16* __restrict__ 
   constexpr int KC = HD / 32;  // k-chunks of the QK^T product
   constexpr int HT = HD / 16;  // 16-wide hd tiles of the output
   using L = AttnLds<HD>;
-  __shared__ __attribute__((aligned(16))) bf16 sK[64 * L::KLD];
-  __shared__ __attribute__((aligned(16))) bf16 sV[64 * L::VLD];
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 64 * (L::KLD + L::VLD)];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int nqb = (T + 63) / 64;
   const int qb = nqb - 1 - (int)(blockIdx.x % nqb);  // heavy (late) query blocks first
@@ -88,11 +149,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int kt = 0; kt <= qb; ++kt) {
-    __syncthreads();
-    stage_tile<HD, 64>(sK, L::KLD, Kb, ts, kt * 64, T, tid, 256);
-    stage_tile<HD, 64>(sV, L::VLD, Vb, ts, kt * 64, T, tid, 256);
-    __syncthreads();
+  auto body = [&](const bf16* sK, const bf16* sV, int kt) {
     f32x4 s[4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
@@ -134,7 +191,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16* __restrict__ 
       acc[t] = mfma(tr_frag(sV, L::VLD, 0, t * 16, lane), pf0, acc[t]);
       acc[t] = mfma(tr_frag(sV, L::VLD, 32, t * 16, lane), pf1, acc[t]);
     }
-  }
+  };
+  pipelined_tiles<HD, 64>(qb + 1, [](int it) { return it * 64; }, Kb, ts, Vb, ts, T, lds, L::KLD, L::VLD, tid, body);
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   if (q < T) {
@@ -177,11 +235,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restri
                                                             bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
-  __shared__ __attribute__((aligned(16))) bf16 sQ[32 * L::VLD];
-  __shared__ __attribute__((aligned(16))) bf16 sD[32 * L::VLD];
+  __shared__ __attribute__((aligned(16))) bf16 lds[4 * 32 * L::VLD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int nkb = (T + 63) / 64;
-  const int kb = (int)(blockIdx.x % nkb);  // light first: kb 0 sweeps all queries
+  const int kb = (int)(blockIdx.x % nkb);  // kb 0 (sweeps all queries, heaviest) launches first
   const int bh = blockIdx.x / nkb, b = bh / H, h = bh % H;
   const long ts = 3L * H * HD, dts = (long)H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
@@ -202,11 +259,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restri
 #pragma unroll
   for (int t = 0; t < HT; ++t) { dk[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
 
-  for (int q0 = kb * 64; q0 < T; q0 += 32) {
-    __syncthreads();
-    stage_tile<HD, 32>(sQ, L::VLD, Qb, ts, q0, T, tid, 256);
-    stage_tile<HD, 32>(sD, L::VLD, dOb, dts, q0, T, tid, 256);
-    __syncthreads();
+  auto body = [&](const bf16* sQ, const bf16* sD, int it) {
+    const int q0 = kb * 64 + 32 * it;
     f32x4 p[2], ds[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -234,7 +288,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restri
       dv[t] = mfma(tr_frag(sD, L::VLD, 0, t * 16, lane), pb, dv[t]);   // dV^T[hd][key] += dO^T P
       dk[t] = mfma(tr_frag(sQ, L::VLD, 0, t * 16, lane), dsb, dk[t]);  // dK^T[hd][key] += Q^T dS
     }
-  }
+  };
+  const int nq = (T - kb * 64 + 31) / 32;
+  pipelined_tiles<HD, 32>(nq, [kb](int it) { return kb * 64 + 32 * it; }, Qb, ts, dOb, dts, T, lds, L::VLD, L::VLD,
+                          tid, body);
   if (key < T) {
     bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
     bf16* pv = dqkv + ((long)b * T + key) * ts + (2 * H + h) * HD;
@@ -254,8 +311,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
                                                           bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
-  __shared__ __attribute__((aligned(16))) bf16 sK[32 * L::VLD];
-  __shared__ __attribute__((aligned(16))) bf16 sV[32 * L::VLD];
+  __shared__ __attribute__((aligned(16))) bf16 lds[4 * 32 * L::VLD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int nqb = (T + 63) / 64;
   const int qb = nqb - 1 - (int)(blockIdx.x % nqb);
@@ -279,11 +335,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
   for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kend = min(T, qb * 64 + 64);
-  for (int k0 = 0; k0 < kend; k0 += 32) {
-    __syncthreads();
-    stage_tile<HD, 32>(sK, L::VLD, Kb, ts, k0, T, tid, 256);
-    stage_tile<HD, 32>(sV, L::VLD, Vb, ts, k0, T, tid, 256);
-    __syncthreads();
+  auto body = [&](const bf16* sK, const bf16* sV, int it) {
+    const int k0 = 32 * it;
     f32x4 ds[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -303,7 +356,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
     const bf16x8 dsb = pack_p(ds[0], ds[1]);
 #pragma unroll
     for (int t = 0; t < HT; ++t) acc[t] = mfma(tr_frag(sK, L::VLD, 0, t * 16, lane), dsb, acc[t]);  // dQ^T += K^T dS^T
-  }
+  };
+  pipelined_tiles<HD, 32>((kend + 31) / 32, [](int it) { return 32 * it; }, Kb, ts, Vb, ts, T, lds, L::VLD, L::VLD,
+                          tid, body);
   if (q < T) {
     bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
 #pragma unroll

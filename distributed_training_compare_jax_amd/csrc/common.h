@@ -12,6 +12,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 #define DTC_WAVE 64
 #define DTC_LDS __attribute__((address_space(3)))
@@ -56,14 +57,20 @@ __device__ __forceinline__ float warp_max(float v) {
 }
 
 // gelu (tanh approximation, jax.nn.gelu(approximate=True) = flax nn.gelu default)
+// tanh via one v_exp_f32 + one v_rcp_f32 (libm tanhf is ~40 VALU ops and made the fc1/fc2
+// epilogues VALU-bound: 11-15 VALU per MFMA in the PMC profile).  |err| ~1e-7, far below bf16.
+__device__ __forceinline__ float fast_tanh(float z) {
+  const float e = __expf(2.f * fminf(fmaxf(z, -15.f), 15.f));
+  return 1.f - 2.f * __frcp_rn(e + 1.f);
+}
 __device__ __forceinline__ float gelu_tanh_f(float u) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float t = tanhf(k0 * (u + k1 * u * u * u));
+  float t = fast_tanh(k0 * (u + k1 * u * u * u));
   return 0.5f * u * (1.f + t);
 }
 __device__ __forceinline__ float gelu_tanh_grad_f(float u) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float t = tanhf(k0 * (u + k1 * u * u * u));
+  float t = fast_tanh(k0 * (u + k1 * u * u * u));
   return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
 }
 

@@ -156,7 +156,16 @@ __global__ void __launch_bounds__(256) sumsq_stage1(const float* __restrict__ x,
     const long off = (long)seg[3 * s], len = (long)seg[3 * s + 1];
     const float w = (float)seg[3 * s + 2];
     float a = 0.f;
-    for (long i = tid; i < len; i += stride) { float v = x[off + i]; a += v * v; }
+    const long len4 = len >> 2;  // ranges are 64-element aligned: 16-byte loads, 4 in flight
+    const f32x4* x4 = (const f32x4*)(x + off);
+    long i = tid;
+    for (; i + 3 * stride < len4; i += 4 * stride) {
+      f32x4 v0 = x4[i], v1 = x4[i + stride], v2 = x4[i + 2 * stride], v3 = x4[i + 3 * stride];
+      f32x4 q = v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+      a += (q[0] + q[1]) + (q[2] + q[3]);
+    }
+    for (; i < len4; i += stride) { f32x4 v = x4[i] * x4[i]; a += (v[0] + v[1]) + (v[2] + v[3]); }
+    for (long j = (len4 << 2) + tid; j < len; j += stride) { float v = x[off + j]; a += v * v; }
     acc += w * a;
   }
   __shared__ float red[4];

@@ -24,6 +24,7 @@
 //    blocks sharing a weight panel share an L2).
 //  * Split-K (fp32 slabs + deterministic reduce) for the small wgrad grids.
 #include "common.h"
+#include <algorithm>
 
 namespace {
 
@@ -31,28 +32,35 @@ constexpr int NT = 256;
 
 template <int R, int BK, bool KMAJ>
 struct Tile {
-  static constexpr int LD = KMAJ ? (BK + 8) : (R + 16);  // LDS row length (elements)
+  // LDS row length (elements).  K-major: 160-B rows (40 dwords): a ds_read_b128 fragment read by 16
+  // rows x 4 lane groups covers all 64 banks exactly once per 16-lane group (conflict-free).
+  // MN-major: 288-B rows for R=128 / 160-B for R=64 (rows 8 apart stay 32 B apart in bank space,
+  // conflict-free for ds_read_b64_tr_b16).
+  static constexpr int LD = KMAJ ? (BK + 16) : (R + 16);
   static constexpr int ROWS = KMAJ ? R : BK;
   static constexpr int ELEMS = ROWS * LD;
   static constexpr int CHUNKS = R * BK / 8;  // 16-byte chunks in the tile
   static constexpr int PER_THREAD = CHUNKS / NT;
   static_assert(CHUNKS % NT == 0, "tile too small for 256 threads");
 
-  // global -> registers.  rows: extent of the R dimension (M or N); r0/k0 tile origin.
-  __device__ __forceinline__ static void load(u32x4 (&reg)[PER_THREAD], const bf16* __restrict__ g, long ld,
-                                              int r0, int k0, int rows, int tid) {
+  // global -> registers through a buffer resource: branch-free, and any byte past the operand's
+  // extent (rows/cols beyond M or N at a ragged edge) reads as 0 by the hardware range check.
+  // Columns beyond the extent INSIDE a row (MN-major operand) only feed output rows/cols that
+  // the epilogue never stores.
+  __device__ __forceinline__ static void load(u32x4 (&reg)[PER_THREAD], __amdgpu_buffer_rsrc_t rs, long ld, int r0,
+                                              int k0, int tid) {
 #pragma unroll
     for (int i = 0; i < PER_THREAD; ++i) {
       int c = tid + i * NT;
+      long off;
       if (KMAJ) {
         int row = c / (BK / 8), col = (c % (BK / 8)) * 8;
-        int gr = r0 + row;
-        reg[i] = gr < rows ? *(const u32x4*)(g + (long)gr * ld + k0 + col) : u32x4{0, 0, 0, 0};
+        off = ((long)(r0 + row) * ld + k0 + col) * 2;
       } else {
         int krow = c / (R / 8), col = (c % (R / 8)) * 8;
-        int gc = r0 + col;
-        reg[i] = gc < rows ? *(const u32x4*)(g + (long)(k0 + krow) * ld + gc) : u32x4{0, 0, 0, 0};
+        off = ((long)(k0 + krow) * ld + r0 + col) * 2;
       }
+      reg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
     }
   }
   __device__ __forceinline__ static void store(const u32x4 (&reg)[PER_THREAD], bf16* lds, int tid) {
@@ -60,8 +68,14 @@ struct Tile {
     for (int i = 0; i < PER_THREAD; ++i) {
       int c = tid + i * NT;
       if (KMAJ) {
+        // k-permuted image: inside each 32-k group, the 8-byte segment a = k/4 (k = 4a..4a+3)
+        // lands at element 8*(a&3) + 4*(a>>2), so lane group g's 8 fragment elements
+        // (k = 4g..4g+3 and 16+4g..16+4g+3) are contiguous -> ONE ds_read_b128 per fragment
         int row = c / (BK / 8), col = (c % (BK / 8)) * 8;
-        *(u32x4*)(lds + row * LD + col) = reg[i];
+        int grp = col & ~31, a0 = (col & 31) >> 2;  // a0 even: segments a0, a0+1
+        bf16* rp = lds + row * LD + grp;
+        *(u32x2*)(rp + 8 * (a0 & 3) + 4 * (a0 >> 2)) = u32x2{reg[i][0], reg[i][1]};
+        *(u32x2*)(rp + 8 * ((a0 + 1) & 3) + 4 * ((a0 + 1) >> 2)) = u32x2{reg[i][2], reg[i][3]};
       } else {
         int krow = c / (R / 8), col = (c % (R / 8)) * 8;
         *(u32x4*)(lds + krow * LD + col) = reg[i];
@@ -72,10 +86,7 @@ struct Tile {
   __device__ __forceinline__ static bf16x8 frag(const bf16* lds, int t, int kk, int lane) {
     const int g = lane >> 4;
     if (KMAJ) {
-      const bf16* p = lds + (t * 16 + (lane & 15)) * LD + kk * 32 + 4 * g;
-      bf16x4 lo = *(const bf16x4*)p;
-      bf16x4 hi = *(const bf16x4*)(p + 16);
-      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      return *(const bf16x8*)(lds + (t * 16 + (lane & 15)) * LD + kk * 32 + 8 * g);
     } else {
       const int li = lane & 15, q = li >> 2, pp = li & 3;
       const bf16* p0 = lds + (kk * 32 + 4 * g + q) * LD + t * 16 + 4 * pp;
@@ -144,8 +155,9 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
 
 template <int BM, int BN, int BK, bool AK, bool BKM, int EPI, bool OUTF32>
 __global__ void __launch_bounds__(NT, 2)
-gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
-            int tiles_m, int tiles_n, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __restrict__ B, long ldb, int b_bytes, int M,
+            int N, int K,
+            int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
   using TA = Tile<BM, BK, AK>;
   using TB = Tile<BN, BK, BKM>;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -157,9 +169,14 @@ gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, lo
   const int ntiles = tiles_m * tiles_n;
   const int lid = xcd_remap(blockIdx.x, ntiles * split);
   const int tile = lid % ntiles, z = lid / ntiles;
-  const int m0 = (tile % tiles_m) * BM, n0 = (tile / tiles_m) * BN;
+  // grouped tile order: groups of `gm` M-tiles sweep all N-tiles, so the run of tiles one XCD
+  // receives touches few A rows AND few B columns (per-XCD L2 footprint; gm = tiles_m -> M fastest)
+  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+  const int gm_eff = min(gm, tiles_m - grp * gm);
+  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
   const int kbeg = z * k_per_split;
-  const int nk = k_per_split / BK;
+  const int nk = min(k_per_split, K - kbeg) / BK;
 
   f32x4 acc[TN][TM];
 #pragma unroll
@@ -167,22 +184,10 @@ gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, lo
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[TA::PER_THREAD], rb[TB::PER_THREAD];
-  TA::load(ra, A, lda, m0, kbeg, M, tid);
-  TB::load(rb, B, ldb, n0, kbeg, N, tid);
-  TA::store(ra, smem, tid);
-  TB::store(rb, smem + TA::ELEMS, tid);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    const bf16* sAc = smem + cur * BUF;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
+  auto compute = [&](const bf16* sAc) {
     const bf16* sBc = sAc + TA::ELEMS;
-    if (more) {
-      TA::load(ra, A, lda, m0, kbeg + (kt + 1) * BK, M, tid);
-      TB::load(rb, B, ldb, n0, kbeg + (kt + 1) * BK, N, tid);
-    }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 fa[TM], fb[TN];
@@ -195,11 +200,70 @@ gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, lo
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      TA::store(ra, smem + (cur ^ 1) * BUF, tid);
-      TB::store(rb, smem + (cur ^ 1) * BUF + TA::ELEMS, tid);
+  };
+  bf16* const s0 = smem;
+  bf16* const s1 = smem + BUF;
+  if constexpr (BM * BN <= 64 * 64) {
+    // small tiles (few MFMAs per k-step): 2-deep register prefetch.  While the MFMAs consume LDS
+    // stage kt, tile kt+1's loads are a full k-step old and tile kt+2's are being issued (two
+    // named register sets, no runtime-indexed register arrays -> no scratch; guide §5.4 rule 20).
+    u32x4 ra0[TA::PER_THREAD], rb0[TB::PER_THREAD], ra1[TA::PER_THREAD], rb1[TB::PER_THREAD];
+    TA::load(ra0, rsA, lda, m0, kbeg, tid);
+    TB::load(rb0, rsB, ldb, n0, kbeg, tid);
+    if (nk > 1) {
+      TA::load(ra1, rsA, lda, m0, kbeg + BK, tid);
+      TB::load(rb1, rsB, ldb, n0, kbeg + BK, tid);
     }
+    TA::store(ra0, s0, tid);
+    TB::store(rb0, s0 + TA::ELEMS, tid);
     __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) {
+        TA::load(ra0, rsA, lda, m0, kbeg + (kt + 2) * BK, tid);
+        TB::load(rb0, rsB, ldb, n0, kbeg + (kt + 2) * BK, tid);
+      }
+      compute(s0);
+      if (kt + 1 < nk) {
+        TA::store(ra1, s1, tid);
+        TB::store(rb1, s1 + TA::ELEMS, tid);
+      }
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) {
+        TA::load(ra1, rsA, lda, m0, kbeg + (kt + 3) * BK, tid);
+        TB::load(rb1, rsB, ldb, n0, kbeg + (kt + 3) * BK, tid);
+      }
+      compute(s1);
+      if (kt + 2 < nk) {
+        TA::store(ra0, s0, tid);
+        TB::store(rb0, s0 + TA::ELEMS, tid);
+      }
+      __syncthreads();
+    }
+  } else {
+    // large tiles: one register set (T14: issue tile kt+1 before the MFMAs of tile kt, write it
+    // to the other LDS stage after them; the co-resident block's MFMAs cover the rest)
+    u32x4 ra[TA::PER_THREAD], rb[TB::PER_THREAD];
+    TA::load(ra, rsA, lda, m0, kbeg, tid);
+    TB::load(rb, rsB, ldb, n0, kbeg, tid);
+    TA::store(ra, s0, tid);
+    TB::store(rb, s0 + TA::ELEMS, tid);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      bf16* cur = (kt & 1) ? s1 : s0;
+      bf16* nxt = (kt & 1) ? s0 : s1;
+      if (more) {
+        TA::load(ra, rsA, lda, m0, kbeg + (kt + 1) * BK, tid);
+        TB::load(rb, rsB, ldb, n0, kbeg + (kt + 1) * BK, tid);
+      }
+      compute(cur);
+      if (more) {
+        TA::store(ra, nxt, tid);
+        TB::store(rb, nxt + TA::ELEMS, tid);
+      }
+      __syncthreads();
+    }
   }
 
   // ---------------- epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + r]
@@ -222,7 +286,7 @@ gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, lo
   }
   if (EPI == EPI_LMHEAD) {
     // logits (bf16) + per-row partial (max, sum exp) over this wave's WN columns + label logit.
-    const int part_idx = (tile / tiles_m) * 2 + wn;
+    const int part_idx = tn_idx * 2 + wn;
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int m = m0 + wm * WM + j * 16 + (lane & 15);
@@ -296,17 +360,28 @@ struct Plan {
   int bm, bn, bk, split;
 };
 
-Plan make_plan(int M, int N, int K, bool allow_split) {
+// allow_split: 1 = small-grid split (wgrad), 2 = huge-K only (dgrad through the lm_head)
+Plan make_plan(int M, int N, int K, int allow_split) {
   Plan p{128, 128, 64, 1};
-  long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  const int nk = K / 64;
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  if (allow_split && K >= 8192 && t128 >= 32) {  // e.g. dH = dlogits . W_lm (K = vocab)
+    p.split = (int)std::max(1L, std::min((long)nk / 64, (512 + t128 - 1) / t128));
+    return p;
+  }
   if (t128 < 256) {
     p.bm = p.bn = 64;
-    long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
-    if (allow_split) {
-      while (t64 * p.split < 512 && K % (p.split * 2 * p.bk) == 0 && K / (p.split * 2) >= 256) p.split *= 2;
-    }
+    const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
+    if (allow_split == 1)
+      while (t64 * p.split < 512 && nk / (p.split * 2) >= 4) p.split *= 2;
   }
   return p;
+}
+
+// exact byte extent of an operand (rows x K if K-major, K x rows if MN-major) for the buffer range check
+inline int operand_bytes(bool kmajor, int rows, int K, long ld) {
+  long n = kmajor ? ((long)(rows - 1) * ld + K) : ((long)(K - 1) * ld + rows);
+  return (int)std::min(n * 2, (long)0x7FFFFFF0);
 }
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, bool OUTF32>
@@ -317,11 +392,17 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
   int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   e.nparts = tiles_n * 2;
-  int kps = a.K / p.split;
-  dim3 grid(tiles_m * tiles_n * p.split);
+  const int nk = a.K / 64;
+  const int kps = ((nk + p.split - 1) / p.split) * 64;
+  const int ntiles = tiles_m * tiles_n;
+  // per-XCD share of tiles = ntiles*split/8: with few N-tiles make each XCD own whole M-row groups
+  int gm = tiles_m;
+  if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
+  dim3 grid(ntiles * p.split);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st,
-                     (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, p.split, kps,
-                     (float*)a.workspace, e);
+                     (const bf16*)a.A, a.lda, operand_bytes(AK, a.M, a.K, a.lda), (const bf16*)a.B, a.ldb,
+                     operand_bytes(BKM, a.N, a.K, a.ldb), a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split,
+                     kps, (float*)a.workspace, e);
   DTC_CHECK_LAUNCH();
   if (p.split > 1) {
     long MN = (long)a.M * a.N;
@@ -346,7 +427,7 @@ extern "C" {
 int dtc_lmhead_nparts(int N) { return ((N + 127) / 128) * 2; }
 
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
-  Plan p = make_plan(M, N, K, layout == 2);
+  Plan p = make_plan(M, N, K, layout == 2 ? 1 : (layout == 1 ? 2 : 0));
   return p.split > 1 ? (long)p.split * M * N * 4 : 0;
 }
 
@@ -357,7 +438,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
   if (a->layout == 0) {
-    Plan p = make_plan(a->M, a->N, a->K, false);
+    Plan p = make_plan(a->M, a->N, a->K, 0);
     if (epi == EPI_LMHEAD) { p.bm = p.bn = 128; return launch_t<128, 128, true, true, EPI_LMHEAD, false>(*a, p, st); }
     if (epi == EPI_GELU) return launch_sz<true, true, EPI_GELU, false>(*a, p, st);
     if (epi == EPI_RESID) return launch_sz<true, true, EPI_RESID, true>(*a, p, st);
@@ -367,7 +448,8 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   }
   if (a->layout == 1) {
     if (a->N % 8) return 1004;
-    Plan p = make_plan(a->M, a->N, a->K, false);
+    Plan p = make_plan(a->M, a->N, a->K, (epi == EPI_STORE && f32) ? 2 : 0);
+    if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;
     if (epi == EPI_DGELU) return launch_sz<true, false, EPI_DGELU, false>(*a, p, st);
     if (epi == EPI_STORE) return f32 ? launch_sz<true, false, EPI_STORE, true>(*a, p, st)
                                      : launch_sz<true, false, EPI_STORE, false>(*a, p, st);
@@ -376,7 +458,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->layout == 2) {
     if (a->M % 8 || a->N % 8) return 1004;
     if (epi != EPI_STORE || !f32 || a->bias) return 1003;
-    Plan p = make_plan(a->M, a->N, a->K, true);
+    Plan p = make_plan(a->M, a->N, a->K, 1);
     if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;
     return launch_sz<false, false, EPI_STORE, true>(*a, p, st);
   }

@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-constexpr int LN_BWD_ROWS = 16;  // rows per block (4 waves x 4 rows)
+constexpr int LN_BWD_ROWS = 16;  // rows per block (4 waves x 4 rows): 256 blocks at M=4096
 
 template <int NV>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy, int dy_f32, const float* __restrict__ x,
@@ -121,49 +121,66 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
   }
 }
 
-// out[c] (+)= sum_p part[p*stride + c]   for the two slabs of ln bwd (dgamma, dbeta)
-__global__ void slab_reduce2(const float* __restrict__ part, int P, int D, float* __restrict__ o0,
-                             float* __restrict__ o1, int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * D) return;
-  int which = c / D, col = c % D;
+// out (+)= sum_p part[p*C + c], c in [0, C); columns [0, split_c) go to o0, the rest to o1.
+// Block = 64 columns x 4 partial groups (coalesced 256-B row reads), LDS tree for the groups.
+__global__ void __launch_bounds__(256) slab_reduce(const float* __restrict__ part, int P, int C, float* __restrict__ o0,
+                                                   float* __restrict__ o1, int split_c, float beta) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[((long)p * 2 + which) * D + col];
-  float* o = which ? o1 : o0;
-  o[col] = accumulate ? o[col] + s : s;
-}
-
-constexpr int CS_ROWS = 64;
-
-// stage 1: part[slab][n] = sum over rows of the slab (4 columns per thread, vector loads)
-__global__ void __launch_bounds__(256) colsum_stage1(const void* __restrict__ dy, int is_f32, int M, int N, long ld,
-                                                     float* __restrict__ part) {
-  const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
-  const int r0 = blockIdx.y * CS_ROWS;
-  if (n >= N) return;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  const int r1 = min(M, r0 + CS_ROWS);
-  if (n + 4 <= N) {
-    for (int r = r0; r < r1; ++r) {
-      if (is_f32) s += *(const f32x4*)((const float*)dy + (long)r * ld + n);
-      else { bf16x4 t = *(const bf16x4*)((const bf16*)dy + (long)r * ld + n); s += f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]}; }
-    }
-    *(f32x4*)(part + (long)blockIdx.y * N + n) = s;
-  } else {
-    for (int j = 0; j < 4 && n + j < N; ++j) {
-      float a = 0.f;
-      for (int r = r0; r < r1; ++r) a += is_f32 ? ((const float*)dy)[(long)r * ld + n + j] : (float)((const bf16*)dy)[(long)r * ld + n + j];
-      part[(long)blockIdx.y * N + n + j] = a;
-    }
+  if (c < C) {
+#pragma unroll 4
+    for (int p = ty; p < P; p += 4) s += part[(long)p * C + c];
+  }
+  __shared__ float red[4][64];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    const float t = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    float* o = c < split_c ? o0 : o1;
+    const int col = c < split_c ? c : c - split_c;
+    o[col] = beta != 0.f ? beta * o[col] + t : t;
   }
 }
 
-__global__ void colsum_stage2(const float* __restrict__ part, int P, int N, float* __restrict__ out, float beta) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(long)p * N + n];
-  out[n] = beta != 0.f ? beta * out[n] + s : s;
+constexpr int CS_ROWS = 32;  // rows per stage-1 slab
+
+// stage 1: part[slab][n] = sum over the slab's rows.  Block = 64 column-threads (4 columns each,
+// vector loads) x 4 row groups of CS_ROWS/4 rows, LDS combine of the groups.
+__global__ void __launch_bounds__(256) colsum_stage1(const void* __restrict__ dy, int is_f32, int M, int N, long ld,
+                                                     float* __restrict__ part) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = (blockIdx.x * 64 + tx) * 4;
+  const int r0 = blockIdx.y * CS_ROWS + ty * (CS_ROWS / 4);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    if (n + 4 <= N) {
+#pragma unroll
+      for (int i = 0; i < CS_ROWS / 4; ++i) {
+        const int r = r0 + i;
+        if (r < M) {
+          if (is_f32) s += *(const f32x4*)((const float*)dy + (long)r * ld + n);
+          else { bf16x4 t = *(const bf16x4*)((const bf16*)dy + (long)r * ld + n); s += f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]}; }
+        }
+      }
+    } else {
+      for (int i = 0; i < CS_ROWS / 4; ++i) {
+        const int r = r0 + i;
+        if (r < M)
+          for (int j = 0; j < 4 && n + j < N; ++j)
+            s[j] += is_f32 ? ((const float*)dy)[(long)r * ld + n + j] : (float)((const bf16*)dy)[(long)r * ld + n + j];
+      }
+    }
+  }
+  __shared__ f32x4 red[4][64];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && n < N) {
+    f32x4 t = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    float* o = part + (long)blockIdx.y * N + n;
+    if (n + 4 <= N) *(f32x4*)o = t;
+    else for (int j = 0; j < 4 && n + j < N; ++j) o[j] = t[j];
+  }
 }
 
 }  // namespace
@@ -206,7 +223,8 @@ int dtc_layernorm_bwd(const void* dy, int dy_f32, const float* x, const float* g
   DTC_NV_SWITCH(nv, hipLaunchKernelGGL(ln_bwd_kernel<NVC>, dim3(blocks), dim3(256), 0, st, dy, dy_f32, x, g, mean, rstd,
                                        dres, dx, dx_c, ws, M, D));
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_reduce2, dim3((2 * D + 255) / 256), dim3(256), 0, st, ws, blocks, D, dg, db, accumulate);
+  hipLaunchKernelGGL(slab_reduce, dim3((2 * D + 63) / 64), dim3(256), 0, st, ws, blocks, 2 * D, dg, db, D,
+                     accumulate ? 1.f : 0.f);
   DTC_CHECK_LAUNCH();
   return 0;
 }
@@ -218,10 +236,17 @@ int dtc_colsum(const void* dy, int is_f32, int M, int N, long ld, float* out, fl
   int P = (M + CS_ROWS - 1) / CS_ROWS;
   if (ws_bytes < dtc_colsum_workspace_bytes(M, N)) return 2004;
   if (ld % 4) return 2005;
-  dim3 g1((N / 4 + 255) / 256 + 1, P);
+  dim3 g1((N + 255) / 256, P);
   hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, st, dy, is_f32, M, N, ld, ws);
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_stage2, dim3((N + 255) / 256), dim3(256), 0, st, ws, P, N, out, beta);
+  hipLaunchKernelGGL(slab_reduce, dim3((N + 63) / 64), dim3(256), 0, st, ws, P, N, out, out, N, beta);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// generic ordered reduction of fp32 partial slabs: out (beta*out +) sum_p part[p][c]
+int dtc_slab_reduce(const float* part, int P, int C, float* out, float beta, hipStream_t st) {
+  hipLaunchKernelGGL(slab_reduce, dim3((C + 63) / 64), dim3(256), 0, st, part, P, C, out, out, C, beta);
   DTC_CHECK_LAUNCH();
   return 0;
 }

@@ -47,6 +47,34 @@ class NoComm:
         return t.unsqueeze(0)
 
 
+class SideStream:
+    """Runs weight-gradient work (wgrad GEMMs, bias column sums) on a second HIP stream.
+
+    In backward only the dgrad chain is on the critical path; each layer's 4 wgrad GEMMs and 4
+    bias reductions are independent of it, so they overlap the next dgrad kernels (these small
+    GEMMs fill only part of the 256 CUs).  Inputs are kept referenced until :meth:`join`, so the
+    caching allocator cannot hand their memory to the main stream while the side stream reads it.
+    Under hipGraph capture the fork/join become graph edges."""
+
+    def __init__(self, device, enabled: bool):
+        self.stream = torch.cuda.Stream(device) if (enabled and torch.device(device).type == "cuda") else None
+        self.keep = []
+
+    def run(self, fn, *keep):
+        if self.stream is None:
+            fn()
+            return
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream), G.workspace_role("side"):
+            fn()
+        self.keep.extend(keep)
+
+    def join(self):
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
+            self.keep.clear()
+
+
 @dataclass
 class StageLayout:
     layers: range
@@ -58,8 +86,9 @@ class GPTStage:
     """The slice of the GPT owned by one rank (all of it, a TP shard, or a PP stage)."""
 
     def __init__(self, cfg: ModelConfig, flat: FlatParams, layout: StageLayout, tp=None,
-                 dropout_seed: int = 0, act_dtype: torch.dtype = torch.bfloat16):
+                 dropout_seed: int = 0, act_dtype: torch.dtype = torch.bfloat16, side_stream: bool = True):
         self.cfg = cfg
+        self.side = SideStream(flat.device, side_stream)
         self.flat = flat
         self.layout = layout
         self.tp = tp if tp is not None else NoComm()
@@ -111,24 +140,24 @@ class GPTStage:
         tp = self.tp
         x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch = ctx.pop(l)
         T = x.shape[0] // batch
-        # MLP
+        side = self.side
+        # MLP (dgrad chain on the main stream, weight grads on the side stream)
+        side.run(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), G.colsum(dx3, f.g(p + "fc2.b"), beta)),
+                 dx3_c, gact, dx3)
         du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
-        G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta)
-        G.colsum(dx3, f.g(p + "fc2.b"), beta)
+        side.run(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta), G.colsum(du, f.g(p + "fc1.b"), beta)), du, y2)
         dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
-        G.wgrad(du, y2, f.g(p + "fc1.w"), beta)
-        G.colsum(du, f.g(p + "fc1.b"), beta)
         tp.all_reduce_(dy2)
         dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta)
         # attention
+        side.run(lambda: (G.wgrad(dx2_c, o, f.g(p + "out.w"), beta), G.colsum(dx2, f.g(p + "out.b"), beta)),
+                 dx2_c, o, dx2)
         do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
-        G.wgrad(dx2_c, o, f.g(p + "out.w"), beta)
-        G.colsum(dx2, f.g(p + "out.b"), beta)
         dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                           self.heads_local).view(batch * T, -1)
+        side.run(lambda: (G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta), G.colsum(dqkv, f.g(p + "qkv.b"), beta)),
+                 dqkv, y1)
         dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
-        G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta)
-        G.colsum(dqkv, f.g(p + "qkv.b"), beta)
         tp.all_reduce_(dy1)
         return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta)
 
@@ -169,9 +198,9 @@ class GPTStage:
         f = self.flat
         x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
         dlogits = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale)
+        self.side.run(lambda: (G.wgrad(dlogits, yf, f.g("lm_head.w"), beta),
+                               G.colsum(dlogits, f.g("lm_head.b"), beta)), dlogits, yf)
         dyf = G.matmul_nn(dlogits, f.w("lm_head.w"))
-        G.wgrad(dlogits, yf, f.g("lm_head.w"), beta)
-        G.colsum(dlogits, f.g("lm_head.b"), beta)
         del logits, dlogits
         self.tp.all_reduce_(dyf)
         return self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta)

@@ -46,8 +46,11 @@ _WS = {}
 
 
 def _workspace(device, nbytes: int) -> torch.Tensor:
-    """Persistent per-device scratch (split-K slabs etc.).  Grows, never shrinks; stream-ordered reuse."""
-    key = (device.type, device.index)
+    """Persistent scratch (split-K slabs, reduction partials) per (device, stream role): kernels of
+    one role run in stream order and reuse it; the backward side stream (role "side", set by
+    :func:`workspace_role`) gets its own so concurrent kernels never share scratch.  Keyed by role,
+    not stream handle, so the capture stream of a hipGraph reuses the eager step's buffers."""
+    key = (device.type, device.index, _ROLE[0])
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
@@ -57,8 +60,26 @@ def _workspace(device, nbytes: int) -> torch.Tensor:
     return ws
 
 
-def reserve_workspace(device, nbytes: int):
-    _workspace(torch.device(device), nbytes)
+_ROLE = ["main"]
+
+
+class workspace_role:
+    """Context manager selecting the scratch-buffer role (``"main"`` / ``"side"``)."""
+
+    def __init__(self, role: str):
+        self.role = role
+
+    def __enter__(self):
+        self.prev = _ROLE[0]
+        _ROLE[0] = self.role
+
+    def __exit__(self, *a):
+        _ROLE[0] = self.prev
+
+
+def reserve_workspace(device, nbytes: int, role: str = "main"):
+    with workspace_role(role):
+        _workspace(torch.device(device), nbytes)
 
 
 def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, *,

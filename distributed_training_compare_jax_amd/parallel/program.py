@@ -37,10 +37,15 @@ class StepProgram:
         self._pool = None
         self._handles: Dict[str, Any] = {}
         self._stream = torch.cuda.Stream(self.device) if self.use_graph else None
+        # called before every cut/collective: forked streams (e.g. the backward side stream)
+        # must re-join the capture stream before a graph segment ends / a collective reads data
+        self.before_comm: List[Callable[[], None]] = []
 
     # -------------------------------------------------------------- step-code API
     def comm(self, fn: Callable[[], Any], name: Optional[str] = None):
         """Issue a collective.  ``fn`` may return an async Work handle, retrievable by ``wait(name)``."""
+        for h in self.before_comm:
+            h()
         if self.recording:
             self._cut()
             self.items.append(("comm", fn, name))
@@ -55,6 +60,8 @@ class StepProgram:
         return res
 
     def wait(self, name: str):
+        for h in self.before_comm:
+            h()
         if self.recording:
             self._cut()
             self.items.append(("wait", None, name))
@@ -96,9 +103,21 @@ class StepProgram:
             with torch.cuda.stream(self._stream):
                 self._begin()
                 out = step_fn()
+                for h in self.before_comm:
+                    h()
                 self._cut()
         except BaseException:
+            import sys
+            import traceback
+
+            traceback.print_exc(file=sys.stderr)
+            sys.stderr.flush()
             # never leave the stream in capture mode (the process would abort at teardown)
+            for h in self.before_comm:
+                try:
+                    h()
+                except Exception:
+                    pass
             if self._graph is not None:
                 try:
                     self._graph.capture_end()

@@ -66,7 +66,8 @@ class Engine:
         self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu)
         self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program)
         self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
-                              act_dtype=self.act_dtype)
+                              act_dtype=self.act_dtype, side_stream=on_gpu)
+        self.program.before_comm.append(self.stage.side.join)
         self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb)
         self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,
                               pp_global_clip=(train_cfg.pp_clip == "global"))
@@ -95,6 +96,8 @@ class Engine:
         from ..ops.gemm import reserve_workspace
 
         reserve_workspace(self.device, 64 << 20)
+        if self.stage.side.stream is not None:
+            reserve_workspace(self.device, 64 << 20, role="side")
 
     @property
     def tokens_per_step(self) -> int:
@@ -123,6 +126,7 @@ class Engine:
         bk = self.buckets
         dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=lambda l: bk.ready_upto(bk.layer_end_offset(l)))
         st.embed_backward(ctx, dx, step, 0.0)
+        st.side.join()
         self.buckets.ready_all()
         self.buckets.wait_all()
         self._loss_allreduce()
@@ -144,6 +148,7 @@ class Engine:
         from ..parallel.pp import run_pipeline
 
         run_pipeline(self)
+        self.stage.side.join()
         self.buckets.ready_all()
         self.buckets.wait_all()
         self._loss_allreduce()

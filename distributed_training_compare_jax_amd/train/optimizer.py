@@ -21,6 +21,22 @@ from ..ops import optim as O
 from ..parallel.buffers import FlatParams
 
 
+def merge_segments(segs, total: int):
+    """Coalesce per-parameter (offset, len, weight) into maximal ranges of equal weight.
+
+    Alignment gaps between params are zero in the grad buffer, so each range may absorb the gap
+    up to the next param; at tp=1 the whole buffer becomes ONE range (a single streaming pass)."""
+    segs = sorted(segs)
+    out = []
+    for i, (o, n, w) in enumerate(segs):
+        end = segs[i + 1][0] if i + 1 < len(segs) else total
+        if out and out[-1][2] == w and out[-1][0] + out[-1][1] == o:
+            out[-1] = (out[-1][0], end - out[-1][0], w)
+        else:
+            out.append((o, end - o, w))
+    return out
+
+
 class FusedAdamW:
     def __init__(self, flat: FlatParams, cfg: OptimConfig, program, tp_size: int = 1, tp_group=None,
                  pp_group=None, pp_global_clip: bool = False):
@@ -31,7 +47,7 @@ class FusedAdamW:
         self.pp_group = pp_group if pp_global_clip else None
         dev = flat.device
         w = (lambda spec: 1.0 if spec.tp != "rep" else 1.0 / tp_size)
-        self.segments = O.make_segments(flat.segments(w), dev)
+        self.segments = O.make_segments(merge_segments(flat.segments(w), flat.numel), dev)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
 

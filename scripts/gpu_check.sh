@@ -23,6 +23,7 @@ for s in $STEPS; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py --steps 30 --warmup 5 ;;
     benchng) run benchng 600 python bench.py --steps 20 --warmup 3 --no_graph ;;
+    gemmb)   run gemmb 600 python benchmarks/gemm_bench.py --json gpurun_out/gemm_bench.json ;;
     prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o prof --output-format csv -- python bench.py --steps 10 --warmup 3 ;;
   esac
 done
