@@ -225,6 +225,11 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, l
   }
 }
 
+__global__ void zero4_kernel(f32x4* __restrict__ x, long n4) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n4) x[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
 __global__ void fill_kernel(float* __restrict__ x, float v, long n) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = v;
@@ -251,9 +256,10 @@ int dtc_embed_fwd(const int* ids, const float* wte, const float* wpe, float* h, 
 int dtc_embed_bwd(const int* ids, const float* dh, float* dwte, float* dwpe, int B, int T, int D, int V, float p,
                   long seed, const int64_t* step, long row0, int accumulate, hipStream_t st) {
   if (D % 4) return 3001;
-  if (!accumulate) {
-    hipError_t e = hipMemsetAsync(dwte, 0, (size_t)V * D * sizeof(float), st);
-    if (e != hipSuccess) return (int)e;
+  if (!accumulate) {  // zero the table with a kernel node (not a memset node) before the scatter
+    long n4 = (long)V * D / 4;
+    hipLaunchKernelGGL(zero4_kernel, dim3(blocks_for(n4, 256)), dim3(256), 0, st, (f32x4*)dwte, n4);
+    DTC_CHECK_LAUNCH();
   }
   long n = (long)T * (D / 4);
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ids, dh, dwte, dwpe, B, T, D, p,

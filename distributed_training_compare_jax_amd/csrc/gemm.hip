@@ -363,6 +363,11 @@ struct Plan {
 // allow_split: 1 = small-grid split (wgrad), 2 = huge-K only (dgrad through the lm_head)
 Plan make_plan(int M, int N, int K, int allow_split) {
   Plan p{128, 128, 64, 1};
+  if (K % 64) {  // K a multiple of 32 only (e.g. a TP shard of d_model=768): BK=32, small tiles
+    p.bm = p.bn = 64;
+    p.bk = 32;
+    return p;
+  }
   const int nk = K / 64;
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
   if (allow_split && K >= 8192 && t128 >= 32) {  // e.g. dH = dlogits . W_lm (K = vocab)
@@ -392,17 +397,24 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
   int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   e.nparts = tiles_n * 2;
-  const int nk = a.K / 64;
-  const int kps = ((nk + p.split - 1) / p.split) * 64;
+  const int nk = a.K / p.bk;
+  const int kps = ((nk + p.split - 1) / p.split) * p.bk;
   const int ntiles = tiles_m * tiles_n;
   // per-XCD share of tiles = ntiles*split/8: with few N-tiles make each XCD own whole M-row groups
   int gm = tiles_m;
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
   dim3 grid(ntiles * p.split);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st,
-                     (const bf16*)a.A, a.lda, operand_bytes(AK, a.M, a.K, a.lda), (const bf16*)a.B, a.ldb,
-                     operand_bytes(BKM, a.N, a.K, a.ldb), a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split,
-                     kps, (float*)a.workspace, e);
+  const int ab = operand_bytes(AK, a.M, a.K, a.lda), bb = operand_bytes(BKM, a.N, a.K, a.ldb);
+  if (BM == 64 && p.bk == 32)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A, a.lda,
+                       ab, (const bf16*)a.B, a.ldb, bb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
+                       (float*)a.workspace, e);
+  else if (p.bk == 64)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A, a.lda,
+                       ab, (const bf16*)a.B, a.ldb, bb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
+                       (float*)a.workspace, e);
+  else
+    return 1007;
   DTC_CHECK_LAUNCH();
   if (p.split > 1) {
     long MN = (long)a.M * a.N;
@@ -432,14 +444,17 @@ long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
 }
 
 int dtc_gemm(const GemmArgs* a, hipStream_t st) {
-  if (a->K % 64 != 0) return 1001;               // K must be a multiple of BK=64
+  if (a->K % 32 != 0) return 1001;               // K must be a multiple of 32 (BK = 64, or 32)
   if (a->lda % 8 || a->ldb % 8 || a->ldc % 4) return 1002;  // 16-B row alignment
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
   if (a->layout == 0) {
     Plan p = make_plan(a->M, a->N, a->K, 0);
-    if (epi == EPI_LMHEAD) { p.bm = p.bn = 128; return launch_t<128, 128, true, true, EPI_LMHEAD, false>(*a, p, st); }
+    if (epi == EPI_LMHEAD) {
+      if (p.bk != 64) return 1008;
+      p.bm = p.bn = 128;
+      return launch_t<128, 128, true, true, EPI_LMHEAD, false>(*a, p, st); }
     if (epi == EPI_GELU) return launch_sz<true, true, EPI_GELU, false>(*a, p, st);
     if (epi == EPI_RESID) return launch_sz<true, true, EPI_RESID, true>(*a, p, st);
     if (epi == EPI_STORE) return f32 ? launch_sz<true, true, EPI_STORE, true>(*a, p, st)

@@ -48,6 +48,9 @@ def init_distributed(device: str = "auto", timeout_s: float = 600.0) -> DistInfo
     else:
         dev = torch.device("cpu")
         backend = "gloo"
+    # DTC_DIST_BACKEND=gloo runs several GPU ranks on ONE GPU (RCCL refuses duplicate devices):
+    # the 1-GPU test box uses it to exercise the multi-rank GPU code paths (graphs + collectives).
+    backend = os.environ.get("DTC_DIST_BACKEND", backend)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
@@ -56,6 +59,11 @@ def init_distributed(device: str = "auto", timeout_s: float = 600.0) -> DistInfo
             kw["device_id"] = dev
         dist.init_process_group(**kw)
     return DistInfo(rank, world, local_rank, dev, backend)
+
+
+def staged_p2p() -> bool:
+    """True when point-to-point traffic of GPU tensors must go through host memory (gloo)."""
+    return is_dist() and dist.get_backend() == "gloo"
 
 
 def is_dist() -> bool:

@@ -25,6 +25,25 @@ import torch
 import torch.distributed as dist
 
 from ..ops.optim import cast_to_bf16, fill_
+from .dist import staged_p2p
+
+
+class _HostSend:
+    """isend of a device tensor through a host copy (gloo backend); ``wait()`` like a Work."""
+
+    def __init__(self, t, dst):
+        self.host = t.detach().to("cpu")
+        self.work = dist.isend(self.host, dst)
+
+    def wait(self):
+        self.work.wait()
+        self.host = None
+
+
+def _host_recv(buf, src):
+    host = torch.empty(buf.shape, dtype=buf.dtype)
+    dist.recv(host, src)
+    buf.copy_(host)
 
 
 def _schedule(kind: str, S: int, s: int, M: int) -> List[tuple]:
@@ -65,13 +84,21 @@ def run_pipeline(eng) -> None:
     if not last:
         fill_(eng.loss, 0.0)
 
+    staged = staged_p2p() and eng.device.type == "cuda"
+
     def isend(t, dst, tag):
         name = f"send_{tag}"
-        prog.comm(lambda: dist.isend(t, dst), name=name)
+        if staged:  # gloo carries host tensors only: stage through pinned host memory
+            prog.comm(lambda: _HostSend(t, dst), name=name)
+        else:
+            prog.comm(lambda: dist.isend(t, dst), name=name)
         sends.append(name)
 
     def recv(buf, src, tag):
         name = f"recv_{tag}"
+        if staged:
+            prog.comm(lambda: _host_recv(buf, src), name=None)
+            return
         prog.comm(lambda: dist.irecv(buf, src), name=name)
         prog.wait(name)
 

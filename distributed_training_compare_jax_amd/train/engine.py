@@ -10,6 +10,7 @@ segments after the first eager warmup step.
 
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -66,7 +67,8 @@ class Engine:
         self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu)
         self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program)
         self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
-                              act_dtype=self.act_dtype, side_stream=on_gpu)
+                              act_dtype=self.act_dtype,
+                              side_stream=on_gpu and os.environ.get("DTC_NO_SIDE_STREAM", "0") != "1")
         self.program.before_comm.append(self.stage.side.join)
         self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb)
         self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,

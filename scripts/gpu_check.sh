@@ -20,6 +20,7 @@ for s in $STEPS; do
     kernels) run kernels 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x -rf ;;
     engine)  run engine 600 python -m pytest tests/test_engine_gpu.py -q -m gpu -rf ;;
     gpu)     run gpu 900 python -m pytest tests -q -m gpu -rf ;;
+    dist)    run dist 900 python -m pytest tests/test_dist_gpu.py -q -m gpu -rf ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py --steps 30 --warmup 5 ;;
     benchng) run benchng 600 python bench.py --steps 20 --warmup 3 --no_graph ;;

@@ -33,7 +33,7 @@ def _close(a, b, rtol, name=""):
     assert err <= rtol * ref, f"{name}: max abs err {err:.3e} vs ref max {ref:.3e} (rel {err / ref:.2e})"
 
 
-GEMM_SHAPES = [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048), (256, 384, 128),
+GEMM_SHAPES = [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048), (256, 384, 128), (512, 768, 96),
                (200, 136, 64), (4096, 50304, 512)]
 
 
@@ -61,7 +61,8 @@ def test_gemm_resid_gelu(cuda):
     _close(g, G.gelu_tanh(uref), 1e-2, "gelu_g")
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 512, 1536), (4096, 2048, 512), (4096, 512, 50304), (256, 128, 64)])
+@pytest.mark.parametrize("M,N,K", [(4096, 512, 1536), (4096, 2048, 512), (4096, 512, 50304), (256, 128, 64), (256, 64, 96),
+                                   (256, 32, 64)])
 def test_gemm_nn(cuda, M, N, K):
     dy, w = _r(M, K, seed=5), _r(K, N, scale=0.05, seed=6)
     dx = G.matmul_nn(dy, w)
