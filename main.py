@@ -50,10 +50,17 @@ def _spawn_target(args):
 @click.option("--nproc", type=int, default=None, help="ranks to spawn (default: all visible GPUs, else 1)")
 @click.option("--steps", type=int, default=None, help="override train_config.steps")
 @click.option("--device", type=click.Choice(["auto", "cuda", "cpu"]), default=None)
-def main(train_config_path: str, model_config_path: str, optim_config_path: str, nproc, steps, device):
+@click.option("--log_every", type=int, default=None, help="override train_config.log_every")
+@click.option("--warmup_steps", type=int, default=None, help="override the 5 untimed warmup steps")
+def main(train_config_path: str, model_config_path: str, optim_config_path: str, nproc, steps, device, log_every,
+         warmup_steps):
     overrides = {}
     if steps is not None:
         overrides["steps"] = steps
+    if log_every is not None:
+        overrides["log_every"] = log_every
+    if warmup_steps is not None:
+        overrides["warmup_steps"] = warmup_steps
     if device is not None:
         overrides["device"] = device
     args = (train_config_path, model_config_path, optim_config_path, overrides)
