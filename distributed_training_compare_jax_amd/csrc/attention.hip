@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restri
                                                             bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
-  __shared__ __attribute__((aligned(16))) bf16 lds[4 * 32 * L::VLD];
+  __shared__ __attribute__((aligned(16))) bf16 lds[4 * 64 * L::VLD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int nkb = (T + 63) / 64;
   const int kb = (int)(blockIdx.x % nkb);  // kb 0 (sweeps all queries, heaviest) launches first
@@ -260,10 +260,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restri
   for (int t = 0; t < HT; ++t) { dk[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
 
   auto body = [&](const bf16* sQ, const bf16* sD, int it) {
-    const int q0 = kb * 64 + 32 * it;
-    f32x4 p[2], ds[2];
+    const int q0 = kb * 64 + 64 * it;  // 64 queries per pipeline step (4 MFMA row tiles)
+    f32x4 p[4], ds[4];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < 4; ++qt) {
       f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
@@ -282,15 +282,18 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restri
         ds[qt][r] = pv * (dp[r] - d4[r]);
       }
     }
-    const bf16x8 pb = pack_p(p[0], p[1]), dsb = pack_p(ds[0], ds[1]);
 #pragma unroll
-    for (int t = 0; t < HT; ++t) {
-      dv[t] = mfma(tr_frag(sD, L::VLD, 0, t * 16, lane), pb, dv[t]);   // dV^T[hd][key] += dO^T P
-      dk[t] = mfma(tr_frag(sQ, L::VLD, 0, t * 16, lane), dsb, dk[t]);  // dK^T[hd][key] += Q^T dS
+    for (int hq = 0; hq < 2; ++hq) {  // two 32-query k-chunks of the dV / dK products
+      const bf16x8 pb = pack_p(p[2 * hq], p[2 * hq + 1]), dsb = pack_p(ds[2 * hq], ds[2 * hq + 1]);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        dv[t] = mfma(tr_frag(sD, L::VLD, 32 * hq, t * 16, lane), pb, dv[t]);   // dV^T[hd][key] += dO^T P
+        dk[t] = mfma(tr_frag(sQ, L::VLD, 32 * hq, t * 16, lane), dsb, dk[t]);  // dK^T[hd][key] += Q^T dS
+      }
     }
   };
-  const int nq = (T - kb * 64 + 31) / 32;
-  pipelined_tiles<HD, 32>(nq, [kb](int it) { return kb * 64 + 32 * it; }, Qb, ts, dOb, dts, T, lds, L::VLD, L::VLD,
+  const int nq = (T - kb * 64 + 63) / 64;
+  pipelined_tiles<HD, 64>(nq, [kb](int it) { return kb * 64 + 64 * it; }, Qb, ts, dOb, dts, T, lds, L::VLD, L::VLD,
                           tid, body);
   if (key < T) {
     bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
@@ -311,7 +314,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
                                                           bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
-  __shared__ __attribute__((aligned(16))) bf16 lds[4 * 32 * L::VLD];
+  __shared__ __attribute__((aligned(16))) bf16 lds[4 * 64 * L::VLD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int nqb = (T + 63) / 64;
   const int qb = nqb - 1 - (int)(blockIdx.x % nqb);
@@ -336,10 +339,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
   for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kend = min(T, qb * 64 + 64);
   auto body = [&](const bf16* sK, const bf16* sV, int it) {
-    const int k0 = 32 * it;
-    f32x4 ds[2];
+    const int k0 = 64 * it;  // 64 keys per pipeline step
+    f32x4 ds[4];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < 4; ++kt) {
       f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
@@ -353,11 +356,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
         ds[kt][r] = pv * (dp[r] - dq_);
       }
     }
-    const bf16x8 dsb = pack_p(ds[0], ds[1]);
 #pragma unroll
-    for (int t = 0; t < HT; ++t) acc[t] = mfma(tr_frag(sK, L::VLD, 0, t * 16, lane), dsb, acc[t]);  // dQ^T += K^T dS^T
+    for (int hk = 0; hk < 2; ++hk) {
+      const bf16x8 dsb = pack_p(ds[2 * hk], ds[2 * hk + 1]);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) acc[t] = mfma(tr_frag(sK, L::VLD, 32 * hk, t * 16, lane), dsb, acc[t]);  // dQ^T += K^T dS^T
+    }
   };
-  pipelined_tiles<HD, 32>((kend + 31) / 32, [](int it) { return 32 * it; }, Kb, ts, Vb, ts, T, lds, L::VLD, L::VLD,
+  pipelined_tiles<HD, 64>((kend + 63) / 64, [](int it) { return 64 * it; }, Kb, ts, Vb, ts, T, lds, L::VLD, L::VLD,
                           tid, body);
   if (q < T) {
     bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;

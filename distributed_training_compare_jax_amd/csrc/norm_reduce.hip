@@ -51,94 +51,120 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-constexpr int LN_BWD_ROWS = 16;  // rows per block (4 waves x 4 rows): 256 blocks at M=4096
+constexpr int LN_BWD_ROWS = 8;  // rows per block (4 waves x 2 rows, processed together): 512 blocks at M=4096
 
+// LayerNorm backward, 2 rows per wave with all loads issued before the two row reductions (ILP),
+// fused residual-gradient add, bf16 copy of dx, and per-block column partials of
+//   slab 0: sum dy*xhat (dgamma)   slab 1: sum dy (dbeta)   slab 2: sum dx (the bias grad of the
+//   layer whose OUTPUT gradient dx is: out_proj.b / fc2.b — saves a separate colsum pass)
 template <int NV>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy, int dy_f32, const float* __restrict__ x,
                                                      const float* __restrict__ g, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ dres,
                                                      float* __restrict__ dx, bf16* __restrict__ dx_c,
-                                                     float* __restrict__ part, int M, int D) {
+                                                     float* __restrict__ part, int nslab, int M, int D) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int D4 = D / 4;
-  f32x4 ag[NV], ab[NV];
+  f32x4 ag[NV], ab[NV], ao[NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) { ag[i] = f32x4{0.f, 0.f, 0.f, 0.f}; ab[i] = ag[i]; }
-  for (int rr = wave; rr < LN_BWD_ROWS; rr += 4) {
-    const int row = blockIdx.x * LN_BWD_ROWS + rr;
-    if (row >= M) break;
-    const float mu = mean[row], rs = rstd[row];
-    f32x4 xh[NV], d[NV];
-    float s1 = 0.f, s2 = 0.f;
+  for (int i = 0; i < NV; ++i) { ag[i] = f32x4{0.f, 0.f, 0.f, 0.f}; ab[i] = ag[i]; ao[i] = ag[i]; }
+  const int r0 = blockIdx.x * LN_BWD_ROWS + wave * 2;
+  f32x4 xh[2][NV], d[2][NV], rs_[2];
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, rsv[2] = {0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int row = r0 + q;
+    const bool ok = row < M;
+    const float mu = ok ? mean[row] : 0.f;
+    rsv[q] = ok ? rstd[row] : 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      int c = lane + 64 * i;
-      if (c < D4) {
-        f32x4 xv = ((const f32x4*)(x + (long)row * D))[c];
-        f32x4 dv;
+      const int c = lane + 64 * i;
+      f32x4 xv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+      if (ok && c < D4) {
+        xv = ((const f32x4*)(x + (long)row * D))[c];
         if (dy_f32) dv = ((const f32x4*)((const float*)dy + (long)row * D))[c];
         else { bf16x4 t = ((const bf16x4*)((const bf16*)dy + (long)row * D))[c]; dv = f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]}; }
-        xh[i] = (xv - mu) * rs;
-        d[i] = dv;
-        f32x4 gd = dv * ((const f32x4*)g)[c];
-        s1 += gd[0] + gd[1] + gd[2] + gd[3];
-        f32x4 t2 = gd * xh[i];
-        s2 += t2[0] + t2[1] + t2[2] + t2[3];
-        ag[i] += dv * xh[i];
-        ab[i] += dv;
       }
+      xh[q][i] = (xv - mu) * rsv[q];
+      d[q][i] = dv;
     }
-    const float c1 = warp_sum(s1) / D, c2 = warp_sum(s2) / D;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      int c = lane + 64 * i;
+      const int c = lane + 64 * i;
       if (c < D4) {
-        f32x4 gd = d[i] * ((const f32x4*)g)[c];
-        f32x4 o = (gd - c1 - xh[i] * c2) * rs;
+        f32x4 gd = d[q][i] * ((const f32x4*)g)[c];
+        s1[q] += gd[0] + gd[1] + gd[2] + gd[3];
+        f32x4 t2 = gd * xh[q][i];
+        s2[q] += t2[0] + t2[1] + t2[2] + t2[3];
+        ag[i] += d[q][i] * xh[q][i];
+        ab[i] += d[q][i];
+      }
+    }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int row = r0 + q;
+    const float c1 = warp_sum(s1[q]) / D, c2 = warp_sum(s2[q]) / D;
+    if (row >= M) continue;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D4) {
+        f32x4 gd = d[q][i] * ((const f32x4*)g)[c];
+        f32x4 o = (gd - c1 - xh[q][i] * c2) * rsv[q];
         if (dres) o += ((const f32x4*)(dres + (long)row * D))[c];
         ((f32x4*)(dx + (long)row * D))[c] = o;
         if (dx_c) ((bf16x4*)(dx_c + (long)row * D))[c] = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+        ao[i] += o;
       }
     }
   }
-  // block reduce of the dgamma/dbeta partials over the 4 waves (fixed order)
-  __shared__ __attribute__((aligned(16))) float red[4][2][1024];
-  float* mine = &red[wave][0][0];
+  (void)rs_;
+  // block reduce of the column partials over the 4 waves (fixed order); part[block][nslab][D]
+  __shared__ __attribute__((aligned(16))) float red[4][3][NV * 256];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    int c = lane + 64 * i;
-    if (c < D4 && c < 256) { ((f32x4*)mine)[c] = ag[i]; ((f32x4*)(mine + 1024))[c] = ab[i]; }
+    const int c = lane + 64 * i;
+    ((f32x4*)red[wave][0])[c] = ag[i];
+    ((f32x4*)red[wave][1])[c] = ab[i];
+    ((f32x4*)red[wave][2])[c] = ao[i];
   }
   __syncthreads();
-  // partial layout: part[block][2][D]
   for (int c = threadIdx.x; c < D; c += 256) {
-    float sg = 0.f, sb = 0.f;
-    if (c < 1024) {
-      for (int w = 0; w < 4; ++w) { sg += red[w][0][c]; sb += red[w][1][c]; }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      if (s >= nslab) break;
+      const float v = (red[0][s][c] + red[1][s][c]) + (red[2][s][c] + red[3][s][c]);
+      part[((long)blockIdx.x * nslab + s) * D + c] = v;
     }
-    part[((long)blockIdx.x * 2 + 0) * D + c] = sg;
-    part[((long)blockIdx.x * 2 + 1) * D + c] = sb;
   }
 }
 
-// out (+)= sum_p part[p*C + c], c in [0, C); columns [0, split_c) go to o0, the rest to o1.
-// Block = 64 columns x 4 partial groups (coalesced 256-B row reads), LDS tree for the groups.
+// out (beta*out +)= sum_p part[p*C + c], c in [0, C), the C columns cut into segments of `seg`
+// columns routed to o0 / o1 / o2.  Block = 16 columns x 16 partial groups (64-B row segments),
+// LDS tree over the groups — deterministic order, short per-thread chains (P/16 loads).
+constexpr int SR_COLS = 16, SR_GROUPS = 256 / SR_COLS;
 __global__ void __launch_bounds__(256) slab_reduce(const float* __restrict__ part, int P, int C, float* __restrict__ o0,
-                                                   float* __restrict__ o1, int split_c, float beta) {
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+                                                   float* __restrict__ o1, float* __restrict__ o2, int seg, float beta) {
+  const int tx = threadIdx.x % SR_COLS, ty = threadIdx.x / SR_COLS;
+  const int c = blockIdx.x * SR_COLS + tx;
   float s = 0.f;
   if (c < C) {
 #pragma unroll 4
-    for (int p = ty; p < P; p += 4) s += part[(long)p * C + c];
+    for (int p = ty; p < P; p += SR_GROUPS) s += part[(long)p * C + c];
   }
-  __shared__ float red[4][64];
+  __shared__ float red[SR_GROUPS][SR_COLS];
   red[ty][tx] = s;
   __syncthreads();
   if (ty == 0 && c < C) {
-    const float t = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
-    float* o = c < split_c ? o0 : o1;
-    const int col = c < split_c ? c : c - split_c;
+    float t = 0.f;
+#pragma unroll
+    for (int gq = 0; gq < SR_GROUPS; ++gq) t += red[gq][tx];
+    const int which = c / seg, col = c % seg;
+    float* o = which == 0 ? o0 : (which == 1 ? o1 : o2);
     o[col] = beta != 0.f ? beta * o[col] + t : t;
   }
 }
@@ -210,21 +236,22 @@ int dtc_layernorm_fwd(const float* x, const float* g, const float* b, void* y, f
 
 long dtc_layernorm_bwd_workspace_bytes(int M, int D) {
   long blocks = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
-  return blocks * 2 * D * 4;
+  return blocks * 3 * D * 4;
 }
 
 int dtc_layernorm_bwd(const void* dy, int dy_f32, const float* x, const float* g, const float* mean, const float* rstd,
-                      const float* dres, float* dx, bf16* dx_c, float* dg, float* db, int M, int D, int accumulate,
-                      float* ws, long ws_bytes, hipStream_t st) {
+                      const float* dres, float* dx, bf16* dx_c, float* dg, float* db, float* dbias, int M, int D,
+                      int accumulate, float* ws, long ws_bytes, hipStream_t st) {
   if (D % 4 || D > 1024) return 2002;  // dgamma/dbeta block reduce holds D <= 1024 in LDS
   int blocks = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
   if (ws_bytes < dtc_layernorm_bwd_workspace_bytes(M, D)) return 2003;
   int nv = (D / 4 + 63) / 64;
+  const int nslab = dbias ? 3 : 2;
   DTC_NV_SWITCH(nv, hipLaunchKernelGGL(ln_bwd_kernel<NVC>, dim3(blocks), dim3(256), 0, st, dy, dy_f32, x, g, mean, rstd,
-                                       dres, dx, dx_c, ws, M, D));
+                                       dres, dx, dx_c, ws, nslab, M, D));
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_reduce, dim3((2 * D + 63) / 64), dim3(256), 0, st, ws, blocks, 2 * D, dg, db, D,
-                     accumulate ? 1.f : 0.f);
+  hipLaunchKernelGGL(slab_reduce, dim3((nslab * D + SR_COLS - 1) / SR_COLS), dim3(256), 0, st, ws, blocks, nslab * D, dg, db, dbias,
+                     D, accumulate ? 1.f : 0.f);
   DTC_CHECK_LAUNCH();
   return 0;
 }
@@ -239,14 +266,14 @@ int dtc_colsum(const void* dy, int is_f32, int M, int N, long ld, float* out, fl
   dim3 g1((N + 255) / 256, P);
   hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, st, dy, is_f32, M, N, ld, ws);
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_reduce, dim3((N + 63) / 64), dim3(256), 0, st, ws, P, N, out, out, N, beta);
+  hipLaunchKernelGGL(slab_reduce, dim3((N + SR_COLS - 1) / SR_COLS), dim3(256), 0, st, ws, P, N, out, out, out, N, beta);
   DTC_CHECK_LAUNCH();
   return 0;
 }
 
 // generic ordered reduction of fp32 partial slabs: out (beta*out +) sum_p part[p][c]
 int dtc_slab_reduce(const float* part, int P, int C, float* out, float beta, hipStream_t st) {
-  hipLaunchKernelGGL(slab_reduce, dim3((C + 63) / 64), dim3(256), 0, st, part, P, C, out, out, C, beta);
+  hipLaunchKernelGGL(slab_reduce, dim3((C + SR_COLS - 1) / SR_COLS), dim3(256), 0, st, part, P, C, out, out, out, C, beta);
   DTC_CHECK_LAUNCH();
   return 0;
 }

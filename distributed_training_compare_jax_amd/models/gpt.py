@@ -89,6 +89,7 @@ class GPTStage:
                  dropout_seed: int = 0, act_dtype: torch.dtype = torch.bfloat16, side_stream: bool = True):
         self.cfg = cfg
         self.side = SideStream(flat.device, side_stream)
+        self._bias_fused = set()  # layers whose fc2.b grad an upstream LN backward already produced
         self.flat = flat
         self.layout = layout
         self.tp = tp if tp is not None else NoComm()
@@ -141,17 +142,24 @@ class GPTStage:
         x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch = ctx.pop(l)
         T = x.shape[0] // batch
         side = self.side
+        # fc2.b's gradient = Σ_rows dx3 was already emitted by the LayerNorm backward that produced
+        # dx3 (lnf or the next block's ln1) unless dx3 arrived from another pipeline stage
+        fc2b_fused = l in self._bias_fused
+        self._bias_fused.discard(l)
         # MLP (dgrad chain on the main stream, weight grads on the side stream)
-        side.run(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), G.colsum(dx3, f.g(p + "fc2.b"), beta)),
-                 dx3_c, gact, dx3)
+        if fc2b_fused:
+            side.run(lambda: G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), dx3_c, gact)
+        else:
+            side.run(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), G.colsum(dx3, f.g(p + "fc2.b"), beta)),
+                     dx3_c, gact, dx3)
         du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
         side.run(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta), G.colsum(du, f.g(p + "fc1.b"), beta)), du, y2)
         dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
         tp.all_reduce_(dy2)
-        dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta)
+        # LN2 backward also emits out_proj.b's gradient (Σ_rows dx2)
+        dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
         # attention
-        side.run(lambda: (G.wgrad(dx2_c, o, f.g(p + "out.w"), beta), G.colsum(dx2, f.g(p + "out.b"), beta)),
-                 dx2_c, o, dx2)
+        side.run(lambda: G.wgrad(dx2_c, o, f.g(p + "out.w"), beta), dx2_c, o)
         do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
         dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                           self.heads_local).view(batch * T, -1)
@@ -159,14 +167,21 @@ class GPTStage:
                  dqkv, y1)
         dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
         tp.all_reduce_(dy1)
-        return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta)
+        return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
 
-    def _ln_bwd(self, dy, x, ln: str, mu, rs, dres, beta):
+    def _prev_fc2b(self, l: int):
+        """fc2.b of the block feeding layer l's input, if this stage owns it (its grad = Σ_rows dx)."""
+        if (l - 1) in self.layout.layers:
+            self._bias_fused.add(l - 1)
+            return f"h.{l - 1}.fc2.b"
+        return None
+
+    def _ln_bwd(self, dy, x, ln: str, mu, rs, dres, beta, bias_grad: Optional[str] = None):
         f = self.flat
         dx_c = None if self.act_dtype == torch.float32 else torch.empty(dy.shape, dtype=self.act_dtype,
                                                                         device=dy.device)
         dx = LN.layernorm_bwd(dy, x, f.p(ln + ".g"), mu, rs, dres, f.g(ln + ".g"), f.g(ln + ".b"), beta,
-                              out_c=dx_c)
+                              out_c=dx_c, dbias=None if bias_grad is None else f.g(bias_grad))
         return dx, (dx if dx_c is None else dx_c)
 
     def stage_forward(self, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
@@ -203,7 +218,9 @@ class GPTStage:
         dyf = G.matmul_nn(dlogits, f.w("lm_head.w"))
         del logits, dlogits
         self.tp.all_reduce_(dyf)
-        return self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta)
+        last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None
+        return self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
+                            bias_grad=None if last is None else self._prev_fc2b(last))
 
     def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None):
         """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist."""

@@ -70,7 +70,7 @@ def _declare(lib):
         "dtc_gemm_workspace_bytes": ([i, i, i, i], l),
         "dtc_lmhead_nparts": ([i], i),
         "dtc_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
-        "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, vp], i),
+        "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, vp], i),
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, vp], i),
         "dtc_colsum_workspace_bytes": ([i, i], l),

@@ -40,11 +40,14 @@ def layernorm_fwd(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
 
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, g: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
                   dres: Optional[torch.Tensor], dg: torch.Tensor, db: torch.Tensor, beta: float = 0.0,
-                  out: Optional[torch.Tensor] = None, out_c: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, out_c: Optional[torch.Tensor] = None,
+                  dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Returns fp32 ``dx = dres + dLN/dx·dy``; writes ``dg/db = β·(dg/db) + Σ_rows`` (β ∈ {0, 1}).
 
     ``out`` may alias ``dres`` (in-place residual-gradient update); ``out_c`` (optional)
-    receives a compute-dtype (bf16) copy of ``dx`` — the next dgrad/wgrad GEMM operand."""
+    receives a compute-dtype (bf16) copy of ``dx`` — the next dgrad/wgrad GEMM operand.
+    ``dbias`` (optional) receives ``β·dbias + Σ_rows dx``: the bias gradient of the layer whose
+    output gradient ``dx`` is (out_proj.b / fc2.b), fused into the same pass."""
     M, D = x.shape
     if not x.is_cuda:
         xhat = (x.float() - mean[:, None]) * rstd[:, None]
@@ -63,6 +66,11 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, g: torch.Tensor, mean: torc
         else:
             dg.copy_(sg)
             db.copy_(sb)
+        if dbias is not None:
+            if beta != 0.0:
+                dbias.mul_(beta).add_(dx.sum(0))
+            else:
+                dbias.copy_(dx.sum(0))
         if out_c is not None:
             out_c.copy_(dx)
         if out is not None:
@@ -76,6 +84,6 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, g: torch.Tensor, mean: torc
     ws = _workspace(x.device, int(L.dtc_layernorm_bwd_workspace_bytes(M, D)))
     N.check(L.dtc_layernorm_bwd(dy.data_ptr(), 1 if dy.dtype == torch.float32 else 0, x.data_ptr(), g.data_ptr(),
                                 mean.data_ptr(), rstd.data_ptr(), N.ptr(dres), out.data_ptr(), N.ptr(out_c),
-                                dg.data_ptr(), db.data_ptr(), M, D, 1 if beta != 0.0 else 0,
+                                dg.data_ptr(), db.data_ptr(), N.ptr(dbias), M, D, 1 if beta != 0.0 else 0,
                                 ws.data_ptr(), ws.numel(), N.stream_ptr(x.device)), "dtc_layernorm_bwd")
     return out
