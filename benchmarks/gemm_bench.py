@@ -75,6 +75,9 @@ def main():
         us = timeit(lambda: G.colsum(dy, db), a.reps)
         rows.append(dict(op=f"colsum {tag}", us=round(us, 2)))
         print(f"colsum {tag:31s} {us:9.1f} us", flush=True)
+    # lm_head forward without the CE epilogue (isolates the epilogue cost)
+    x, w = r(M, D), r(V, D) * 0.05
+    rec(f"fwd  lm_head plain-epilogue [{M}x{V}x{D}]", timeit(lambda: G.linear(x, w, None), a.reps), 2 * M * V * D)
     qkv = r(8, 512, 3 * D)
     o, lse = A.attn_fwd(qkv, 16)
     fl = A.attn_flops(8, 512, 16, 32)
