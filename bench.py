@@ -71,7 +71,7 @@ def main():
                      pp_schedule=args.pp_schedule)
     oc = OptimConfig(lr=3e-4, weight_decay=0.1, grad_clip=1.0)
     eng = Engine(mc, tc, oc, dinfo)
-    data = get_batch_iterator(global_batch, mc.max_seq_len + 1, seed=0, row0=eng.row0, nrows=eng.b_local)
+    data = get_batch_iterator(global_batch, mc.max_seq_len + 1, seed=0, row0=eng.feed_row0, nrows=eng.feed_rows)
 
     for _ in range(args.warmup):
         eng.set_batch(next(data))

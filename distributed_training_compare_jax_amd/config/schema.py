@@ -15,7 +15,10 @@ are optional and default to the reference behaviour:
   reference's stage-local global-norm clip, ``create_train_step.py:190``; ``global``
   all-reduces the norm across stages).
 * ``TrainConfig.data`` (``synthetic`` | ``fineweb``), ``use_graph``, ``profile``,
-  ``dp_bucket_mb``, ``warmup_steps`` (reference hard-codes 5, ``train/train.py:64``),
+  ``dp_bucket_mb`` / ``dp_tail_mb`` (DP grad bucket sizes; the last bucket is kept small
+  because its all-reduce is exposed), ``dp_embed_gather`` (DP: all-gather the embedding
+  output grads and rebuild wte/wpe grads locally instead of all-reducing the 103 MB table),
+  ``warmup_steps`` (reference hard-codes 5, ``train/train.py:64``),
   ``grad_reduce_dtype``, ``ckpt_every``/``resume``.
 """
 
@@ -104,6 +107,8 @@ class TrainConfig:
     use_graph: bool = True
     profile: bool = False
     dp_bucket_mb: float = 64.0
+    dp_tail_mb: float = 16.0
+    dp_embed_gather: bool = True
     grad_reduce_dtype: str = "fp32"
     warmup_steps: int = 5
     ckpt_every: int = 0

@@ -50,33 +50,135 @@ __global__ void embed_fwd_kernel(const int* __restrict__ ids, const float* __res
   *(f32x4*)(h + tok * D + d) = v;
 }
 
-// One thread per (t, 4 channels): loops over the batch — dwpe is a deterministic sum, dwte rows
-// get fp32 atomics (rows repeat only for repeated tokens).
-__global__ void embed_bwd_kernel(const int* __restrict__ ids, const float* __restrict__ dh, float* __restrict__ dwte,
-                                 float* __restrict__ dwpe, int B, int T, int D, float p, uint32_t seed,
-                                 const int64_t* __restrict__ step, long row0, int accumulate) {
+// ---------------------------------------------------------------- embedding backward
+// Deterministic (no float atomics), so every DP rank that rebuilds dwte from the same gathered
+// tokens gets bit-identical rows, and two runs give bit-identical grads:
+//   1. embed_sort_kernel  (runs early, off the critical path: it only needs the ids)
+//      key = id << nb | token  -> one-block bitonic sort in LDS.  Keys are unique, so the sorted
+//      order (hence every summation order below) is a pure function of the ids.
+//   2. embed_piece_sums   pieces of 16-64 sorted keys: each run of equal ids inside a tile is summed
+//      in order into P[first position of the run]
+//   3. embed_segment_sum  per id: P[segment start] + P[each tile boundary inside the segment]
+//   dwpe: one thread per (t, 4 channels) sums over the batch in order.
+constexpr int SORT_MAX = 32768;
+
+__global__ void __launch_bounds__(1024) embed_sort_kernel(const int* __restrict__ ids, int n, int npad, int nb,
+                                                          uint32_t* __restrict__ keys) {
+  __shared__ uint32_t s[SORT_MAX];
+  for (int i = threadIdx.x; i < npad; i += 1024) s[i] = i < n ? ((uint32_t)ids[i] << nb) | (uint32_t)i : 0xFFFFFFFFu;
+  __syncthreads();
+  for (int k = 2; k <= npad; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < npad; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          uint32_t a = s[i], b = s[l];
+          if ((a > b) == ((i & k) == 0)) { s[i] = b; s[l] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = threadIdx.x; i < n; i += 1024) keys[i] = s[i];
+}
+
+__device__ __forceinline__ f32x4 dropped_row(const float* __restrict__ dh, long tok, int T, int D, int d, float p,
+                                             uint32_t thr, float sc, uint32_t seed, uint32_t step, long row0) {
+  f32x4 g = *(const f32x4*)(dh + tok * D + d);
+  if (p > 0.f) {
+    uint64_t grp = ((uint64_t)(row0 * T + tok) * D + d) >> 2;
+    u32x4 u = philox(grp, seed, step);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[r] = u[r] >= thr ? g[r] * sc : 0.f;
+  }
+  return g;
+}
+
+// grid (pieces, ceil(D/256)), 64 threads x 4 channels
+__global__ void __launch_bounds__(64) embed_piece_sums(const uint32_t* __restrict__ keys, int n, int nb, int piece,
+                                                       const float* __restrict__ dh, float* __restrict__ P, int T,
+                                                       int D, float p, uint32_t seed, const int64_t* __restrict__ step,
+                                                       long row0) {
+  const int d = (blockIdx.y * 64 + threadIdx.x) * 4;
+  if (d >= D) return;
+  const int q_beg = blockIdx.x * piece, q_end = min(n, q_beg + piece);
+  const uint32_t tmask = (1u << nb) - 1;
+  const uint32_t thr = drop_threshold(p), stp = (uint32_t)step[0];
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int start = q_beg;
+  uint32_t cur = keys[q_beg] >> nb;
+  for (int q0 = q_beg; q0 < q_end; q0 += 8) {
+    f32x4 g[8];
+    uint32_t id[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // 8 independent row loads in flight
+      const int q = min(q0 + u, q_end - 1);
+      const uint32_t key = keys[q];
+      id[u] = key >> nb;
+      g[u] = dropped_row(dh, key & tmask, T, D, d, p, thr, sc, seed, stp, row0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (q0 + u >= q_end) break;
+      if (id[u] != cur) {
+        *(f32x4*)(P + (long)start * D + d) = acc;
+        acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        start = q0 + u;
+        cur = id[u];
+      }
+      acc += g[u];
+    }
+  }
+  *(f32x4*)(P + (long)start * D + d) = acc;
+}
+
+// grid (n, ceil(D/256)), 64 threads; only the first key of each id does work.  Pieces of one id
+// start at its first key and at every piece boundary inside its run; they are fetched 8 at a time
+// (membership is monotone along the run) and added in order.
+__global__ void __launch_bounds__(64) embed_segment_sum(const uint32_t* __restrict__ keys, int n, int nb, int piece,
+                                                        const float* __restrict__ P, float* __restrict__ dwte, int D,
+                                                        int accumulate) {
+  const int s = blockIdx.x;
+  const uint32_t id = keys[s] >> nb;
+  if (s > 0 && (keys[s - 1] >> nb) == id) return;  // not the first occurrence of this id
+  const int d = (blockIdx.y * 64 + threadIdx.x) * 4;
+  if (d >= D) return;
+  f32x4 acc = *(const f32x4*)(P + (long)s * D + d);
+  for (int q = (s / piece + 1) * piece; q < n; q += 8 * piece) {
+    bool in[8];
+    f32x4 t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int qq = q + u * piece;
+      in[u] = qq < n && (keys[min(qq, n - 1)] >> nb) == id;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      t[u] = in[u] ? *(const f32x4*)(P + (long)(q + u * piece) * D + d) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bool more = true;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (!in[u]) { more = false; break; }
+      acc += t[u];
+    }
+    if (!more) break;
+  }
+  float* o = dwte + (long)id * D + d;
+  if (accumulate) acc += *(const f32x4*)o;
+  *(f32x4*)o = acc;
+}
+
+__global__ void wpe_bwd_kernel(const float* __restrict__ dh, float* __restrict__ dwpe, int B, int T, int D, float p,
+                               uint32_t seed, const int64_t* __restrict__ step, long row0, int accumulate) {
   const int D4 = D / 4;
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)T * D4) return;
   int t = (int)(i / D4);
   int d = (int)(i % D4) * 4;
-  uint32_t thr = drop_threshold(p);
-  float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = drop_threshold(p), stp = (uint32_t)step[0];
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int b = 0; b < B; ++b) {
-    long tok = (long)b * T + t;
-    f32x4 g = *(const f32x4*)(dh + tok * D + d);
-    if (p > 0.f) {
-      uint64_t grp = ((uint64_t)((row0 + b) * T + t) * D + d) >> 2;
-      u32x4 u = philox(grp, seed, (uint32_t)step[0]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) g[r] = u[r] >= thr ? g[r] * sc : 0.f;
-    }
-    acc += g;
-    float* w = dwte + (long)ids[tok] * D + d;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) atomicAdd(w + r, g[r]);
-  }
+  for (int b = 0; b < B; ++b) acc += dropped_row(dh, (long)b * T + t, T, D, d, p, thr, sc, seed, stp, row0);
   float* o = dwpe + (long)t * D + d;
   if (accumulate) acc += *(f32x4*)o;
   *(f32x4*)o = acc;
@@ -253,16 +355,47 @@ int dtc_embed_fwd(const int* ids, const float* wte, const float* wpe, float* h, 
   return 0;
 }
 
-int dtc_embed_bwd(const int* ids, const float* dh, float* dwte, float* dwpe, int B, int T, int D, int V, float p,
-                  long seed, const int64_t* step, long row0, int accumulate, hipStream_t st) {
+int dtc_embed_sort_bits(int n) {
+  int nb = 1;
+  while ((1 << nb) < n) ++nb;
+  return nb;
+}
+
+// keys[n] (uint32) = sorted (id << nb | token); n <= 32768 and V <= 2^(32-nb)
+int dtc_embed_sort(const int* ids, int n, int V, uint32_t* keys, hipStream_t st) {
+  if (n <= 0 || n > SORT_MAX) return 3003;
+  const int nb = dtc_embed_sort_bits(n);
+  if (nb < 32 && (long)V > (1L << (32 - nb))) return 3004;
+  int npad = 2;
+  while (npad < n) npad <<= 1;
+  hipLaunchKernelGGL(embed_sort_kernel, dim3(1), dim3(1024), 0, st, ids, n, npad, nb, keys);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// dwte (+)= scatter(ids, dropout'(dh)), dwpe (+)= sum_b dropout'(dh); keys from dtc_embed_sort,
+// P = n*D fp32 scratch.  Bitwise deterministic.
+int dtc_embed_bwd(const uint32_t* keys, const float* dh, float* dwte, float* dwpe, float* P, int B, int T, int D, int V,
+                  float p, long seed, const int64_t* step, long row0, int accumulate, hipStream_t st) {
   if (D % 4) return 3001;
-  if (!accumulate) {  // zero the table with a kernel node (not a memset node) before the scatter
+  const int n = B * T;
+  if (n > SORT_MAX) return 3003;
+  const int nb = dtc_embed_sort_bits(n);
+  if (!accumulate) {  // zero the table with a kernel node (not a memset node) before the row writes
     long n4 = (long)V * D / 4;
     hipLaunchKernelGGL(zero4_kernel, dim3(blocks_for(n4, 256)), dim3(256), 0, st, (f32x4*)dwte, n4);
     DTC_CHECK_LAUNCH();
   }
-  long n = (long)T * (D / 4);
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ids, dh, dwte, dwpe, B, T, D, p,
+  // piece length trades the sequential in-piece sum against the per-id walk over pieces
+  const int piece = n <= 4096 ? 16 : (n <= 16384 ? 32 : 64);
+  const int dblk = (D / 4 + 63) / 64;
+  hipLaunchKernelGGL(embed_piece_sums, dim3((n + piece - 1) / piece, dblk), dim3(64), 0, st, keys, n, nb, piece, dh, P,
+                     T, D, p, (uint32_t)seed, step, row0);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(embed_segment_sum, dim3(n, dblk), dim3(64), 0, st, keys, n, nb, piece, P, dwte, D, accumulate);
+  DTC_CHECK_LAUNCH();
+  long nt = (long)T * (D / 4);
+  hipLaunchKernelGGL(wpe_bwd_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, st, dh, dwpe, B, T, D, p,
                      (uint32_t)seed, step, row0, accumulate);
   DTC_CHECK_LAUNCH();
   return 0;
@@ -299,6 +432,21 @@ int dtc_sumsq_segments(const float* x, const double* seg, int S, float* out, int
   hipLaunchKernelGGL(sumsq_stage1, dim3(SS_BLOCKS), dim3(256), 0, st, x, seg, S, ws);
   DTC_CHECK_LAUNCH();
   hipLaunchKernelGGL(sumsq_stage2, dim3(1), dim3(1024), 0, st, ws, SS_BLOCKS, out, step);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// Incremental global norm: chunk i of the grads is reduced into part[0:nblocks] as soon as it
+// is final (overlapping backward); dtc_sum_finish sums all chunk partials in a fixed order.
+int dtc_sumsq_partial(const float* x, const double* seg, int S, float* part, int nblocks, hipStream_t st) {
+  if (nblocks <= 0) return 3006;
+  hipLaunchKernelGGL(sumsq_stage1, dim3(nblocks), dim3(256), 0, st, x, seg, S, part);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_sum_finish(const float* part, int P, float* out, int64_t* step, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_stage2, dim3(1), dim3(1024), 0, st, part, P, out, step);
   DTC_CHECK_LAUNCH();
   return 0;
 }

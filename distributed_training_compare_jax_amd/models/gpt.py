@@ -105,16 +105,40 @@ class GPTStage:
         self.eps = cfg.layernorm_eps
 
     # ------------------------------------------------------------------ embed
-    def embed_forward(self, ids: torch.Tensor, step: torch.Tensor, row0: int, ctx: Dict) -> torch.Tensor:
+    def embed_forward(self, ids: torch.Tensor, step: torch.Tensor, row0: int, ctx: Dict,
+                      want_keys: bool = True) -> torch.Tensor:
         """ids int32 [b, T] → h fp32 [b*T, D]  (wte gather + wpe + dropout, GPTModel.py:30-38)."""
         f = self.flat
-        ctx["embed"] = (ids, row0)
-        return E.embed_fwd(ids, f.p("wte"), f.p("wpe"), self.cfg.dropout, self.seed, step, row0)
+        h = E.embed_fwd(ids, f.p("wte"), f.p("wpe"), self.cfg.dropout, self.seed, step, row0)
+        ctx["embed"] = (ids, row0, self.embed_keys(ids) if want_keys else None)
+        return h
 
-    def embed_backward(self, ctx: Dict, dh: torch.Tensor, step: torch.Tensor, beta: float):
-        ids, row0 = ctx.pop("embed")
+    def embed_keys(self, ids: torch.Tensor):
+        """Sort keys for the deterministic embedding backward, computed on the side stream (they
+        depend only on the ids) so the sort is off the critical path."""
+        if not ids.is_cuda or ids.numel() > E.SORT_MAX:
+            return None  # CPU path / chunked backward sorts per chunk
+        # allocated on the main stream (its consumer); the side stream only writes it
+        keys = torch.empty(ids.numel(), dtype=torch.int32, device=ids.device)
+        self.side.run(lambda: E.embed_sort_keys(ids, self.flat.p("wte").shape[0], out=keys), ids)
+        ev = None
+        if self.side.stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(self.side.stream)
+        return keys, ev
+
+    def embed_backward(self, ctx: Dict, dh: torch.Tensor, step: torch.Tensor, beta: float, gathered=None):
+        """``gathered`` = (ids, row0, keys) of a DP-gathered batch whose ``dh`` rows were all-gathered
+        (every DP rank then builds the identical wte/wpe grads locally, no all-reduce)."""
+        ids, row0, keys = ctx.pop("embed")
+        if gathered is not None:
+            ids, row0, keys = gathered
+        if keys is not None:
+            keys, ev = keys
+            if ev is not None:  # keys were produced on the side stream
+                torch.cuda.current_stream().wait_event(ev)
         f = self.flat
-        E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta)
+        E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta, keys=keys)
 
     # ------------------------------------------------------------------ block
     def block_forward(self, l: int, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:

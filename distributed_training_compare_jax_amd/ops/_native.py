@@ -75,7 +75,9 @@ def _declare(lib):
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, vp], i),
         "dtc_colsum_workspace_bytes": ([i, i], l),
         "dtc_embed_fwd": ([vp, vp, vp, vp, i, i, i, i, f, l, vp, l, vp], i),
-        "dtc_embed_bwd": ([vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),
+        "dtc_embed_sort_bits": ([i], i),
+        "dtc_embed_sort": ([vp, i, i, vp, vp], i),
+        "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),
         "dtc_attn_fwd": ([vp, vp, vp, i, i, i, i, l, f, vp], i),
         "dtc_attn_bwd": ([vp, vp, vp, vp, vp, vp, i, i, i, i, l, f, vp, l, vp], i),
         "dtc_attn_bwd_workspace_bytes": ([i, i, i, i], l),
@@ -83,6 +85,8 @@ def _declare(lib):
         "dtc_ce_bwd": ([vp, l, vp, vp, i, i, i, i, f, vp], i),
         "dtc_sumsq_segments": ([vp, vp, i, vp, vp, vp, l, vp], i),
         "dtc_sumsq_workspace_bytes": ([], l),
+        "dtc_sumsq_partial": ([vp, vp, i, vp, i, vp], i),
+        "dtc_sum_finish": ([vp, i, vp, vp, vp], i),
         "dtc_adamw": ([vp, vp, vp, vp, vp, l, l, vp, vp, f, f, f, f, f, f, f, vp], i),
         "dtc_cast_f32_bf16": ([vp, vp, l, vp], i),
         "dtc_fill_f32": ([vp, f, l, vp], i),

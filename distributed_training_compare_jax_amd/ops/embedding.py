@@ -8,7 +8,7 @@ that GSPMD shards, ``train/create_train_step.py:31``).  The backward regenerates
 (nothing stored).  ``step`` is a device-resident int64 counter so the whole step can be
 replayed from a hipGraph.
 
-GPU path: ``csrc/embedding.hip``.  The CPU path below reproduces the kernel's Philox bits
+GPU path: ``csrc/elementwise.hip``.  The CPU path below reproduces the kernel's Philox bits
 exactly (tested).
 """
 
@@ -76,8 +76,11 @@ def embed_fwd(ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, p: float,
 
 
 def embed_bwd(ids: torch.Tensor, dh: torch.Tensor, dwte: torch.Tensor, dwpe: torch.Tensor, p: float, seed: int,
-              step: torch.Tensor, row0: int, beta: float = 0.0):
-    """dwte (β·)+= scatter_add(ids, dropout'(dh)); dwpe (β·)+= Σ_b dropout'(dh)."""
+              step: torch.Tensor, row0: int, beta: float = 0.0, keys: torch.Tensor = None):
+    """dwte (β·)+= scatter_add(ids, dropout'(dh)); dwpe (β·)+= Σ_b dropout'(dh).
+
+    GPU path is bitwise deterministic (sorted segment sums, no float atomics; see
+    ``csrc/elementwise.hip``); ``keys`` = :func:`embed_sort_keys` of ``ids`` if precomputed."""
     B, T = ids.shape
     D = dh.shape[1]
     if not ids.is_cuda:
@@ -91,6 +94,32 @@ def embed_bwd(ids: torch.Tensor, dh: torch.Tensor, dwte: torch.Tensor, dwpe: tor
         dwte.index_add_(0, ids.reshape(-1).long(), g)
         dwpe[:T].add_(g.view(B, T, D).sum(0))
         return
-    N.check(N.lib().dtc_embed_bwd(ids.data_ptr(), dh.data_ptr(), dwte.data_ptr(), dwpe.data_ptr(), B, T, D,
-                                  dwte.shape[0], p, seed, step.data_ptr(), row0, 1 if beta != 0.0 else 0,
+    if B * T > SORT_MAX:  # sort capacity of one workgroup: accumulate row chunks in order
+        rows = max(1, SORT_MAX // T)
+        for r0 in range(0, B, rows):
+            r1 = min(B, r0 + rows)
+            embed_bwd(ids[r0:r1], dh[r0 * T:r1 * T], dwte, dwpe, p, seed, step, row0 + r0,
+                      beta if r0 == 0 else 1.0)
+        return
+    if keys is None:
+        keys = embed_sort_keys(ids, dwte.shape[0])
+    assert keys.numel() == B * T and dh.shape[0] == B * T and dh.is_contiguous()
+    P = torch.empty(B * T, D, dtype=torch.float32, device=dh.device)
+    N.check(N.lib().dtc_embed_bwd(keys.data_ptr(), dh.data_ptr(), dwte.data_ptr(), dwpe.data_ptr(), P.data_ptr(), B,
+                                  T, D, dwte.shape[0], p, seed, step.data_ptr(), row0, 1 if beta != 0.0 else 0,
                                   N.stream_ptr(ids.device)), "dtc_embed_bwd")
+
+
+SORT_MAX = 32768  # keys one LDS bitonic sort handles (csrc/elementwise.hip)
+
+
+def embed_sort_keys(ids: torch.Tensor, vocab: int, out: torch.Tensor = None) -> torch.Tensor:
+    """Sorted ``id << nb | token`` keys (int32 storage of uint32) for the deterministic backward.
+
+    Depends only on the ids, so the step issues it right after the forward embedding, off the
+    critical path (side stream)."""
+    n = ids.numel()
+    keys = out if out is not None else torch.empty(n, dtype=torch.int32, device=ids.device)
+    N.check(N.lib().dtc_embed_sort(ids.data_ptr(), n, vocab, keys.data_ptr(), N.stream_ptr(ids.device)),
+            "dtc_embed_sort")
+    return keys

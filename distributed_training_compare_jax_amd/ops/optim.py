@@ -52,6 +52,33 @@ def sumsq_segments(flat: torch.Tensor, segments: torch.Tensor, out: torch.Tensor
     return out
 
 
+def sumsq_partial(flat: torch.Tensor, segments: torch.Tensor, part: torch.Tensor):
+    """part[:] = per-block partial Σ w·g² over ``segments`` (one chunk of an incremental norm)."""
+    if not flat.is_cuda:
+        acc = torch.zeros((), dtype=torch.float64)
+        for o, n, w in segments.tolist():
+            seg = flat[int(o):int(o) + int(n)].double()
+            acc += w * (seg * seg).sum()
+        part.zero_()
+        part[0] = float(acc)
+        return part
+    N.check(N.lib().dtc_sumsq_partial(flat.data_ptr(), segments.data_ptr(), segments.shape[0], part.data_ptr(),
+                                      part.numel(), N.stream_ptr(flat.device)), "dtc_sumsq_partial")
+    return part
+
+
+def sum_finish(part: torch.Tensor, out: torch.Tensor, step: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[0] = Σ part (fixed order, fp64 accumulate); bumps ``step`` if given."""
+    if not part.is_cuda:
+        out.fill_(float(part.double().sum()))
+        if step is not None:
+            step.add_(1)
+        return out
+    N.check(N.lib().dtc_sum_finish(part.data_ptr(), part.numel(), out.data_ptr(), N.ptr(step),
+                                   N.stream_ptr(part.device)), "dtc_sum_finish")
+    return out
+
+
 def adamw_flat(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                mirror: Optional[torch.Tensor], n_mirror: int, step: torch.Tensor, sumsq: torch.Tensor,
                lr: float, b1: float, b2: float, eps: float, wd: float, max_norm: float):

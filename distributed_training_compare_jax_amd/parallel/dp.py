@@ -23,37 +23,60 @@ from .buffers import FlatParams
 
 
 class GradBuckets:
-    def __init__(self, flat: FlatParams, group, dp: int, program, bucket_mb: float = 64.0):
+    """Contiguous buckets over the flat grad buffer, issued in backward order.
+
+    ``bucket_mb`` sizes the bulk buckets; the LAST bucket (complete only when backward ends,
+    so its all-reduce is exposed) is cut to about ``tail_mb``.  ``local_names`` are params
+    whose grads every rank computes identically on its own (the DP embedding gather); they must
+    form the tail of the buffer and are excluded from the all-reduce."""
+
+    def __init__(self, flat: FlatParams, group, dp: int, program, bucket_mb: float = 64.0, tail_mb: float = 16.0,
+                 local_names=()):
         self.flat = flat
         self.group = group
         self.dp = dp
         self.program = program
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
-        # param boundaries in flat (backward) order
-        bounds: List[Tuple[int, int]] = []
-        for s in flat.slots.values():
-            bounds.append((s.offset, s.offset + s.numel))
-        buckets: List[Tuple[int, int]] = []
+        tail_cap = max(1, int(tail_mb * 1024 * 1024 / 4))
+        end = flat.numel
+        if local_names:
+            lo, _ = flat.range_of(list(local_names))
+            rest = [s for n, s in flat.slots.items() if n not in local_names]
+            if any(s.offset >= lo for s in rest):
+                raise ValueError(f"local-grad params {local_names} must be the tail of the flat buffer")
+            end = lo
+        self.reduce_end = end
+        bounds: List[Tuple[int, int]] = [(s.offset, s.offset + s.numel) for s in flat.slots.values()
+                                         if s.offset < end]
+        # tail bucket: the last params adding up to ~tail_cap elements
+        i_tail = len(bounds)
+        acc = 0
+        while i_tail > 1 and acc < tail_cap:
+            i_tail -= 1
+            acc += bounds[i_tail][1] - bounds[i_tail][0]
+        cuts: List[int] = []  # exclusive end offsets of each bucket
         lo = None
-        hi = 0
-        for a, b in bounds:
-            if lo is None:
-                lo = a
-            hi = b
-            if hi - lo >= cap:
-                buckets.append((lo, self._pad(hi)))
+        for a, b in bounds[:i_tail]:
+            lo = a if lo is None else lo
+            if b - lo >= cap:
+                cuts.append(self._pad(b))
                 lo = None
-        if lo is not None:
-            buckets.append((lo, self._pad(hi)))
-        # make buckets tile the buffer contiguously (alignment gaps included)
-        fixed = []
+        if lo is not None:  # leftover: its own bucket, or folded into the previous one if small
+            c = self._pad(bounds[i_tail - 1][1])
+            if cuts and c - lo < cap // 2:
+                cuts[-1] = c
+            else:
+                cuts.append(c)
+        cuts.append(end)
+        # buckets tile [0, end) contiguously (alignment gaps included)
+        self.buckets = []
         prev = 0
-        for i, (a, b) in enumerate(buckets):
-            end = flat.numel if i == len(buckets) - 1 else b
-            fixed.append((prev, end))
-            prev = end
-        self.buckets = fixed
-        self.issued = [False] * len(fixed)
+        for c in cuts:
+            c = min(c, end)
+            if c > prev:
+                self.buckets.append((prev, c))
+                prev = c
+        self.issued = [False] * len(self.buckets)
 
     def _pad(self, n: int) -> int:
         return min(self.flat.numel, (n + 63) // 64 * 64)
@@ -70,7 +93,7 @@ class GradBuckets:
                 self._issue(i)
 
     def ready_all(self):
-        self.ready_upto(self.flat.numel)
+        self.ready_upto(self.reduce_end)
 
     def _issue(self, i: int):
         a, b = self.buckets[i]

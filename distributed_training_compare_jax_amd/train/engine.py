@@ -70,18 +70,42 @@ class Engine:
                               act_dtype=self.act_dtype,
                               side_stream=on_gpu and os.environ.get("DTC_NO_SIDE_STREAM", "0") != "1")
         self.program.before_comm.append(self.stage.side.join)
-        self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb)
+        # DP embedding-grad gather (pp == 1): instead of all-reducing the dense wte/wpe grads
+        # (103 MB fp32 for the reference vocab, issued last -> fully exposed), all-gather the
+        # embedding-output grads (b_local*T*D fp32 per rank) and let every rank rebuild the
+        # identical wte/wpe grads from the global batch with the deterministic sorted kernel.
+        self.embed_gather = bool(dp > 1 and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed)
+        self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb,
+                                   tail_mb=train_cfg.dp_tail_mb,
+                                   local_names=("wte", "wpe") if self.embed_gather else ())
         self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,
                               pp_global_clip=(train_cfg.pp_clip == "global"))
+        if pp == 1:
+            # incremental Σg²: with dp == 1 each layer's grads are final when its backward ends
+            # (norm chunk per layer, reduced on the side stream); with dp > 1 only the locally
+            # built embedding grads are final before the all-reduces finish
+            if dp == 1:
+                bk = self.buckets
+                cuts = [bk.head_end_offset()] + [bk.layer_end_offset(l) for l in reversed(self.layout.layers)]
+                self.opt.set_chunks(sorted(set(c for c in cuts if 0 < c < self.flat.numel)) + [self.flat.numel])
+            elif self.embed_gather:
+                self.opt.set_chunks([self.buckets.reduce_end, self.flat.numel])
 
         # ---- static device-side inputs/outputs (graph replay reads/writes these)
-        self.ids = torch.zeros(self.b_local, T, dtype=torch.int32, device=self.device)
+        D = model_cfg.d_model
+        if self.embed_gather:
+            self.ids_all = torch.zeros(self.global_batch, T, dtype=torch.int32, device=self.device)
+            self.ids = self.ids_all[self.row0:self.row0 + self.b_local]  # contiguous row view
+            self.dh_all = torch.zeros(self.global_batch * T, D, dtype=torch.float32, device=self.device)
+            self.feed_row0, self.feed_rows = 0, self.global_batch
+        else:
+            self.ids = torch.zeros(self.b_local, T, dtype=torch.int32, device=self.device)
+            self.feed_row0, self.feed_rows = self.row0, self.b_local
         self.labels = torch.zeros(self.b_local, T, dtype=torch.int32, device=self.device)
         pin = on_gpu
-        self._host = [torch.zeros(2, self.b_local, T, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._host = [torch.zeros(2, self.feed_rows, T, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self._host_i = 0
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
-        D = model_cfg.d_model
         if pp > 1:
             self.recv_x = [torch.zeros(self.mb_rows * T, D, dtype=torch.float32, device=self.device)
                            for _ in range(self.n_micro)]
@@ -106,13 +130,20 @@ class Engine:
         return self.global_batch * self.T
 
     def set_batch(self, batch_np: np.ndarray):
-        """batch_np int32 [b_local, T+1] (this rank's rows) → static device ids/labels."""
+        """batch_np int32 [feed_rows, T+1] (global rows [feed_row0, feed_row0+feed_rows): this rank's
+        rows, or the whole global batch under the DP embedding gather) → static device ids/labels."""
+        assert batch_np.shape[0] == self.feed_rows, (batch_np.shape, self.feed_rows)
         h = self._host[self._host_i]
         self._host_i ^= 1
         h[0].copy_(torch.from_numpy(batch_np[:, :-1]))
         h[1].copy_(torch.from_numpy(batch_np[:, 1:]))
-        self.ids.copy_(h[0], non_blocking=True)
-        self.labels.copy_(h[1], non_blocking=True)
+        if self.embed_gather:
+            lo = self.row0 - self.feed_row0
+            self.ids_all.copy_(h[0], non_blocking=True)
+            self.labels.copy_(h[1][lo:lo + self.b_local], non_blocking=True)
+        else:
+            self.ids.copy_(h[0], non_blocking=True)
+            self.labels.copy_(h[1], non_blocking=True)
 
     # ------------------------------------------------------------------ step bodies
     def _step_fn_dp_tp(self):
@@ -120,17 +151,34 @@ class Engine:
         dp = self.mesh.dp
         ctx: Dict = {}
         step = self.opt.step_t
-        h = st.embed_forward(self.ids, step, self.row0, ctx)
+        h = st.embed_forward(self.ids, step, self.row0, ctx, want_keys=not self.embed_gather)
+        gathered = (self.ids_all, 0, st.embed_keys(self.ids_all)) if self.embed_gather else None
         h = st.stage_forward(h, b, ctx)
         st.head_forward(h, self.labels, 1.0 / (b * T), ctx, loss_out=self.loss)
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
-        self.buckets.ready_upto(self.buckets.head_end_offset())
-        bk = self.buckets
-        dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=lambda l: bk.ready_upto(bk.layer_end_offset(l)))
-        st.embed_backward(ctx, dx, step, 0.0)
+        bk, opt, side = self.buckets, self.opt, st.side.run
+        if dp == 1:
+            opt.ready_upto(bk.head_end_offset(), side)
+            hook = lambda l: opt.ready_upto(bk.layer_end_offset(l), side)
+        else:
+            bk.ready_upto(bk.head_end_offset())
+            first = self.layout.layers[0]
+            # the last layer's bucket waits until the embedding gather is queued: the gather
+            # feeds compute (embed backward), the bucket only the optimizer
+            hook = (lambda l: bk.ready_upto(bk.layer_end_offset(l)) if l != first else None) if self.embed_gather \
+                else (lambda l: bk.ready_upto(bk.layer_end_offset(l)))
+        dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=hook)
+        if self.embed_gather:
+            out, g = self.dh_all, self.mesh.dp_group
+            self.program.comm(lambda: dist.all_gather_into_tensor(out, dx, group=g))
+            bk.ready_all()
+            st.embed_backward(ctx, self.dh_all, step, 0.0, gathered=gathered)
+            opt.chunk_ready(len(opt.chunks) - 1, side)  # local wte/wpe grads: overlaps the tail bucket
+        else:
+            st.embed_backward(ctx, dx, step, 0.0)
         st.side.join()
-        self.buckets.ready_all()
-        self.buckets.wait_all()
+        bk.ready_all()
+        bk.wait_all()
         self._loss_allreduce()
         self.opt.step()
         return self.loss

@@ -33,9 +33,10 @@ def make_data_iter(eng: Engine, tcfg: TrainConfig, mcfg: ModelConfig, start_step
     if tcfg.data == "fineweb":
         from ..data import fineweb
 
-        return fineweb.get_batch_iterator(eng.global_batch, mcfg.max_seq_len + 1, row0=eng.row0, nrows=eng.b_local)
-    return synthetic.get_batch_iterator(eng.global_batch, mcfg.max_seq_len + 1, seed=tcfg.seed, row0=eng.row0,
-                                        nrows=eng.b_local, start_step=start_step,
+        return fineweb.get_batch_iterator(eng.global_batch, mcfg.max_seq_len + 1, row0=eng.feed_row0,
+                                          nrows=eng.feed_rows)
+    return synthetic.get_batch_iterator(eng.global_batch, mcfg.max_seq_len + 1, seed=tcfg.seed, row0=eng.feed_row0,
+                                        nrows=eng.feed_rows, start_step=start_step,
                                         vocab=min(synthetic.BPE_VOCAB, mcfg.vocab_size - 1))
 
 

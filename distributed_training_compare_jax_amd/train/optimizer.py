@@ -47,13 +47,58 @@ class FusedAdamW:
         self.pp_group = pp_group if pp_global_clip else None
         dev = flat.device
         w = (lambda spec: 1.0 if spec.tp != "rep" else 1.0 / tp_size)
-        self.segments = O.make_segments(merge_segments(flat.segments(w), flat.numel), dev)
+        self._merged = merge_segments(flat.segments(w), flat.numel)
+        self.segments = O.make_segments(self._merged, dev)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.chunks = []  # incremental-norm chunks: [segments, lo, hi, partial view]
+        self._done = []
+
+    # -- incremental global norm ------------------------------------------------------
+    def set_chunks(self, cuts, total_blocks: int = 1024):
+        """Split Σg² into flat ranges [0,c0), [c0,c1), ... (cuts ascending, 4-aligned, last =
+        numel).  A chunk whose grads are final can be reduced early (:meth:`ready_upto` /
+        :meth:`chunk_ready`, typically on the backward side stream) so only the last chunk and a
+        fixed-order finish remain between backward and the AdamW pass."""
+        f = self.flat
+        assert cuts and cuts[-1] == f.numel and all(c % 4 == 0 for c in cuts)
+        specs, lo = [], 0
+        for hi in cuts:
+            segs = [(max(o, lo), min(o + n, hi) - max(o, lo), wt) for (o, n, wt) in self._merged
+                    if o < hi and o + n > lo]
+            nb = max(8, int(round(total_blocks * (hi - lo) / f.numel)))
+            specs.append((O.make_segments(segs, f.device), lo, hi, nb))
+            lo = hi
+        self.part = torch.zeros(sum(s[3] for s in specs), dtype=torch.float32, device=f.device)
+        self.chunks, off = [], 0
+        for segs, lo, hi, nb in specs:
+            self.chunks.append((segs, lo, hi, self.part[off:off + nb]))
+            off += nb
+        self._done = [False] * len(self.chunks)
+
+    def chunk_ready(self, i: int, runner=None):
+        if self._done[i]:
+            return
+        segs, _, _, part = self.chunks[i]
+        g = self.flat.grads
+        fn = lambda: O.sumsq_partial(g, segs, part)
+        runner(fn) if runner is not None else fn()
+        self._done[i] = True
+
+    def ready_upto(self, offset: int, runner=None):
+        for i, (_, _, hi, _) in enumerate(self.chunks):
+            if hi <= offset:
+                self.chunk_ready(i, runner)
 
     def step(self):
         f, c = self.flat, self.cfg
-        O.sumsq_segments(f.grads, self.segments, self.sumsq, step=self.step_t)
+        if self.chunks:
+            for i in range(len(self.chunks)):
+                self.chunk_ready(i)
+            O.sum_finish(self.part, self.sumsq, step=self.step_t)
+            self._done = [False] * len(self.chunks)
+        else:
+            O.sumsq_segments(f.grads, self.segments, self.sumsq, step=self.step_t)
         if self.tp_size > 1:
             g = self.tp_group
             s = self.sumsq

@@ -27,7 +27,8 @@ def _worker(parallel, kw, out_dir):
     oc = OptimConfig(lr=3e-3, weight_decay=0.1, grad_clip=1.0)
     d = init_distributed("cuda")
     r = train(tc, mc, oc, d, quiet=True, write_csv=False)
-    torch.save({"losses": r["history"], "graphs": r["n_graphs"], "comms": r["n_comms"]},
+    torch.save({"losses": r["history"], "graphs": r["n_graphs"], "comms": r["n_comms"],
+                "params": r["engine"].flat.params.cpu()},
                os.path.join(out_dir, f"rank{d.rank}.pt"))
     destroy()
 
@@ -50,6 +51,7 @@ def single(cuda):
 
 @pytest.mark.parametrize("parallel,kw", [
     ("dp", {}),
+    ("dp", {"dp_embed_gather": False}),
     ("tp", {}),
     ("pp", {"pp_microbatches": 2, "pp_clip": "global"}),
     ("pp", {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b"}),
@@ -60,3 +62,5 @@ def test_two_ranks_match_single_gpu(single, parallel, kw):
     got = res[0]["losses"]
     assert got == pytest.approx(ref, rel=2e-2, abs=2e-2), (parallel, got, ref)
     assert res[0]["graphs"] >= 2  # step was captured and cut at the collectives
+    if parallel == "dp":  # replicas stay bit-identical (deterministic local embedding grads)
+        assert torch.equal(res[0]["params"], res[1]["params"])

@@ -72,3 +72,23 @@ def test_reference_config_step(cuda):
         vals.append(eng.loss_value())
     assert abs(vals[0] - 10.83) < 0.5, vals[0]  # ~ln(50258) at init
     assert vals[-1] < vals[0] - 0.5, vals
+
+
+def test_bitwise_deterministic_training(cuda):
+    """Deterministic mode is the only mode: no float atomics anywhere in the step (sorted
+    embedding backward, slab reductions), so two runs give bit-identical losses and params."""
+    runs = []
+    for _ in range(2):
+        eng, mc = _engine(cuda, use_graph=True, preset="ref", vocab=50258, batch=8)
+        it = get_batch_iterator(8, mc.max_seq_len + 1)
+        out = []
+        for _ in range(4):
+            eng.set_batch(next(it))
+            eng.run_step()
+            out.append(eng.loss_value())
+        torch.cuda.synchronize()
+        runs.append((out, eng.flat.params.clone(), eng.flat.exp_avg_sq.clone()))
+        del eng
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1]), "params differ bitwise between identical runs"
+    assert torch.equal(runs[0][2], runs[1][2]), "Adam state differs bitwise between identical runs"

@@ -139,6 +139,46 @@ def test_embedding_dropout_bits(cuda):
     _close(dwpe.cpu(), dpc, 1e-5, "dwpe")
 
 
+@pytest.mark.parametrize("B,T,D,V,skew", [(8, 512, 512, 50304, True), (64, 512, 128, 50304, True),
+                                           (3, 100, 64, 300, False), (80, 512, 64, 1000, True)])
+def test_embedding_bwd_sorted_deterministic(cuda, B, T, D, V, skew):
+    """Sorted segment-sum backward: exact vs index_add (fp64), bitwise repeatable, accumulate mode.
+    ``skew`` draws Zipf-like ids so one id spans many 64-key tiles (the multi-piece path)."""
+    g = torch.Generator().manual_seed(3)
+    if skew:
+        r = torch.rand(B * T, generator=g)
+        ids = torch.minimum((V ** r).long() - 1, torch.tensor(V - 1)).to(torch.int32).view(B, T)
+        ids.view(-1)[: 3 * 64 + 5] = 7  # one long run crossing tile boundaries
+    else:
+        ids = torch.randint(0, V, (B, T), generator=g, dtype=torch.int32)
+    step = torch.tensor([3], dtype=torch.int64)
+    dh = _r(B * T, D, dtype=torch.float32, seed=21)
+    keys = None
+    if B * T <= E.SORT_MAX:  # else: the row-chunked path sorts each chunk itself
+        keys = E.embed_sort_keys(ids.to(cuda), V)
+        nb = max(1, (B * T - 1).bit_length())
+        kc = keys.cpu().long() & 0xFFFFFFFF
+        assert torch.equal(kc >> nb, ids.view(-1).long().sort().values), "sorted ids"
+        assert torch.equal(torch.sort(kc & ((1 << nb) - 1)).values, torch.arange(B * T)), "token permutation"
+    outs = []
+    for _ in range(2):
+        dwte, dwpe = torch.full((V, D), 5.0, device=cuda), torch.zeros(T, D, device=cuda)
+        E.embed_bwd(ids.to(cuda), dh, dwte, dwpe, 0.1, 99, step.to(cuda), 2, 0.0, keys=keys)
+        outs.append((dwte.clone(), dwpe.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), "not bitwise repeatable"
+    keep = E.dropout_keep_mask(B * T, D, 2 * T, 0.1, 99, 3)
+    gd = torch.where(keep, dh.cpu().double() / 0.9, torch.zeros((), dtype=torch.float64))
+    ref_w = torch.zeros(V, D, dtype=torch.float64).index_add_(0, ids.view(-1).long(), gd)
+    ref_p = gd.view(B, T, D).sum(0)
+    _close(outs[0][0].cpu(), ref_w, 2e-6, "dwte")
+    _close(outs[0][1].cpu(), ref_p, 2e-6, "dwpe")
+    # accumulate (beta = 1): adds onto the existing grads
+    dwte, dwpe = outs[0][0].clone(), outs[0][1].clone()
+    E.embed_bwd(ids.to(cuda), dh, dwte, dwpe, 0.1, 99, step.to(cuda), 2, 1.0, keys=keys)
+    _close(dwte.cpu(), 2 * ref_w, 2e-6, "dwte_acc")
+    _close(dwpe.cpu(), 2 * ref_p, 2e-6, "dwpe_acc")
+
+
 @pytest.mark.parametrize("B,T,H,hd", [(2, 512, 4, 32), (1, 256, 2, 64), (2, 128, 3, 32)])
 def test_attention(cuda, B, T, H, hd):
     qkv = _r(B, T, 3 * H * hd, seed=20)
