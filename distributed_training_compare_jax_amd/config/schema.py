@@ -14,7 +14,9 @@ are optional and default to the reference behaviour:
 * ``TrainConfig.pp_schedule`` (``gpipe`` | ``1f1b``), ``pp_clip`` (``local`` is the
   reference's stage-local global-norm clip, ``create_train_step.py:190``; ``global``
   all-reduces the norm across stages).
-* ``TrainConfig.data`` (``synthetic`` | ``fineweb``), ``use_graph``, ``profile``,
+* ``TrainConfig.data`` (``synthetic`` | ``fineweb``), ``use_graph``, ``profile`` (roctx
+  ranges, device step times and a Chrome trace under ``<output_dir>/trace/``, see
+  ``utils/trace.py``), ``watchdog_s`` (abort a rank whose step stalls that long, 0 = off),
   ``dp_bucket_mb`` / ``dp_tail_mb`` (DP grad bucket sizes; the last bucket is kept small
   because its all-reduce is exposed), ``dp_embed_gather`` (DP: all-gather the embedding
   output grads and rebuild wte/wpe grads locally instead of all-reducing the 103 MB table),
@@ -106,6 +108,7 @@ class TrainConfig:
     data: str = "synthetic"
     use_graph: bool = True
     profile: bool = False
+    watchdog_s: float = 900.0
     dp_bucket_mb: float = 64.0
     dp_tail_mb: float = 16.0
     dp_embed_gather: bool = True

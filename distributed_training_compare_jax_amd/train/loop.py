@@ -53,11 +53,20 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
     if start:
         data = make_data_iter(eng, train_config, model_config, start_step=start)
 
+    from ..utils.trace import Tracer
+    from ..utils.watchdog import Watchdog
+
+    tr = Tracer(train_config.profile, train_config.output_dir, dinfo.rank, eng.device)
+    dog = Watchdog(dinfo.rank, train_config.watchdog_s).start()
     say("Warmup")
-    for _ in range(train_config.warmup_steps):
-        eng.set_batch(next(data))
-        eng.run_step()
-        eng.loss_value()
+    for i in range(train_config.warmup_steps):
+        with tr.span("data"):
+            eng.set_batch(next(data))
+        with tr.device_step(-train_config.warmup_steps + i):
+            eng.run_step()
+        with tr.span("loss sync"):
+            eng.loss_value()
+        dog.beat(-train_config.warmup_steps + i)
 
     barrier()
     say("Start measuring")
@@ -66,10 +75,15 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
     t0 = time.perf_counter()
     for step in range(1, train_config.steps + 1):
         eng.set_batch(batch)
-        eng.run_step()
+        with tr.device_step(step):
+            eng.run_step()
         if step < train_config.steps:
-            batch = next(data)  # host data for the next step overlaps this step's GPU work
-        loss = eng.loss_value()
+            with tr.span("data"):
+                batch = next(data)  # host data for the next step overlaps this step's GPU work
+        with tr.span("loss sync"):
+            loss = eng.loss_value()
+        dog.beat(step)
+        tr.collect()
         running.append(loss)
         history.append(loss)
         now = time.perf_counter()
@@ -77,8 +91,10 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
         if step % train_config.log_every == 0:
             say(f"Step: {step} | Avg loss: {np.mean(running):.4f} | Average step time: {(now - t0) / step:.4f}")
             running = []
-        maybe_save(eng, train_config, start + train_config.warmup_steps + step)
+        with tr.span("checkpoint"):
+            maybe_save(eng, train_config, start + train_config.warmup_steps + step)
     t1 = time.perf_counter()
+    dog.stop()
     say(f"Total time: {t1 - t0}")
     say("End")
     total = t1 - t0
@@ -90,6 +106,11 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
                   model=model_config.name, global_batch=eng.global_batch, seq_len=eng.T,
                   dtype=str(eng.act_dtype).replace("torch.", ""), n_graphs=eng.program.n_graphs,
                   n_comms=eng.program.n_comms)
+    if tr.enabled:
+        path = tr.write()
+        n_warm = train_config.warmup_steps
+        dev = tr.device_ms[n_warm:] if len(tr.device_ms) > n_warm else tr.device_ms
+        result.update(device_step_ms=dev, device_step_ms_mean=float(np.mean(dev)) if dev else None, trace=path)
     if is_main and write_csv:
         os.makedirs(train_config.output_dir, exist_ok=True)
         _write_csv(os.path.join(train_config.output_dir, "log.csv"), elapsed, history)

@@ -1,0 +1,44 @@
+"""Auxiliary subsystems on CPU: watchdog (failure detection) and step tracing."""
+
+import json
+import os
+import time
+
+import torch
+
+from distributed_training_compare_jax_amd.config.schema import OptimConfig, TrainConfig, model_config_from_preset
+from distributed_training_compare_jax_amd.parallel.dist import DistInfo
+from distributed_training_compare_jax_amd.train.loop import train
+from distributed_training_compare_jax_amd.utils.watchdog import Watchdog
+
+
+def test_watchdog_fires_on_stall(capfd):
+    codes = []
+    dog = Watchdog(rank=3, timeout_s=0.2, exit_fn=codes.append).start()
+    dog.beat(7)
+    time.sleep(0.8)
+    dog.stop()
+    assert codes == [124] and dog.fired
+    err = capfd.readouterr().err
+    assert "[rank 3] watchdog" in err and "last completed step 7" in err
+
+
+def test_watchdog_quiet_while_beating():
+    codes = []
+    with Watchdog(rank=0, timeout_s=0.3, exit_fn=codes.append) as dog:
+        for i in range(8):
+            dog.beat(i)
+            time.sleep(0.05)
+    assert codes == [] and not dog.fired
+
+
+def test_profile_writes_trace_and_metrics(tmp_path):
+    mc = model_config_from_preset("tiny", vocab_size=500)
+    tc = TrainConfig(seed=0, parallel="dp", batch=2, steps=3, log_every=100, output_dir=str(tmp_path), device="cpu",
+                     warmup_steps=1, profile=True)
+    r = train(tc, mc, OptimConfig(lr=1e-3, weight_decay=0.1, grad_clip=1.0), DistInfo(0, 1, 0, torch.device("cpu"), "gloo"), quiet=True)
+    tr = json.load(open(os.path.join(tmp_path, "trace", "rank0.json")))
+    names = {e["name"] for e in tr["traceEvents"]}
+    assert {"data", "loss sync", "step 1", "step 3"} <= names
+    m = json.load(open(os.path.join(tmp_path, "metrics.json")))
+    assert m["trace"].endswith("rank0.json")

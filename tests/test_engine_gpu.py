@@ -92,3 +92,20 @@ def test_bitwise_deterministic_training(cuda):
     assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
     assert torch.equal(runs[0][1], runs[1][1]), "params differ bitwise between identical runs"
     assert torch.equal(runs[0][2], runs[1][2]), "Adam state differs bitwise between identical runs"
+
+
+def test_profile_device_step_times(cuda, tmp_path):
+    """profile: true on the GPU: HIP-event step times around graph replays + Chrome trace."""
+    import json
+    import os
+
+    from distributed_training_compare_jax_amd.train.loop import train
+
+    mc = model_config_from_preset("tiny", vocab_size=1000)
+    tc = TrainConfig(seed=0, parallel="dp", batch=4, steps=4, log_every=100, output_dir=str(tmp_path), device="cuda",
+                     warmup_steps=2, profile=True)
+    r = train(tc, mc, OptimConfig(lr=1e-3, weight_decay=0.1, grad_clip=1.0), DistInfo(0, 1, 0, cuda, "nccl"),
+              quiet=True)
+    assert len(r["device_step_ms"]) == 4 and all(0 < t < 1e4 for t in r["device_step_ms"])
+    tr = json.load(open(os.path.join(tmp_path, "trace", "rank0.json")))
+    assert any(e["name"].startswith("device step") for e in tr["traceEvents"])
