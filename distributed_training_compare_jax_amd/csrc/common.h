@@ -38,7 +38,7 @@ struct GemmArgs {
   int split_k;
 };
 
-enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_LMHEAD = 4 };
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_LMHEAD = 4, EPI_NONE = 99 /* microbench: no store */ };
 
 #define DTC_CHECK_LAUNCH() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
 

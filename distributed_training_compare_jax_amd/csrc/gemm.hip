@@ -25,6 +25,7 @@
 //  * Split-K (fp32 slabs + deterministic reduce) for the small wgrad grids.
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -151,6 +152,112 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
       else for (int r = 0; r < 4; ++r) if (n + r < e.N) g[r] = gb[r];
     }
   }
+}
+
+
+// Per-wave LDS staging of a bf16 (TM*16) x 64 output tile, so global stores go out as full
+// 128-B rows (8 rows per instruction) instead of 16 rows x 32 B.  8-byte chunk c of row R sits
+// at chunk c ^ (R & 15): fragment writes and row reads are both bank-conflict-free.
+__device__ __forceinline__ void stage_put(bf16* st, int row, int chunk, bf16x4 v) {
+  *(bf16x4*)(st + row * 64 + ((chunk ^ (row & 15)) << 2)) = v;
+}
+
+template <int ROWS>
+__device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int m_base, int n_base, int M, int N,
+                                          int lane) {
+#pragma unroll 4
+  for (int it = 0; it < ROWS / 8; ++it) {
+    const int row = it * 8 + (lane >> 3), p = lane & 7;
+    u32x4 v = *(const u32x4*)(st + row * 64 + ((p ^ ((row >> 1) & 7)) << 3));
+    if (row & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+    const int m = m_base + row, n = n_base + p * 8;
+    if (m >= M) continue;
+    bf16* c = C + (long)m * ldc + n;
+    if (n + 8 <= N) {
+      *(u32x4*)c = v;
+    } else {
+      const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+      for (int r = 0; r < 8; ++r) if (n + r < N) c[r] = b[r];
+    }
+  }
+}
+
+// lm_head epilogue: logits (bf16) + per-row partial (max, sum exp) over this wave's TN*16 columns +
+// the label logit.  acc[i][j]: lane holds C[m_base + 16j + (lane&15)][n_base + 16i + 4(lane>>4) + r].
+// Epilogue operands loaded up front (all loads in flight together, ideally before the main loop
+// ends): one bias vector per column group and one label per fragment row.
+template <int TN, int TM>
+struct EpiPre {
+  f32x4 bb[TN];
+  int lab[TM];
+};
+
+template <int TN, int TM>
+__device__ __forceinline__ void epi_prefetch(const Epi& e, int m_base, int n_base, int lane, bool labels,
+                                             EpiPre<TN, TM>& pre) {
+  const int g4 = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n_base + i * 16 + g4;
+    pre.bb[i] = (e.bias && n + 4 <= e.N) ? *(const f32x4*)(e.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int m = m_base + j * 16 + (lane & 15);
+    pre.lab[j] = (labels && m < e.M) ? e.labels[m] - e.vocab_start : -1;
+  }
+}
+
+template <int TN, int TM>
+__device__ __forceinline__ void lmhead_epilogue(const f32x4 (&acc)[TN][TM], const Epi& e, int m_base, int n_base,
+                                                int part_idx, int lane, const EpiPre<TN, TM>& pre,
+                                                bf16* stage = nullptr) {
+  const int g4 = 4 * (lane >> 4);
+  bool okv[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {  // validity: once per column group, shared by all TM rows
+    const int n = n_base + i * 16 + g4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) okv[i][r] = (n + r) < e.n_valid && (n + r) < e.N;
+  }
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int m = m_base + j * 16 + (lane & 15);
+    const bool mvalid = m < e.M;
+    const int lab = pre.lab[j];
+    float v[TN][4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n_base + i * 16 + g4;
+      bf16x4 ob;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ob[r] = f2bf(acc[i][j][r] + pre.bb[i][r]);
+        v[i][r] = okv[i][r] ? (float)ob[r] : -INFINITY;
+        mx = fmaxf(mx, v[i][r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) if (!okv[i][r]) ob[r] = f2bf(-INFINITY);
+      if (stage) stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
+      else if (mvalid && n + 4 <= e.N) *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
+      if (lab >= n && lab < n + 4 && lab < e.n_valid) e.label_out[m] = v[i][lab - n];
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+    if (mx != -INFINITY) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum += __expf(v[i][r] - mx);
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    // part-major [nparts][M]: the 16 rows of a fragment write one contiguous 128-B line
+    if (mvalid && lane < 16) *(f32x2*)(e.part + ((long)part_idx * e.M + m) * 2) = f32x2{mx, sum};
+  }
+  if (stage) stage_out<TM * 16>(stage, (bf16*)e.C, e.ldc, m_base, n_base, e.M, e.N, lane);
 }
 
 template <int BM, int BN, int BK, bool AK, bool BKM, int EPI, bool OUTF32>
@@ -285,45 +392,9 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
     return;
   }
   if (EPI == EPI_LMHEAD) {
-    // logits (bf16) + per-row partial (max, sum exp) over this wave's WN columns + label logit.
-    const int part_idx = tn_idx * 2 + wn;
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wm * WM + j * 16 + (lane & 15);
-      const bool mvalid = m < M;
-      const int lab = mvalid ? e.labels[m] - e.vocab_start : -1;
-      float v[TN][4];
-      float mx = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + g4;
-        f32x4 bb = (n + 4 <= e.N) ? *(const f32x4*)(e.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = (float)f2bf(acc[i][j][r] + bb[r]);
-          bool ok = (n + r) < e.n_valid && (n + r) < e.N;
-          v[i][r] = ok ? x : -INFINITY;
-          mx = fmaxf(mx, v[i][r]);
-        }
-        if (mvalid && n + 4 <= e.N) {
-          bf16x4 ob = {f2bf(v[i][0]), f2bf(v[i][1]), f2bf(v[i][2]), f2bf(v[i][3])};
-          *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
-        }
-        if (lab >= n && lab < n + 4 && lab < e.n_valid) e.label_out[m] = v[i][lab - n];
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      float s = 0.f;
-      if (mx != -INFINITY) {
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s += __expf(v[i][r] - mx);
-      }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (mvalid && lane < 16) *(f32x2*)(e.part + ((long)m * e.nparts + part_idx) * 2) = f32x2{mx, s};
-    }
+    EpiPre<TN, TM> pre;
+    epi_prefetch<TN, TM>(e, m0 + wm * WM, n0 + wn * WN, lane, true, pre);
+    lmhead_epilogue<TN, TM>(acc, e, m0 + wm * WM, n0 + wn * WN, tn_idx * 2 + wn, lane, pre);
     return;
   }
 #pragma unroll
@@ -332,6 +403,142 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
     for (int j = 0; j < TM; ++j) {
       int m = m0 + wm * WM + j * 16 + (lane & 15);
       int n = n0 + wn * WN + i * 16 + g4;
+      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+    }
+}
+
+
+// ============================================================================================
+// 256x256 tile, 8 waves (2 along M x 4 along N, 128x64 per wave), for the large forward-layout
+// GEMMs (the lm_head: [4096 x 50304 x 512]).  Why a second kernel: at 128^2 / 64x64-per-wave
+// the LDS->VGPR traffic equals the MFMA rate (1/64+1/64 B per FLOP) and the L2->LDS traffic is
+// 64 FLOP/B, so those tiles cap near ~40 % of peak; 128x64 per wave cuts LDS bytes/FLOP by 25 %
+// and the 256^2 block halves L2 bytes/FLOP.  1 block/CU (128 KB LDS), so the staging is direct
+// global->LDS DMA (global_load_lds_dwordx4, no staging VGPRs, cdna_hip_programming.md §5):
+// tile k+1 streams into the other LDS buffer while the MFMAs consume tile k.
+//  * LDS image per operand: [256 rows][64 k] bf16, 128-B rows, 16-B chunk c stored at
+//    c ^ ((row>>1)&7): the DMA destination is lane-linear per wave (8 rows per instruction), the
+//    swizzle is applied on the per-lane SOURCE address, and a fragment read (16 rows x one
+//    chunk per 16-lane group) hits 16 distinct 16-B bank groups -> conflict-free ds_read_b128.
+//  * Out-of-range rows (ragged M/N edge) are clamped to the last row: they only feed outputs
+//    the epilogue never stores.  K must be a multiple of 64.
+constexpr int NT2 = 512;
+constexpr int BIG = 256;
+constexpr int IMG = BIG * 64;  // elements per operand image
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* glb_vptr;
+
+__device__ __forceinline__ int swz_off(int row, int c) { return row * 64 + ((c ^ ((row >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ void dma_tile(const bf16* __restrict__ X, long ldx, int r0, int rmax, int k0, bf16* img,
+                                         int wave, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int blk = q * 8 + wave;  // 8-row group: one 1-KB DMA instruction per wave
+    const int row = blk * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int grow = min(r0 + row, rmax - 1);
+    __builtin_amdgcn_global_load_lds((glb_vptr)(X + (long)grow * ldx + k0 + c * 8), (lds_vptr)(img + blk * 512), 16,
+                                     0, 0);
+  }
+}
+
+template <int EPI, bool OUTF32>
+__global__ void __launch_bounds__(NT2, 1)
+gemm256_nt_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+                  int tiles_m, int tiles_n, int gm, Epi e) {
+  constexpr int TM = 8, TN = 4;  // 16x16 fragments per wave: 128 (m) x 64 (n)
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = tiles_m * tiles_n;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+  const int gm_eff = min(gm, tiles_m - grp * gm);
+  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
+  const int nk = K / 64;
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  dma_tile(A, lda, m0, M, 0, smem, wave, lane);
+  dma_tile(B, ldb, n0, N, 0, smem + IMG, wave, lane);
+  EpiPre<TN, TM> pre;  // epilogue operands: loaded under the main loop, not after it
+  if (EPI == EPI_LMHEAD || EPI == EPI_STORE)
+    epi_prefetch<TN, TM>(e, m0 + wm * 128, n0 + wn * 64, lane, EPI == EPI_LMHEAD, pre);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16* sA = smem + (kt & 1) * 2 * IMG;
+    const bf16* sB = sA + IMG;
+    if (kt + 1 < nk) {
+      bf16* nA = smem + ((kt + 1) & 1) * 2 * IMG;
+      dma_tile(A, lda, m0, M, (kt + 1) * 64, nA, wave, lane);
+      dma_tile(B, ldb, n0, N, (kt + 1) * 64, nA + IMG, wave, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+      const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = *(const bf16x8*)(sA + swz_off(wm * 128 + j * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = *(const bf16x8*)(sB + swz_off(wn * 64 + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 landed
+    __syncthreads();                                  // ... and every other wave's; reads of kt done
+  }
+
+  bf16* stage = smem + wave * (128 * 64);  // main-loop buffers are free after the last barrier
+  if (EPI == EPI_LMHEAD) {
+    lmhead_epilogue<TN, TM>(acc, e, m0 + wm * 128, n0 + wn * 64, tn_idx * 4 + wn, lane, pre, stage);
+    return;
+  }
+  if (EPI == EPI_STORE && !OUTF32) {
+    const int g4s = 4 * (lane >> 4);
+    f32x4 bb[TN];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wn * 64 + i * 16 + g4s;
+      bb[i] = pre.bb[i];
+      if (e.bias && n < N && n + 4 > N)
+        for (int r = 0; r < 4; ++r) bb[i][r] = n + r < N ? e.bias[n + r] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        bf16x4 ob;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ob[r] = f2bf(e.alpha * acc[i][j][r] + bb[i][r]);
+        stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
+      }
+    stage_out<128>(stage, (bf16*)e.C, e.ldc, m0 + wm * 128, n0 + wn * 64, M, N, lane);
+    return;
+  }
+  if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  const int g4 = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      int m = m0 + wm * 128 + j * 16 + (lane & 15);
+      int n = n0 + wn * 64 + i * 16 + g4;
       if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
     }
 }
@@ -432,11 +639,37 @@ int launch_sz(const GemmArgs& a, const Plan& p, hipStream_t st) {
   return launch_t<64, 64, AK, BKM, EPI, OUTF32>(a, p, st);
 }
 
+
+// the 256^2 kernel pays when it still fills the chip twice over (lm_head-sized problems)
+bool use_big(int M, int N, int K) {
+  static const int enabled = [] { const char* v = getenv("DTC_GEMM256"); return v ? atoi(v) : 1; }();
+  if (!enabled || K % 64) return false;
+  const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
+  return t >= 512;
+}
+
+template <int EPI, bool OUTF32>
+int launch_big(const GemmArgs& a, hipStream_t st) {
+  Epi e;
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
+  e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
+  const int tiles_m = (a.M + BIG - 1) / BIG, tiles_n = (a.N + BIG - 1) / BIG;
+  e.nparts = tiles_n * 4;
+  const int ntiles = tiles_m * tiles_n;
+  int gm = tiles_m;
+  if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
+  hipLaunchKernelGGL((gemm256_nt_kernel<EPI, OUTF32>), dim3(ntiles), dim3(NT2), 0, st, (const bf16*)a.A, a.lda,
+                     (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, e);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
 
-int dtc_lmhead_nparts(int N) { return ((N + 127) / 128) * 2; }
+int dtc_lmhead_nparts(int M, int N, int K) { return use_big(M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }
 
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   Plan p = make_plan(M, N, K, layout == 2 ? 1 : (layout == 1 ? 2 : 0));
@@ -451,6 +684,13 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   const bool f32 = a->c_f32 != 0;
   if (a->layout == 0) {
     Plan p = make_plan(a->M, a->N, a->K, 0);
+    if (use_big(a->M, a->N, a->K)) {
+      if (epi == EPI_LMHEAD) return launch_big<EPI_LMHEAD, false>(*a, st);
+      if (epi == EPI_GELU) return launch_big<EPI_GELU, false>(*a, st);
+      if (epi == EPI_RESID) return launch_big<EPI_RESID, true>(*a, st);
+      if (epi == EPI_STORE) return f32 ? launch_big<EPI_STORE, true>(*a, st) : launch_big<EPI_STORE, false>(*a, st);
+      return 1003;
+    }
     if (epi == EPI_LMHEAD) {
       if (p.bk != 64) return 1008;
       p.bm = p.bn = 128;

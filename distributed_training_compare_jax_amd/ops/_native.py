@@ -48,7 +48,7 @@ class GemmArgs(ctypes.Structure):
         ("alpha", c_float), ("beta", c_float),
         ("labels", c_vp),        # int32 [M] (lm-head CE epilogue)
         ("vocab_start", c_int), ("n_valid", c_int),
-        ("part", c_vp),          # float2 [M][nparts]
+        ("part", c_vp),          # float2 [nparts][M]
         ("label_out", c_vp),     # fp32 [M]
         ("workspace", c_vp), ("ws_bytes", c_long),
         ("split_k", c_int),      # 0 = auto
@@ -68,7 +68,7 @@ def _declare(lib):
         "dtc_version": ([], i),
         "dtc_gemm": ([ctypes.POINTER(GemmArgs), vp], i),
         "dtc_gemm_workspace_bytes": ([i, i, i, i], l),
-        "dtc_lmhead_nparts": ([i], i),
+        "dtc_lmhead_nparts": ([i, i, i], i),
         "dtc_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
         "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, vp], i),
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),

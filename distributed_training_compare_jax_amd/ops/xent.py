@@ -40,16 +40,16 @@ def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, la
         lab = torch.where(inside, logits.gather(1, loc.clamp(0, Vl - 1)[:, None])[:, 0], torch.zeros(M))
         return logits.to(h.dtype), torch.stack([mx, se], -1), lab
     L = N.lib()
-    P = int(L.dtc_lmhead_nparts(Vl))
+    P = int(L.dtc_lmhead_nparts(M, Vl, D))
     logits = torch.empty(M, Vl, dtype=torch.bfloat16, device=h.device)
-    part = torch.empty(M, P, 2, dtype=torch.float32, device=h.device)
+    part = torch.empty(P, M, 2, dtype=torch.float32, device=h.device)  # part-major (coalesced epilogue writes)
     lab = torch.zeros(M, dtype=torch.float32, device=h.device)
     from .gemm import _gemm_native
 
     _gemm_native(0, M, Vl, D, h, h.stride(0), w, w.stride(0), logits, Vl, epi=N.EPI_LMHEAD, bias=b,
                  labels=labels, vocab_start=vocab_start, n_valid=n_valid, part=part, label_out=lab)
     rowstat = torch.empty(M, 2, dtype=torch.float32, device=h.device)
-    N.check(L.dtc_ce_combine(part.data_ptr(), M, P, P, 1, None, None, rowstat.data_ptr(), 0.0, None, 0,
+    N.check(L.dtc_ce_combine(part.data_ptr(), M, P, 1, M, None, None, rowstat.data_ptr(), 0.0, None, 0,
                              N.stream_ptr(h.device)), "dtc_ce_combine")
     return logits, rowstat, lab
 

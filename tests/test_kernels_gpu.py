@@ -34,7 +34,7 @@ def _close(a, b, rtol, name=""):
 
 
 GEMM_SHAPES = [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048), (256, 384, 128), (512, 768, 96),
-               (200, 136, 64), (4096, 50304, 512)]
+               (200, 136, 64), (4096, 50304, 512), (2000, 33000, 128)]
 
 
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
@@ -194,8 +194,9 @@ def test_attention(cuda, B, T, H, hd):
         _close(d3[:, :, i], r3[:, :, i], 3e-2, f"attn_d{n}")
 
 
-def test_lmhead_ce(cuda):
-    M, D, V, Vp = 512, 128, 1000, 1024
+@pytest.mark.parametrize("M,D,V,Vp", [(512, 128, 1000, 1024), (2048, 256, 50258, 50304)])
+def test_lmhead_ce(cuda, M, D, V, Vp):
+    """Second case runs the 256x256 DMA-staged kernel (>= 512 tiles), incl. its ragged last N tile."""
     h = _r(M, D, seed=22)
     w = _r(Vp, D, scale=0.2, seed=23)
     b = _r(Vp, dtype=torch.float32, seed=24)
