@@ -9,13 +9,13 @@
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-template <int EPI, bool F32>
-float run(const GemmArgs& a, int reps) {
+template <int EPI, bool F32, bool AK = true, bool BKM = true>
+float run(const GemmArgs& a, int reps, int split = 1) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) { int rc = launch_big<EPI, F32>(a, 0); CK((hipError_t)rc); }
+  for (int i = 0; i < 3; ++i) { int rc = launch_big<AK, BKM, EPI, F32>(a, split, 0); CK((hipError_t)rc); }
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < reps; ++i) launch_big<EPI, F32>(a, 0);
+  for (int i = 0; i < reps; ++i) launch_big<AK, BKM, EPI, F32>(a, split, 0);
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -44,5 +44,22 @@ int main() {
     float t = run<EPI_NONE, false>(a, 10);
     printf("main loop K=%5d  %8.1f us  %6.1f TF/s\n", K, t, 2.0 * M * N * K / t * 1e-6);
   }
+  // lm_head wgrad: dW[V x D] = dlogits^T[V x T] . h[T x D]  (both operands MN-major)
+  float* W32; CK(hipMalloc(&W32, (size_t)N * 512 * 4));
+  GemmArgs w{};
+  w.layout = 2; w.M = N; w.N = 512; w.K = M; w.A = B; w.lda = N; w.B = A; w.ldb = 512; w.C = W32; w.ldc = 512;
+  w.c_f32 = 1; w.alpha = 1.f;
+  float tw = run<EPI_STORE, true, false, false>(w, 10);
+  printf("wgrad [%d x 512 x %d] %7.1f us (%6.1f TF/s)\n", N, M, tw, 2.0 * N * 512 * M / tw * 1e-6);
+  // lm_head dgrad: dH[T x D] = dlogits[T x V] . W[V x D]  (A K-major, B MN-major), split-K
+  float* ws; CK(hipMalloc(&ws, (size_t)64 << 20));
+  bf16* Wb; CK(hipMalloc(&Wb, (size_t)N * 512 * 2));
+  CK(hipMemcpy(Wb, h.data(), (size_t)N * 512 * 2, hipMemcpyHostToDevice));
+  GemmArgs d{};
+  d.layout = 1; d.M = M; d.N = 512; d.K = N; d.A = B; d.lda = N; d.B = Wb; d.ldb = 512; d.C = W32; d.ldc = 512;
+  d.c_f32 = 1; d.alpha = 1.f; d.workspace = ws; d.ws_bytes = (long)64 << 20;
+  const int sp = big_split(1, M, 512, N);
+  float td = run<EPI_STORE, true, true, false>(d, 10, sp);
+  printf("dgrad [%d x 512 x %d] split %d %7.1f us (%6.1f TF/s)\n", M, N, sp, td, 2.0 * N * 512 * M / td * 1e-6);
   return 0;
 }

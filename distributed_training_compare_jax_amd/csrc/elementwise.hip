@@ -245,6 +245,42 @@ __global__ void ce_bwd_kernel(bf16* __restrict__ logits, long ld, const float* _
   *p = o;
 }
 
+// Same, plus per-column partial sums of dlogits (the lm_head bias gradient) over chunks of
+// CE_ROWS rows: colpart[chunk][V] (fp32, pre-rounding).  Grid (ceil(V/8/256), ceil(M/CE_ROWS)):
+// a thread walks CE_ROWS rows of one 8-column group, so the 412 MB dlogits pass also yields
+// db without a second read of it.
+constexpr int CE_ROWS = 64;
+__global__ void __launch_bounds__(256) ce_bwd_colsum_kernel(bf16* __restrict__ logits, long ld,
+                                                           const float* __restrict__ lse,
+                                                           const int* __restrict__ labels, int M, int V, int vstart,
+                                                           int n_valid, float scale, float* __restrict__ colpart) {
+  const int n = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (n >= V) return;
+  const int m0 = blockIdx.y * CE_ROWS, m1 = min(M, m0 + CE_ROWS);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int m = m0; m < m1; ++m) {
+    bf16x8* p = (bf16x8*)(logits + (long)m * ld + n);
+    const bf16x8 v = *p;
+    const float l = lse[m];
+    const int lab = labels[m] - vstart;
+    bf16x8 o;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int c = n + r;
+      float g = c < n_valid ? __expf((float)v[r] - l) : 0.f;
+      if (c == lab) g -= 1.f;
+      g *= scale;
+      cs[r] += g;
+      o[r] = f2bf(g);
+    }
+    *p = o;
+  }
+  float* out = colpart + (long)blockIdx.y * V + n;
+  *(f32x4*)out = f32x4{cs[0], cs[1], cs[2], cs[3]};
+  *(f32x4*)(out + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+}
+
 // ---------------------------------------------------------------- optimizer
 constexpr int SS_BLOCKS = 1024;
 
@@ -414,9 +450,19 @@ int dtc_ce_combine(const float* part, int M, int P, long srow, long spart, const
   return 0;
 }
 
+int dtc_ce_colsum_rows() { return CE_ROWS; }
+
+// colpart (optional): [ceil(M/CE_ROWS)][V] fp32 column partial sums of dlogits
 int dtc_ce_bwd(bf16* logits, long ld, const float* lse, const int* labels, int M, int V, int vstart, int n_valid,
-               float scale, hipStream_t st) {
+               float scale, float* colpart, hipStream_t st) {
   if (V % 8 || ld % 8) return 3003;
+  if (colpart) {
+    dim3 grid((V / 8 + 255) / 256, (M + CE_ROWS - 1) / CE_ROWS);
+    hipLaunchKernelGGL(ce_bwd_colsum_kernel, grid, dim3(256), 0, st, logits, ld, lse, labels, M, V, vstart, n_valid,
+                       scale, colpart);
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
   long n = (long)M * (V / 8);
   hipLaunchKernelGGL(ce_bwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, logits, ld, lse, labels, M, V, vstart,
                      n_valid, scale);

@@ -409,19 +409,22 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
 
 
 // ============================================================================================
-// 256x256 tile, 8 waves (2 along M x 4 along N, 128x64 per wave), for the large forward-layout
-// GEMMs (the lm_head: [4096 x 50304 x 512]).  Why a second kernel: at 128^2 / 64x64-per-wave
-// the LDS->VGPR traffic equals the MFMA rate (1/64+1/64 B per FLOP) and the L2->LDS traffic is
-// 64 FLOP/B, so those tiles cap near ~40 % of peak; 128x64 per wave cuts LDS bytes/FLOP by 25 %
-// and the 256^2 block halves L2 bytes/FLOP.  1 block/CU (128 KB LDS), so the staging is direct
+// 256x256 tile, 8 waves (2 along M x 4 along N, 128x64 per wave), for the lm_head-sized GEMMs
+// (fwd [4096 x 50304 x 512], wgrad [50304 x 512 x 4096], dgrad [4096 x 512 x 50304]).  Why a
+// second kernel: at 128^2 / 64x64-per-wave the LDS->VGPR traffic equals the MFMA rate
+// (1/64+1/64 B per FLOP) and the L2->LDS traffic is 64 FLOP/B, so those tiles cap near ~40 % of
+// peak; 128x64 per wave cuts LDS bytes/FLOP by 25 % and the 256^2 block halves L2 bytes/FLOP
+// (measured main loop 1.0-1.3 PF/s).  1 block/CU (128 KB LDS), so staging is direct
 // global->LDS DMA (global_load_lds_dwordx4, no staging VGPRs, cdna_hip_programming.md §5):
 // tile k+1 streams into the other LDS buffer while the MFMAs consume tile k.
-//  * LDS image per operand: [256 rows][64 k] bf16, 128-B rows, 16-B chunk c stored at
-//    c ^ ((row>>1)&7): the DMA destination is lane-linear per wave (8 rows per instruction), the
-//    swizzle is applied on the per-lane SOURCE address, and a fragment read (16 rows x one
-//    chunk per 16-lane group) hits 16 distinct 16-B bank groups -> conflict-free ds_read_b128.
-//  * Out-of-range rows (ragged M/N edge) are clamped to the last row: they only feed outputs
-//    the epilogue never stores.  K must be a multiple of 64.
+//  * K-major operand image: [256 rows][64 k] bf16 (128-B rows); 16-B chunk c of row r stored at
+//    c ^ ((r>>1)&7).  MN-major image: [64 k][256 rows] (512-B rows); chunk c of k-row r stored at
+//    c ^ mn_swz(r).  The DMA destination is lane-linear per wave, so the swizzle is applied on the
+//    per-lane SOURCE address; every fragment read below is bank-conflict-free.
+//  * Both operand kinds deliver the natural k order (K-major: one ds_read_b128 per fragment;
+//    MN-major: two ds_read_b64_tr_b16 over k-rows 8g..8g+3 / 8g+4..8g+7), so any pairing works.
+//  * Out-of-range rows/cols (ragged edges) are clamped to valid addresses: they only feed outputs
+//    the epilogue never stores.  K (per split) must be a multiple of 64; MN-major extents % 8 == 0.
 constexpr int NT2 = 512;
 constexpr int BIG = 256;
 constexpr int IMG = BIG * 64;  // elements per operand image
@@ -429,36 +432,70 @@ constexpr int IMG = BIG * 64;  // elements per operand image
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef __attribute__((address_space(1))) void* glb_vptr;
 
-__device__ __forceinline__ int swz_off(int row, int c) { return row * 64 + ((c ^ ((row >> 1) & 7)) << 3); }
+// MN-major image swizzle: 16-B chunk c of k-row r lives at c ^ mn_swz(r).  The 8 k-rows one
+// ds_read_b64_tr_b16 pass touches ({0-3, 8-11} + 16u, or +4) get 8 distinct 32-B bank windows.
+__device__ __forceinline__ int mn_swz(int r) { return 2 * ((r & 3) | ((r >> 1) & 4)); }
 
+template <bool KMAJ>
 __device__ __forceinline__ void dma_tile(const bf16* __restrict__ X, long ldx, int r0, int rmax, int k0, bf16* img,
                                          int wave, int lane) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int blk = q * 8 + wave;  // 8-row group: one 1-KB DMA instruction per wave
-    const int row = blk * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
-    const int grow = min(r0 + row, rmax - 1);
-    __builtin_amdgcn_global_load_lds((glb_vptr)(X + (long)grow * ldx + k0 + c * 8), (lds_vptr)(img + blk * 512), 16,
-                                     0, 0);
+    const int blk = q * 8 + wave;  // one 1-KB DMA instruction per wave
+    if (KMAJ) {                    // 8 rows x 128 B
+      const int row = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int grow = min(r0 + row, rmax - 1);
+      __builtin_amdgcn_global_load_lds((glb_vptr)(X + (long)grow * ldx + k0 + c * 8), (lds_vptr)(img + blk * 512), 16,
+                                       0, 0);
+    } else {                       // 2 k-rows x 512 B
+      const int kr = blk * 2 + (lane >> 5);
+      const int c = (lane & 31) ^ mn_swz(kr);
+      const int col = min(r0 + c * 8, rmax - 8);
+      __builtin_amdgcn_global_load_lds((glb_vptr)(X + (long)(k0 + kr) * ldx + col), (lds_vptr)(img + blk * 512), 16,
+                                       0, 0);
+    }
   }
 }
 
-template <int EPI, bool OUTF32>
+// MFMA fragment of 16-row group t (0..15) at k-chunk kk (32 k), natural k order (lane group g
+// holds k = 8g..8g+7): K-major = one ds_read_b128; MN-major = two ds_read_b64_tr_b16 over the
+// k-rows 8g..8g+3 and 8g+4..8g+7 (the transpose hands lane i column i of the 4 rows).
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 big_frag(const bf16* img, int t, int kk, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  if (KMAJ) {
+    const int row = t * 16 + li;
+    return *(const bf16x8*)(img + row * 64 + (((kk * 4 + g) ^ ((row >> 1) & 7)) << 3));
+  } else {
+    const int q = li >> 2, pp = li & 3;
+    const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
+    const int c = 2 * t + (pp >> 1), w = (pp & 1) * 4;
+    const bf16* p0 = img + k0 * 256 + ((c ^ mn_swz(k0)) << 3) + w;
+    const bf16* p1 = img + k1 * 256 + ((c ^ mn_swz(k1)) << 3) + w;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p1));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
 __global__ void __launch_bounds__(NT2, 1)
-gemm256_nt_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
-                  int tiles_m, int tiles_n, int gm, Epi e) {
+gemm256_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+               int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
   constexpr int TM = 8, TN = 4;  // 16x16 fragments per wave: 128 (m) x 64 (n)
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   const int ntiles = tiles_m * tiles_n;
-  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int lid = xcd_remap(blockIdx.x, ntiles * split);
+  const int tile = lid % ntiles, z = lid / ntiles;
   const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
   const int gm_eff = min(gm, tiles_m - grp * gm);
   const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
   const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
-  const int nk = K / 64;
+  const int kbeg = z * k_per_split;
+  const int nk = min(k_per_split, K - kbeg) / 64;
 
   f32x4 acc[TN][TM];
 #pragma unroll
@@ -466,10 +503,10 @@ gemm256_nt_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  dma_tile(A, lda, m0, M, 0, smem, wave, lane);
-  dma_tile(B, ldb, n0, N, 0, smem + IMG, wave, lane);
+  dma_tile<AK>(A, lda, m0, M, kbeg, smem, wave, lane);
+  dma_tile<BKM>(B, ldb, n0, N, kbeg, smem + IMG, wave, lane);
   EpiPre<TN, TM> pre;  // epilogue operands: loaded under the main loop, not after it
-  if (EPI == EPI_LMHEAD || EPI == EPI_STORE)
+  if (split == 1 && (EPI == EPI_LMHEAD || EPI == EPI_STORE))
     epi_prefetch<TN, TM>(e, m0 + wm * 128, n0 + wn * 64, lane, EPI == EPI_LMHEAD, pre);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -478,17 +515,16 @@ gemm256_nt_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__
     const bf16* sB = sA + IMG;
     if (kt + 1 < nk) {
       bf16* nA = smem + ((kt + 1) & 1) * 2 * IMG;
-      dma_tile(A, lda, m0, M, (kt + 1) * 64, nA, wave, lane);
-      dma_tile(B, ldb, n0, N, (kt + 1) * 64, nA + IMG, wave, lane);
+      dma_tile<AK>(A, lda, m0, M, kbeg + (kt + 1) * 64, nA, wave, lane);
+      dma_tile<BKM>(B, ldb, n0, N, kbeg + (kt + 1) * 64, nA + IMG, wave, lane);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 fa[TM], fb[TN];
-      const int c = kk * 4 + (lane >> 4);
 #pragma unroll
-      for (int j = 0; j < TM; ++j) fa[j] = *(const bf16x8*)(sA + swz_off(wm * 128 + j * 16 + (lane & 15), c));
+      for (int j = 0; j < TM; ++j) fa[j] = big_frag<AK>(sA, wm * 8 + j, kk, lane);
 #pragma unroll
-      for (int i = 0; i < TN; ++i) fb[i] = *(const bf16x8*)(sB + swz_off(wn * 64 + i * 16 + (lane & 15), c));
+      for (int i = 0; i < TN; ++i) fb[i] = big_frag<BKM>(sB, wn * 4 + i, kk, lane);
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -498,17 +534,29 @@ gemm256_nt_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__
     __syncthreads();                                  // ... and every other wave's; reads of kt done
   }
 
+  const int g4 = 4 * (lane >> 4);
+  if (split > 1) {  // fp32 slab z; splitk_reduce sums the slabs in a fixed order
+    float* sl = slab + (long)z * M * N;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+        const int n = n0 + wn * 64 + i * 16 + g4;
+        if (m < M && n < N) *(f32x4*)(sl + (long)m * N + n) = acc[i][j];  // N % 4 == 0 (checked by host)
+      }
+    return;
+  }
   bf16* stage = smem + wave * (128 * 64);  // main-loop buffers are free after the last barrier
   if (EPI == EPI_LMHEAD) {
     lmhead_epilogue<TN, TM>(acc, e, m0 + wm * 128, n0 + wn * 64, tn_idx * 4 + wn, lane, pre, stage);
     return;
   }
   if (EPI == EPI_STORE && !OUTF32) {
-    const int g4s = 4 * (lane >> 4);
     f32x4 bb[TN];
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wn * 64 + i * 16 + g4s;
+      const int n = n0 + wn * 64 + i * 16 + g4;
       bb[i] = pre.bb[i];
       if (e.bias && n < N && n + 4 > N)
         for (int r = 0; r < 4; ++r) bb[i][r] = n + r < N ? e.bias[n + r] : 0.f;
@@ -532,7 +580,6 @@ gemm256_nt_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__
       for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  const int g4 = 4 * (lane >> 4);
 #pragma unroll
   for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -640,16 +687,29 @@ int launch_sz(const GemmArgs& a, const Plan& p, hipStream_t st) {
 }
 
 
-// the 256^2 kernel pays when it still fills the chip twice over (lm_head-sized problems)
-bool use_big(int M, int N, int K) {
-  static const int enabled = [] { const char* v = getenv("DTC_GEMM256"); return v ? atoi(v) : 1; }();
-  if (!enabled || K % 64) return false;
+// The 256^2 kernel pays on lm_head-sized problems.  Returns the split-K factor (0 = use the
+// 128/64 kernels).  layout 0 (fwd): no split; layout 1 (dgrad through the lm_head, K = vocab):
+// split so ~256 blocks run; layout 2 (wgrad): no split (a 103 MB fp32 output; extra slab passes
+// cost more than the last partial wave of tiles).
+int big_split(int layout, int M, int N, int K) {
+  // DTC_GEMM256: bit mask of layouts allowed to use it (1 fwd, 2 dgrad, 4 wgrad; default all)
+  static const int enabled = [] { const char* v = getenv("DTC_GEMM256"); return v ? atoi(v) : 7; }();
+  if (!(enabled & (1 << layout)) || K % 64) return 0;
+  if (layout != 0 && N % 8) return 0;              // MN-major B extent (dgrad / wgrad)
+  if (layout == 2 && M % 8) return 0;              // MN-major A extent (wgrad)
   const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
-  return t >= 512;
+  if (layout == 0) return t >= 512 ? 1 : 0;
+  if (layout == 2) return (t >= 256 && K >= 1024) ? 1 : 0;
+  if (K < 16384 || t > 256) return 0;              // dgrad: only the huge-K (vocab) reduction
+  int split = (int)std::max(1L, 256 / t);
+  while (split > 1 && (K / 64) / split < 8) --split;
+  return split;
 }
 
-template <int EPI, bool OUTF32>
-int launch_big(const GemmArgs& a, hipStream_t st) {
+inline int big_kps(int K, int split) { return ((K / 64 + split - 1) / split) * 64; }
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   Epi e;
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
@@ -658,10 +718,20 @@ int launch_big(const GemmArgs& a, hipStream_t st) {
   e.nparts = tiles_n * 4;
   const int ntiles = tiles_m * tiles_n;
   int gm = tiles_m;
-  if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
-  hipLaunchKernelGGL((gemm256_nt_kernel<EPI, OUTF32>), dim3(ntiles), dim3(NT2), 0, st, (const bf16*)a.A, a.lda,
-                     (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, e);
+  if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles * split / 8 + tiles_n - 1) / tiles_n));
+  const int kps = big_kps(a.K, split);
+  if (split > 1 && (a.ws_bytes < (long)split * a.M * a.N * 4 || a.N % 4)) return 1005;
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
+                     (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
+                     (float*)a.workspace, e);
   DTC_CHECK_LAUNCH();
+  if (split > 1) {
+    long MN = (long)a.M * a.N;
+    int blocks = (int)((MN / 4 + 255) / 256);
+    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, split, MN,
+                       (float*)a.C, a.ldc, a.N, a.beta);
+    DTC_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -669,11 +739,13 @@ int launch_big(const GemmArgs& a, hipStream_t st) {
 
 extern "C" {
 
-int dtc_lmhead_nparts(int M, int N, int K) { return use_big(M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }
+int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }
 
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   Plan p = make_plan(M, N, K, layout == 2 ? 1 : (layout == 1 ? 2 : 0));
-  return p.split > 1 ? (long)p.split * M * N * 4 : 0;
+  const int bs = big_split(layout, M, N, K);
+  const int split = bs ? bs : p.split;
+  return split > 1 ? (long)split * M * N * 4 : 0;
 }
 
 int dtc_gemm(const GemmArgs* a, hipStream_t st) {
@@ -684,11 +756,12 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   const bool f32 = a->c_f32 != 0;
   if (a->layout == 0) {
     Plan p = make_plan(a->M, a->N, a->K, 0);
-    if (use_big(a->M, a->N, a->K)) {
-      if (epi == EPI_LMHEAD) return launch_big<EPI_LMHEAD, false>(*a, st);
-      if (epi == EPI_GELU) return launch_big<EPI_GELU, false>(*a, st);
-      if (epi == EPI_RESID) return launch_big<EPI_RESID, true>(*a, st);
-      if (epi == EPI_STORE) return f32 ? launch_big<EPI_STORE, true>(*a, st) : launch_big<EPI_STORE, false>(*a, st);
+    if (big_split(0, a->M, a->N, a->K)) {
+      if (epi == EPI_LMHEAD) return launch_big<true, true, EPI_LMHEAD, false>(*a, 1, st);
+      if (epi == EPI_GELU) return launch_big<true, true, EPI_GELU, false>(*a, 1, st);
+      if (epi == EPI_RESID) return launch_big<true, true, EPI_RESID, true>(*a, 1, st);
+      if (epi == EPI_STORE)
+        return f32 ? launch_big<true, true, EPI_STORE, true>(*a, 1, st) : launch_big<true, true, EPI_STORE, false>(*a, 1, st);
       return 1003;
     }
     if (epi == EPI_LMHEAD) {
@@ -703,6 +776,10 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   }
   if (a->layout == 1) {
     if (a->N % 8) return 1004;
+    if (epi == EPI_STORE && f32) {
+      const int bs = big_split(1, a->M, a->N, a->K);
+      if (bs) return launch_big<true, false, EPI_STORE, true>(*a, bs, st);
+    }
     Plan p = make_plan(a->M, a->N, a->K, (epi == EPI_STORE && f32) ? 2 : 0);
     if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;
     if (epi == EPI_DGELU) return launch_sz<true, false, EPI_DGELU, false>(*a, p, st);
@@ -713,6 +790,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->layout == 2) {
     if (a->M % 8 || a->N % 8) return 1004;
     if (epi != EPI_STORE || !f32 || a->bias) return 1003;
+    if (big_split(2, a->M, a->N, a->K)) return launch_big<false, false, EPI_STORE, true>(*a, 1, st);
     Plan p = make_plan(a->M, a->N, a->K, 1);
     if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;
     return launch_sz<false, false, EPI_STORE, true>(*a, p, st);

@@ -34,6 +34,13 @@ from ..ops import xent as X
 from ..parallel.buffers import FlatParams
 
 
+# where the lm_head weight gradient runs: on the backward side stream (default, overlaps the
+# last layers' backward) or on the main stream right after the dgrad (A/B knob)
+import os as _os
+
+_LMHEAD_WGRAD_MAIN = _os.environ.get("DTC_LMHEAD_WGRAD", "side") == "main"
+
+
 class NoComm:
     """TP communicator stub for tp_size == 1."""
 
@@ -236,10 +243,16 @@ class GPTStage:
     def head_backward(self, ctx: Dict, grad_scale: float, beta: float):
         f = self.flat
         x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
-        dlogits = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale)
-        self.side.run(lambda: (G.wgrad(dlogits, yf, f.g("lm_head.w"), beta),
-                               G.colsum(dlogits, f.g("lm_head.b"), beta)), dlogits, yf)
+        # one pass: dlogits in place + column partials of it (the bias gradient's input)
+        dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale, colpart=True)
+        # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
+        # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
         dyf = G.matmul_nn(dlogits, f.w("lm_head.w"))
+        wg = lambda: (G.wgrad(dlogits, yf, f.g("lm_head.w"), beta), G.colsum(colp, f.g("lm_head.b"), beta))
+        if _LMHEAD_WGRAD_MAIN:
+            wg()
+        else:
+            self.side.run(wg, dlogits, yf, colp)
         del logits, dlogits
         self.tp.all_reduce_(dyf)
         last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None

@@ -82,7 +82,8 @@ def _declare(lib):
         "dtc_attn_bwd": ([vp, vp, vp, vp, vp, vp, i, i, i, i, l, f, vp, l, vp], i),
         "dtc_attn_bwd_workspace_bytes": ([i, i, i, i], l),
         "dtc_ce_combine": ([vp, i, i, l, l, vp, vp, vp, f, vp, i, vp], i),
-        "dtc_ce_bwd": ([vp, l, vp, vp, i, i, i, i, f, vp], i),
+        "dtc_ce_bwd": ([vp, l, vp, vp, i, i, i, i, f, vp, vp], i),
+        "dtc_ce_colsum_rows": ([], i),
         "dtc_sumsq_segments": ([vp, vp, i, vp, vp, vp, l, vp], i),
         "dtc_sumsq_workspace_bytes": ([], l),
         "dtc_sumsq_partial": ([vp, vp, i, vp, i, vp], i),

@@ -81,8 +81,11 @@ def ce_finalize(rowstats: torch.Tensor, label_logit: torch.Tensor, loss_scale: f
 
 
 def ce_backward_inplace(logits: torch.Tensor, lse: torch.Tensor, labels: torch.Tensor, vocab_start: int,
-                        n_valid: int, grad_scale: float) -> torch.Tensor:
-    """logits → dlogits = (exp(logits − lse) − onehot)·grad_scale (pad columns 0), in place."""
+                        n_valid: int, grad_scale: float, colpart: bool = False):
+    """logits → dlogits = (exp(logits − lse) − onehot)·grad_scale (pad columns 0), in place.
+
+    ``colpart=True`` also returns fp32 column partial sums of dlogits ``[R, V]`` (R row chunks)
+    from the same pass — the lm_head bias gradient is their column sum (``gemm.colsum``)."""
     M, Vl = logits.shape
     if not logits.is_cuda:
         p = torch.exp(logits.float() - lse[:, None])
@@ -93,7 +96,14 @@ def ce_backward_inplace(logits: torch.Tensor, lse: torch.Tensor, labels: torch.T
         rows = torch.nonzero(inside)[:, 0]
         p[rows, loc[rows]] -= 1.0
         logits.copy_((p * grad_scale).to(logits.dtype))
+        if colpart:
+            return logits, (p * grad_scale).sum(0, keepdim=True)
         return logits
-    N.check(N.lib().dtc_ce_bwd(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), M, Vl,
-                               vocab_start, n_valid, grad_scale, N.stream_ptr(logits.device)), "dtc_ce_bwd")
-    return logits
+    L = N.lib()
+    cp = None
+    if colpart:
+        R = (M + int(L.dtc_ce_colsum_rows()) - 1) // int(L.dtc_ce_colsum_rows())
+        cp = torch.empty(R, Vl, dtype=torch.float32, device=logits.device)
+    N.check(L.dtc_ce_bwd(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), M, Vl, vocab_start,
+                         n_valid, grad_scale, N.ptr(cp), N.stream_ptr(logits.device)), "dtc_ce_bwd")
+    return (logits, cp) if colpart else logits

@@ -62,7 +62,7 @@ def test_gemm_resid_gelu(cuda):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 512, 1536), (4096, 2048, 512), (4096, 512, 50304), (256, 128, 64), (256, 64, 96),
-                                   (256, 32, 64)])
+                                   (256, 32, 64), (2000, 384, 40000)])
 def test_gemm_nn(cuda, M, N, K):
     dy, w = _r(M, K, seed=5), _r(K, N, scale=0.05, seed=6)
     dx = G.matmul_nn(dy, w)
@@ -73,7 +73,7 @@ def test_gemm_nn(cuda, M, N, K):
 
 
 @pytest.mark.parametrize("Mtok,N,K", [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048),
-                                      (4096, 50304, 512), (128, 64, 64), (512, 200, 96)])
+                                      (4096, 50304, 512), (128, 64, 64), (512, 200, 96), (3072, 50000, 384)])
 def test_gemm_wgrad(cuda, Mtok, N, K):
     dy, x = _r(Mtok, N, seed=8), _r(Mtok, K, seed=9)
     dw = torch.full((N, K), 3.0, device=cuda)
@@ -205,12 +205,18 @@ def test_lmhead_ce(cuda, M, D, V, Vp):
     lse, loss = X.ce_finalize(rowstat.unsqueeze(0).contiguous(), lab, 1.0 / M)
     ref = torch.nn.functional.cross_entropy(h.float().cpu() @ w.float().cpu()[:V].t() + b.cpu()[:V], labels.long())
     assert abs(loss.item() - ref.item()) < 2e-2 * abs(ref.item()), (loss.item(), ref.item())
+    lg2 = logits.clone()
     X.ce_backward_inplace(logits, lse, labels.to(cuda), 0, V, 1.0 / M)
+    lg2, cp = X.ce_backward_inplace(lg2, lse, labels.to(cuda), 0, V, 1.0 / M, colpart=True)
+    assert torch.equal(lg2, logits)  # the fused column-partial variant writes the same dlogits
+    db = torch.zeros(Vp, device=cuda)
+    G.colsum(cp, db)
     lf = h.float().cpu() @ w.float().cpu().t() + b.cpu()
     lf[:, V:] = float("-inf")
     p = torch.softmax(lf, -1)
     p[torch.arange(M), labels.long()] -= 1
     _close(logits.cpu(), p / M, 3e-2, "dlogits")
+    _close(db.cpu(), (p / M).sum(0), 1e-2, "dbias")  # p from bf16 logits vs fp32 reference
     assert logits[:, V:].abs().max().item() == 0.0
 
 
