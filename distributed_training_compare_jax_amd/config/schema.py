@@ -109,6 +109,7 @@ class TrainConfig:
     use_graph: bool = True
     profile: bool = False
     watchdog_s: float = 900.0
+    tp_comm: str = "auto"
     dp_bucket_mb: float = 64.0
     dp_tail_mb: float = 16.0
     dp_embed_gather: bool = True

@@ -697,10 +697,12 @@ int big_split(int layout, int M, int N, int K) {
   if (!(enabled & (1 << layout)) || K % 64) return 0;
   if (layout != 0 && N % 8) return 0;              // MN-major B extent (dgrad / wgrad)
   if (layout == 2 && M % 8) return 0;              // MN-major A extent (wgrad)
+  static const int min_tiles = [] { const char* v = getenv("DTC_BIG_MIN_TILES"); return v ? atoi(v) : 512; }();
   const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
-  if (layout == 0) return t >= 512 ? 1 : 0;
+  if (layout == 0) return t >= min_tiles ? 1 : 0;
   if (layout == 2) return (t >= 256 && K >= 1024) ? 1 : 0;
-  if (K < 16384 || t > 256) return 0;              // dgrad: only the huge-K (vocab) reduction
+  if (K < 16384) return t >= min_tiles ? 1 : 0;   // dgrad, ordinary K: whole tiles
+  if (t > 256) return 0;                           // dgrad through the vocab: split-K
   int split = (int)std::max(1L, 256 / t);
   while (split > 1 && (K / 64) / split < 8) --split;
   return split;
@@ -776,9 +778,14 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   }
   if (a->layout == 1) {
     if (a->N % 8) return 1004;
-    if (epi == EPI_STORE && f32) {
+    {
       const int bs = big_split(1, a->M, a->N, a->K);
-      if (bs) return launch_big<true, false, EPI_STORE, true>(*a, bs, st);
+      if (bs > 1 && epi == EPI_STORE && f32) return launch_big<true, false, EPI_STORE, true>(*a, bs, st);
+      if (bs == 1 && a->K < 16384) {
+        if (epi == EPI_DGELU) return launch_big<true, false, EPI_DGELU, false>(*a, 1, st);
+        if (epi == EPI_STORE)
+          return f32 ? launch_big<true, false, EPI_STORE, true>(*a, 1, st) : launch_big<true, false, EPI_STORE, false>(*a, 1, st);
+      }
     }
     Plan p = make_plan(a->M, a->N, a->K, (epi == EPI_STORE && f32) ? 2 : 0);
     if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;

@@ -1,0 +1,147 @@
+// Peer-to-peer all-reduce over xGMI for the latency-bound tensor-parallel messages
+// (4 all-reduces of the [tokens, d_model] fp32 residual per layer).
+//
+// Every rank allocates one uncached device buffer, exports it with hipIpcGetMemHandle and maps
+// every peer's buffer (hipIpcOpenMemHandle), so a kernel on rank r can load any peer's memory
+// directly over the point-to-point xGMI links — all 7 links of an 8-GPU node at once, instead
+// of the one outgoing link a ring step uses.  The all-reduce is two-shot:
+//
+//   copy   x -> own buffer half (h = call parity)
+//   barrier
+//   reduce-scatter: rank r sums slice r of every peer's half h, in rank order, into its own half
+//   barrier
+//   all-gather: out[slice q] = peer q's reduced slice (own slice local)
+//
+// so each rank moves 2(W-1)/W of the message over xGMI, and every rank computes the SAME sum in
+// the SAME order (bitwise identical replicas).  Alternating halves makes a third barrier
+// unnecessary: call k+2 rewrites half h only after passing call k+1's barriers, which every rank
+// reaches only after finishing call k.
+//
+// Barriers: rank r stores the epoch into flags[r] of every peer (system-scope release) and spins
+// on its own flags[p] >= epoch (system-scope acquire).  The epoch is a device counter, so the
+// whole sequence is plain stream-ordered kernels that hipGraph capture records like any other
+// kernel (no graph cut, unlike an eager RCCL call).  Every spin is bounded: after ~10 s it sets
+// an error word and exits, so a missing peer shows up as an error, never as a hung GPU.
+#include "common.h"
+#include <algorithm>
+#include <cstring>
+
+namespace {
+
+constexpr int P2P_MAX = 8;
+constexpr int FLAG_BYTES = 4096;  // flag area at the start of each buffer (epoch per source rank)
+
+struct PeerTable {
+  unsigned char* base[P2P_MAX];  // buffer base of every rank (own included), as mapped here
+};
+
+__device__ __forceinline__ uint64_t wall_clock() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+
+__global__ void p2p_barrier_kernel(PeerTable t, int rank, int world, uint32_t* __restrict__ epoch,
+                                   int* __restrict__ err) {
+  const int p = threadIdx.x;
+  const uint32_t e = epoch[0] + 1;
+  __threadfence_system();  // this rank's prior writes (its buffer half) before the signal
+  if (p < world && p != rank) {
+    uint32_t* peer_flag = (uint32_t*)t.base[p] + rank;
+    __hip_atomic_store(peer_flag, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t* mine = (const uint32_t*)t.base[rank] + p;
+    const uint64_t t0 = wall_clock();
+    while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock() - t0 > 1000000000ull) {  // ~10 s at 100 MHz
+        atomicExch(err, 1000 + p);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (p == 0) epoch[0] = e;
+}
+
+// copy x into own half h (h read from the epoch counter parity: 2 barriers per call)
+__global__ void p2p_stage_kernel(const f32x4* __restrict__ x, PeerTable t, int rank, long n4, long half_bytes,
+                                 const uint32_t* __restrict__ epoch) {
+  const int h = (epoch[0] >> 1) & 1;
+  f32x4* dst = (f32x4*)(t.base[rank] + FLAG_BYTES + h * half_bytes);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) dst[i] = x[i];
+}
+
+__global__ void p2p_reduce_scatter_kernel(PeerTable t, int rank, int world, long n4, long half_bytes,
+                                          const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 1) >> 1) & 1;  // one barrier has passed since the stage
+  const long chunk = (n4 + world - 1) / world;
+  const long lo = rank * chunk, hi = min(n4, lo + chunk);
+  const long off = FLAG_BYTES + h * half_bytes;
+  for (long i = lo + (long)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (long)gridDim.x * blockDim.x) {
+    f32x4 s = ((const f32x4*)(t.base[0] + off))[i];
+    for (int p = 1; p < world; ++p) s += ((const f32x4*)(t.base[p] + off))[i];
+    ((f32x4*)(t.base[rank] + off))[i] = s;
+  }
+}
+
+__global__ void p2p_all_gather_kernel(PeerTable t, int world, long n4, long half_bytes, f32x4* __restrict__ out,
+                                      const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 2) >> 1) & 1;
+  const long chunk = (n4 + world - 1) / world;
+  const long off = FLAG_BYTES + h * half_bytes;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(i / chunk);
+    out[i] = ((const f32x4*)(t.base[q] + off))[i];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+long dtc_p2p_flag_bytes() { return FLAG_BYTES; }
+
+// uncached device buffer (flags + 2 data halves) and its IPC handle (64 bytes)
+int dtc_p2p_alloc(long bytes, void** ptr, char* handle) {
+  hipError_t e = hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*ptr, 0, FLAG_BYTES);
+  if (e != hipSuccess) return (int)e;
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, *ptr);
+  if (e != hipSuccess) return (int)e;
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "handle size");
+  memcpy(handle, &h, sizeof(h));
+  return 0;
+}
+
+int dtc_p2p_open(const char* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+int dtc_p2p_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+int dtc_p2p_free(void* ptr) { return (int)hipFree(ptr); }
+
+// out = sum over ranks of x (fp32, n % 4 == 0, n*4 <= half_bytes).  x and out may alias.
+int dtc_p2p_allreduce(const float* x, float* out, long n, void* const* bases, int rank, int world, long half_bytes,
+                      uint32_t* epoch, int* err, hipStream_t st) {
+  if (world < 1 || world > P2P_MAX || n % 4 || n * 4 > half_bytes) return 4001;
+  PeerTable t;
+  for (int p = 0; p < P2P_MAX; ++p) t.base[p] = (unsigned char*)(p < world ? bases[p] : nullptr);
+  const long n4 = n / 4;
+  const int blocks = (int)std::min(1024L, std::max(1L, (n4 + 255) / 256));
+  hipLaunchKernelGGL(p2p_stage_kernel, dim3(blocks), dim3(256), 0, st, (const f32x4*)x, t, rank, n4, half_bytes, epoch);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err);
+  DTC_CHECK_LAUNCH();
+  const int rs_blocks = (int)std::min(1024L, std::max(1L, (n4 / world + 255) / 256));
+  hipLaunchKernelGGL(p2p_reduce_scatter_kernel, dim3(rs_blocks), dim3(256), 0, st, t, rank, world, n4, half_bytes,
+                     epoch);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(p2p_all_gather_kernel, dim3(blocks), dim3(256), 0, st, t, world, n4, half_bytes, (f32x4*)out,
+                     epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

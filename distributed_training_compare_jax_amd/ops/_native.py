@@ -75,6 +75,12 @@ def _declare(lib):
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, vp], i),
         "dtc_colsum_workspace_bytes": ([i, i], l),
         "dtc_embed_fwd": ([vp, vp, vp, vp, i, i, i, i, f, l, vp, l, vp], i),
+        "dtc_p2p_flag_bytes": ([], l),
+        "dtc_p2p_alloc": ([l, vp, vp], i),
+        "dtc_p2p_open": ([vp, vp], i),
+        "dtc_p2p_close": ([vp], i),
+        "dtc_p2p_free": ([vp], i),
+        "dtc_p2p_allreduce": ([vp, vp, l, vp, i, i, l, vp, vp, vp], i),
         "dtc_embed_sort_bits": ([i], i),
         "dtc_embed_sort": ([vp, i, i, vp, vp], i),
         "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),

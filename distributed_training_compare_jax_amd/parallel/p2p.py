@@ -1,0 +1,87 @@
+"""xGMI peer-to-peer all-reduce for tensor-parallel activations (``csrc/p2p.hip``).
+
+SURVEY §2.3 / §5.8: TP makes 4 all-reduces of the fp32 residual ``[tokens, d_model]`` per
+layer (+1 for the head).  On an 8×MI355X node every GPU has a direct xGMI link to every other
+one; a ring all-reduce drives one outgoing link per step, while this two-shot kernel lets every
+rank read its slice from all peers at once (reduce-scatter), then read every peer's reduced
+slice (all-gather), through IPC-mapped peer buffers.
+
+Being ordinary stream-ordered kernels (barriers are device-side epoch flags), the collective is
+captured INTO the step's hipGraph: the TP step no longer cuts its graph at every all-reduce the
+way an eager RCCL call does.  The sum runs in rank order on every rank, so TP replicas stay
+bitwise identical.  RCCL remains the path for anything else (scalars, non-fp32, oversize).
+
+Handles are exchanged once over the process group (``all_gather_object``), so the same code runs
+on a real node (RCCL group) and in the one-GPU multi-process tests (gloo group, all ranks on one
+device — IPC within a device works the same way).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _native as N
+
+
+class P2PAllReduce:
+    def __init__(self, group, rank: int, world: int, device, max_bytes: int):
+        assert 1 <= world <= 8, "P2P all-reduce supports up to 8 ranks (one xGMI hive)"
+        self.rank, self.world = rank, world
+        self.device = torch.device(device)
+        self.half = (int(max_bytes) + 4095) // 4096 * 4096
+        L = N.lib()
+        total = int(L.dtc_p2p_flag_bytes()) + 2 * self.half
+        ptr = ctypes.c_void_p()
+        handle = ctypes.create_string_buffer(64)
+        with torch.cuda.device(self.device):
+            N.check(L.dtc_p2p_alloc(total, ctypes.addressof(ptr), ctypes.addressof(handle)), "dtc_p2p_alloc")
+        self._own = ptr.value
+        handles = [None] * world
+        dist.all_gather_object(handles, bytes(handle.raw), group=group)
+        bases = []
+        self._opened = []
+        with torch.cuda.device(self.device):
+            for p, h in enumerate(handles):
+                if p == rank:
+                    bases.append(self._own)
+                    continue
+                q = ctypes.c_void_p()
+                hb = ctypes.create_string_buffer(h, 64)
+                N.check(L.dtc_p2p_open(ctypes.addressof(hb), ctypes.addressof(q)), "dtc_p2p_open")
+                bases.append(q.value)
+                self._opened.append(q.value)
+        self._bases = (ctypes.c_void_p * 8)(*(bases + [None] * (8 - world)))
+        self._bases_ptr = ctypes.addressof(self._bases)
+        self.epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # all ranks' flag areas are zero before anyone's first barrier can run
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)
+
+    def supports(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
+                and t.numel() * 4 <= self.half)
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        N.check(N.lib().dtc_p2p_allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._bases_ptr, self.rank, self.world,
+                                          self.half, self.epoch.data_ptr(), self.err.data_ptr(),
+                                          N.stream_ptr(t.device)), "dtc_p2p_allreduce")
+        return t
+
+    def check(self):
+        """Raise if a barrier timed out (a peer never arrived); call at a host sync point."""
+        e = int(self.err.item())
+        if e:
+            raise RuntimeError(f"P2P all-reduce: rank {self.rank} timed out waiting for rank {e - 1000}")
+
+    def close(self):
+        L = N.lib()
+        for q in self._opened:
+            L.dtc_p2p_close(ctypes.c_void_p(q))
+        self._opened = []
+        if self._own:
+            L.dtc_p2p_free(ctypes.c_void_p(self._own))
+            self._own = None

@@ -18,15 +18,21 @@ import torch.distributed as dist
 
 
 class TPComm:
-    def __init__(self, group, size: int, rank: int, program):
+    """``p2p`` (optional :class:`parallel.p2p.P2PAllReduce`) takes the fp32 activation
+    all-reduces as in-graph xGMI kernels; everything else goes through RCCL (a graph cut)."""
+
+    def __init__(self, group, size: int, rank: int, program, p2p=None):
         self.group = group
         self.size = size
         self.rank = rank
         self.program = program
+        self.p2p = p2p
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
             return t
+        if self.p2p is not None and self.p2p.supports(t):
+            return self.p2p.all_reduce_(t)
         g = self.group
         self.program.comm(lambda: dist.all_reduce(t, group=g))
         return t

@@ -65,7 +65,14 @@ class Engine:
 
         # ---- step program, comms, model, optimizer
         self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu)
-        self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program)
+        self.p2p = None
+        mode = train_cfg.tp_comm
+        if tp > 1 and on_gpu and (mode == "p2p" or (mode == "auto" and dinfo.backend == "nccl")):
+            from ..parallel.p2p import P2PAllReduce
+
+            rows = self.mb_rows if pp > 1 else self.b_local
+            self.p2p = P2PAllReduce(m.tp_group, m.tp_idx, tp, self.device, rows * T * model_cfg.d_model * 4)
+        self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program, p2p=self.p2p)
         self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
                               act_dtype=self.act_dtype,
                               side_stream=on_gpu and os.environ.get("DTC_NO_SIDE_STREAM", "0") != "1")
@@ -228,6 +235,8 @@ class Engine:
     def loss_value(self) -> float:
         """Blocking read of the global mean loss (reference: float(np.asarray(loss)), train.py:82)."""
         v = float(self.loss.item())
+        if self.p2p is not None:
+            self.p2p.check()
         return v / self.mesh.dp
 
     def grad_norm(self) -> float:

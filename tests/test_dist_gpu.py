@@ -53,6 +53,7 @@ def single(cuda):
     ("dp", {}),
     ("dp", {"dp_embed_gather": False}),
     ("tp", {}),
+    ("tp", {"tp_comm": "p2p"}),
     ("pp", {"pp_microbatches": 2, "pp_clip": "global"}),
     ("pp", {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b"}),
 ])
@@ -62,5 +63,66 @@ def test_two_ranks_match_single_gpu(single, parallel, kw):
     got = res[0]["losses"]
     assert got == pytest.approx(ref, rel=2e-2, abs=2e-2), (parallel, got, ref)
     assert res[0]["graphs"] >= 2  # step was captured and cut at the collectives
+    if kw.get("tp_comm") == "p2p":  # activation all-reduces are in-graph kernels: few graph cuts left
+        assert res[0]["comms"] <= 6, res[0]["comms"]
     if parallel == "dp":  # replicas stay bit-identical (deterministic local embedding grads)
         assert torch.equal(res[0]["params"], res[1]["params"])
+
+
+def _p2p_worker(out_dir):
+    os.environ["DTC_DIST_BACKEND"] = "gloo"
+    import torch.distributed as dist
+
+    from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
+    from distributed_training_compare_jax_amd.parallel.p2p import P2PAllReduce
+
+    d = init_distributed("cuda")
+    ar = P2PAllReduce(dist.group.WORLD, d.rank, d.world, d.device, 1 << 20)
+    res = {}
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.randn(d.world, 4096 * k, generator=g) for k in (1, 3, 64)]
+    for k, x in enumerate(xs):  # eager, several sizes (alternating buffer halves)
+        t = x[d.rank].to(d.device).clone()
+        ar.all_reduce_(t)
+        res[f"eager{k}"] = t.cpu()
+    # captured in a hipGraph and replayed: the device epoch counter keeps ranks in step
+    t = torch.zeros(4096 * 2, device=d.device)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        gr.capture_begin(capture_error_mode="thread_local")
+        ar.all_reduce_(t)
+        gr.capture_end()
+    torch.cuda.current_stream().wait_stream(s)
+    outs = []
+    for it in range(3):
+        t.copy_(torch.full((4096 * 2,), float(d.rank + 1 + it)))
+        dist.barrier()
+        gr.replay()
+        torch.cuda.synchronize()
+        outs.append(t.cpu().clone())
+    res["graph"] = outs
+    ar.check()
+    torch.save(res, os.path.join(out_dir, f"p2p{d.rank}.pt"))
+    ar.close()
+    destroy()
+
+
+def test_p2p_allreduce_two_ranks_one_gpu():
+    """IPC-mapped two-shot all-reduce, 2 processes on one GPU: exact sum, identical on both ranks,
+    eager and replayed from a captured hipGraph."""
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        spawn(_p2p_worker, world, args=(td,))
+        r = [torch.load(os.path.join(td, f"p2p{i}.pt")) for i in range(world)]
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.randn(world, 4096 * k, generator=g) for k in (1, 3, 64)]
+    for k, x in enumerate(xs):
+        ref = x[0] + x[1]
+        assert torch.equal(r[0][f"eager{k}"], r[1][f"eager{k}"])
+        assert torch.allclose(r[0][f"eager{k}"], ref, atol=1e-6), k
+    for it in range(3):
+        exp = float(1 + it) + float(2 + it)
+        for i in range(world):
+            assert torch.all(r[i]["graph"][it] == exp), (i, it)

@@ -206,6 +206,7 @@ def test_lmhead_ce(cuda, M, D, V, Vp):
     ref = torch.nn.functional.cross_entropy(h.float().cpu() @ w.float().cpu()[:V].t() + b.cpu()[:V], labels.long())
     assert abs(loss.item() - ref.item()) < 2e-2 * abs(ref.item()), (loss.item(), ref.item())
     lg2 = logits.clone()
+    lg0 = logits.float().cpu()  # the kernel's bf16 logits (-inf pads): the reference for the bias grad
     X.ce_backward_inplace(logits, lse, labels.to(cuda), 0, V, 1.0 / M)
     lg2, cp = X.ce_backward_inplace(lg2, lse, labels.to(cuda), 0, V, 1.0 / M, colpart=True)
     assert torch.equal(lg2, logits)  # the fused column-partial variant writes the same dlogits
@@ -216,7 +217,9 @@ def test_lmhead_ce(cuda, M, D, V, Vp):
     p = torch.softmax(lf, -1)
     p[torch.arange(M), labels.long()] -= 1
     _close(logits.cpu(), p / M, 3e-2, "dlogits")
-    _close(db.cpu(), (p / M).sum(0), 1e-2, "dbias")  # p from bf16 logits vs fp32 reference
+    pb = torch.softmax(lg0, -1)
+    pb[torch.arange(M), labels.long()] -= 1
+    _close(db.cpu(), (pb / M).sum(0), 2e-3, "dbias")
     assert logits[:, V:].abs().max().item() == 0.0
 
 
