@@ -52,11 +52,14 @@ def _spawn_target(args):
 @click.option("--device", type=click.Choice(["auto", "cuda", "cpu"]), default=None)
 @click.option("--log_every", type=int, default=None, help="override train_config.log_every")
 @click.option("--warmup_steps", type=int, default=None, help="override the 5 untimed warmup steps")
+@click.option("--output_dir", default=None, help="override train_config.output_dir")
 @click.option("--profile", is_flag=True, default=False,
               help="roctx ranges + device step times + Chrome trace in <output_dir>/trace/")
 def main(train_config_path: str, model_config_path: str, optim_config_path: str, nproc, steps, device, log_every,
-         warmup_steps, profile):
+         warmup_steps, output_dir, profile):
     overrides = {}
+    if output_dir is not None:
+        overrides["output_dir"] = output_dir
     if profile:
         overrides["profile"] = True
     if steps is not None:
