@@ -610,6 +610,179 @@ __global__ void splitk_reduce(const float* __restrict__ slab, int split, long MN
   *(f32x4*)c = s;
 }
 
+// ============================================================================================
+// DMA-pipelined layer GEMM (64x64 or 128x128 tiles, 4 waves, NSTAGE-deep LDS ring).
+// The layer GEMMs ([4096 x 512..2048 x 512..4096]) give each CU only 1-2 tiles, so they are bound
+// by how many operand bytes a CU keeps in flight from L2, not by MFMA rate: the register-staged
+// kernel above holds 1-2 K-tiles per block.  Here operands stream global->LDS by
+// global_load_lds (no staging VGPRs) into an NSTAGE ring with NSTAGE-1 K-tiles in flight: each
+// K-step waits only for the OLDEST tile with a counted s_waitcnt vmcnt(N) and a raw s_barrier
+// (cdna_hip_programming.md §5 "Pipelining across barriers": __syncthreads would drain every
+// DMA), then refills the slot the previous step just finished reading.
+//  * K-major image [R][64 k] (128-B rows, chunk swizzle c ^ ((r>>1)&7)), MN-major image
+//    [64 k][R] (R*2-B rows, swizzle dimg_mn_swz) — DMA destination lane-linear, swizzle on the
+//    source address, conflict-free ds_read_b128 / ds_read_b64_tr_b16 fragment reads, natural
+//    k order for both (any layout pairing).
+//  * Ragged edges: rows/cols clamped to valid addresses (only feed unstored outputs).
+template <int R>
+__device__ __forceinline__ int dimg_mn_swz(int r) {
+  if (R == 64) return 2 * (((r >> 1) & 1) | ((r >> 2) & 2));  // 128-B rows: 4 windows per bank row
+  return 2 * ((r & 3) | ((r >> 1) & 4));                      // >= 256-B rows: 8 windows
+}
+
+template <int R, bool KMAJ>
+struct DImg {
+  static constexpr int ELEMS = R * 64;
+  static constexpr int NI = ELEMS * 2 / 1024 / 4;  // 1-KB DMA instructions per wave (4 waves)
+  __device__ __forceinline__ static void dma(const bf16* __restrict__ X, long ldx, int r0, int rmax, int k0, bf16* img,
+                                             int wave, int lane) {
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int blk = q * 4 + wave;
+      const bf16* src;
+      if (KMAJ) {
+        const int row = blk * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        src = X + (long)min(r0 + row, rmax - 1) * ldx + k0 + c * 8;
+      } else {
+        constexpr int LPR = R / 8;  // lanes per k-row
+        const int kr = blk * (64 / LPR) + lane / LPR;
+        const int c = (lane % LPR) ^ dimg_mn_swz<R>(kr);
+        src = X + (long)(k0 + kr) * ldx + min(r0 + c * 8, rmax - 8);
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(img + blk * 512), 16, 0, 0);
+    }
+  }
+  __device__ __forceinline__ static bf16x8 frag(const bf16* img, int t, int kk, int lane) {
+    const int g = lane >> 4, li = lane & 15;
+    if (KMAJ) {
+      const int row = t * 16 + li;
+      return *(const bf16x8*)(img + row * 64 + (((kk * 4 + g) ^ ((row >> 1) & 7)) << 3));
+    } else {
+      const int q = li >> 2, pp = li & 3;
+      const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
+      const int c = 2 * t + (pp >> 1), w = (pp & 1) * 4;
+      const bf16* p0 = img + k0 * R + ((c ^ dimg_mn_swz<R>(k0)) << 3) + w;
+      const bf16* p1 = img + k1 * R + ((c ^ dimg_mn_swz<R>(k1)) << 3) + w;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p1));
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `ahead` K-tiles' DMAs (G instructions each) are still in flight
+template <int G, int MAXAHEAD>
+__device__ __forceinline__ void wait_tiles(int ahead) {
+  if (MAXAHEAD >= 3 && ahead >= 3) wait_vmcnt<3 * G>();
+  else if (MAXAHEAD >= 2 && ahead >= 2) wait_vmcnt<2 * G>();
+  else if (ahead >= 1) wait_vmcnt<G>();
+  else wait_vmcnt<0>();
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int NSTAGE, bool AK, bool BKM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(NT, (BM * BN <= 64 * 64) ? 2 : 1)
+gemm_dma_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+                int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+  using IA = DImg<BM, AK>;
+  using IB = DImg<BN, BKM>;
+  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
+  constexpr int G = IA::NI + IB::NI;  // DMA instructions per thread per K-tile
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, ntiles * split);
+  const int tile = lid % ntiles, z = lid / ntiles;
+  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+  const int gm_eff = min(gm, tiles_m - grp * gm);
+  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  const int kbeg = z * k_per_split;
+  const int nk = min(k_per_split, K - kbeg) / 64;
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) {
+      IA::dma(A, lda, m0, M, kbeg + s * 64, smem + s * STAGE, wave, lane);
+      IB::dma(B, ldb, n0, N, kbeg + s * 64, smem + s * STAGE + IA::ELEMS, wave, lane);
+    }
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_tiles<G, NSTAGE - 2>(min(NSTAGE - 2, nk - 1 - kt));  // tile kt landed (this wave)
+    raw_barrier();                                            // ... for every wave; slot kt-1 free
+    const int nt = kt + NSTAGE - 1;
+    if (nt < nk) {
+      bf16* sl = smem + (nt % NSTAGE) * STAGE;
+      IA::dma(A, lda, m0, M, kbeg + nt * 64, sl, wave, lane);
+      IB::dma(B, ldb, n0, N, kbeg + nt * 64, sl + IA::ELEMS, wave, lane);
+    }
+    const bf16* sA = smem + (kt % NSTAGE) * STAGE;
+    const bf16* sB = sA + IA::ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = IA::frag(sA, wm * TM + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = IB::frag(sB, wn * TN + i, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  const int g4 = 4 * (lane >> 4);
+  if (split > 1) {
+    float* sl = slab + (long)z * M * N;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm * WM + j * 16 + (lane & 15);
+        const int n = n0 + wn * WN + i * 16 + g4;
+        if (m < M) {
+          float* c = sl + (long)m * N + n;
+          if (n + 4 <= N) *(f32x4*)c = acc[i][j];
+          else for (int r = 0; r < 4; ++r) if (n + r < N) c[r] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if (EPI == EPI_LMHEAD) {
+    EpiPre<TN, TM> pre;
+    epi_prefetch<TN, TM>(e, m0 + wm * WM, n0 + wn * WN, lane, true, pre);
+    lmhead_epilogue<TN, TM>(acc, e, m0 + wm * WM, n0 + wn * WN, tn_idx * 2 + wn, lane, pre);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + (lane & 15);
+      const int n = n0 + wn * WN + i * 16 + g4;
+      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+    }
+}
+
 struct Plan {
   int bm, bn, bk, split;
 };
@@ -659,7 +832,26 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
   dim3 grid(ntiles * p.split);
   const int ab = operand_bytes(AK, a.M, a.K, a.lda), bb = operand_bytes(BKM, a.N, a.K, a.ldb);
-  if (BM == 64 && p.bk == 32)
+  // DMA-pipelined variant, DTC_GEMM_DMA bit mask: 1 = 64x64 forward layout (default: measured
+  // fc2/out_proj fwd 22 -> 18.6 us), 2 = 64x64 dgrad/wgrad layouts (measured slower: off),
+  // 4 = 128x128 (stages from DTC_DMA_STAGES128, 2 or 3; measured no gain: off)
+  static const int dma_mask = [] { const char* v = getenv("DTC_GEMM_DMA"); return v ? atoi(v) : 1; }();
+  static const int st128 = [] { const char* v = getenv("DTC_DMA_STAGES128"); return v ? atoi(v) : 2; }();
+  const int dma_bit = BM == 64 ? ((AK && BKM) ? 1 : 2) : 4;
+  if (p.bk == 64 && (dma_mask & dma_bit)) {
+    if constexpr (BM == 64)
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, 4, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A,
+                         a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
+                         (float*)a.workspace, e);
+    else if (st128 >= 3)
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, 3, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A,
+                         a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
+                         (float*)a.workspace, e);
+    else
+      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, 2, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A,
+                         a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
+                         (float*)a.workspace, e);
+  } else if (BM == 64 && p.bk == 32)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A, a.lda,
                        ab, (const bf16*)a.B, a.ldb, bb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
                        (float*)a.workspace, e);

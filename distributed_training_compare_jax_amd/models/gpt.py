@@ -66,6 +66,7 @@ class SideStream:
     def __init__(self, device, enabled: bool):
         self.stream = torch.cuda.Stream(device) if (enabled and torch.device(device).type == "cuda") else None
         self.keep = []
+        self._pending = []
 
     def run(self, fn, *keep):
         if self.stream is None:
@@ -76,7 +77,23 @@ class SideStream:
             fn()
         self.keep.extend(keep)
 
+    def defer(self, fn, *keep):
+        """Queue side-stream work; :meth:`flush` forks once for everything queued.  In a replayed
+        hipGraph every fork/join is a cross-queue dependency costing ~10-15 us of idle time, so
+        a layer's four weight-gradient GEMMs (+ its norm chunk) go out as ONE fork after the
+        layer's dgrad chain instead of four forks interleaved with it."""
+        self._pending.append(fn)  # queued even without a stream: CPU runs keep the same ordering
+        if self.stream is not None:
+            self.keep.extend(keep)
+
+    def flush(self):
+        if not self._pending:
+            return
+        fns, self._pending = self._pending, []
+        self.run(lambda: [f() for f in fns])
+
     def join(self):
+        self.flush()
         if self.stream is not None:
             torch.cuda.current_stream().wait_stream(self.stream)
             self.keep.clear()
@@ -179,22 +196,22 @@ class GPTStage:
         self._bias_fused.discard(l)
         # MLP (dgrad chain on the main stream, weight grads on the side stream)
         if fc2b_fused:
-            side.run(lambda: G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), dx3_c, gact)
+            side.defer(lambda: G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), dx3_c, gact)
         else:
-            side.run(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), G.colsum(dx3, f.g(p + "fc2.b"), beta)),
+            side.defer(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), G.colsum(dx3, f.g(p + "fc2.b"), beta)),
                      dx3_c, gact, dx3)
         du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
-        side.run(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta), G.colsum(du, f.g(p + "fc1.b"), beta)), du, y2)
+        side.defer(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta), G.colsum(du, f.g(p + "fc1.b"), beta)), du, y2)
         dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
         tp.all_reduce_(dy2)
         # LN2 backward also emits out_proj.b's gradient (Σ_rows dx2)
         dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
         # attention
-        side.run(lambda: G.wgrad(dx2_c, o, f.g(p + "out.w"), beta), dx2_c, o)
+        side.defer(lambda: G.wgrad(dx2_c, o, f.g(p + "out.w"), beta), dx2_c, o)
         do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
         dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                           self.heads_local).view(batch * T, -1)
-        side.run(lambda: (G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta), G.colsum(dqkv, f.g(p + "qkv.b"), beta)),
+        side.defer(lambda: (G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta), G.colsum(dqkv, f.g(p + "qkv.b"), beta)),
                  dqkv, y1)
         dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
         tp.all_reduce_(dy1)
@@ -248,16 +265,19 @@ class GPTStage:
         # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
         # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
         dyf = G.matmul_nn(dlogits, f.w("lm_head.w"))
-        wg = lambda: (G.wgrad(dlogits, yf, f.g("lm_head.w"), beta), G.colsum(colp, f.g("lm_head.b"), beta))
+        wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta),
+                                                G.colsum(cp, f.g("lm_head.b"), beta))
         if _LMHEAD_WGRAD_MAIN:
             wg()
         else:
-            self.side.run(wg, dlogits, yf, colp)
+            self.side.defer(wg, dlogits, yf, colp)
         del logits, dlogits
         self.tp.all_reduce_(dyf)
         last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None
-        return self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
-                            bias_grad=None if last is None else self._prev_fc2b(last))
+        out = self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
+                           bias_grad=None if last is None else self._prev_fc2b(last))
+        self.side.flush()
+        return out
 
     def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None):
         """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist."""
@@ -265,6 +285,7 @@ class GPTStage:
             dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta)
             if hook is not None:
                 hook(l)
+            self.side.flush()  # one fork per layer: its wgrads (+ anything the hook queued)
         return dx, dx_c
 
 

@@ -163,17 +163,24 @@ class Engine:
         h = st.stage_forward(h, b, ctx)
         st.head_forward(h, self.labels, 1.0 / (b * T), ctx, loss_out=self.loss)
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
-        bk, opt, side = self.buckets, self.opt, st.side.run
+        bk, opt, side = self.buckets, self.opt, st.side.defer
         if dp == 1:
             opt.ready_upto(bk.head_end_offset(), side)
             hook = lambda l: opt.ready_upto(bk.layer_end_offset(l), side)
         else:
-            bk.ready_upto(bk.head_end_offset())
-            first = self.layout.layers[0]
-            # the last layer's bucket waits until the embedding gather is queued: the gather
-            # feeds compute (embed backward), the bucket only the optimizer
-            hook = (lambda l: bk.ready_upto(bk.layer_end_offset(l)) if l != first else None) if self.embed_gather \
-                else (lambda l: bk.ready_upto(bk.layer_end_offset(l)))
+            # A bucket's all-reduce cuts the graph, which joins the side stream (capture needs it);
+            # issuing with a one-layer lag means the join finds that layer's weight-gradient
+            # GEMMs (which ran under the next layer's dgrads) already done instead of blocking
+            # the dgrad chain on them.  The first layer's bucket waits for the embedding gather
+            # (that collective feeds compute; the bucket only the optimizer).
+            layers = list(self.layout.layers)
+            first = layers[0]
+
+            def hook(l):
+                if self.embed_gather and l == first:
+                    return
+                nxt = l + 1
+                bk.ready_upto(bk.layer_end_offset(nxt) if nxt in layers else bk.head_end_offset())
         dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=hook)
         if self.embed_gather:
             out, g = self.dh_all, self.mesh.dp_group
@@ -238,6 +245,34 @@ class Engine:
         if self.p2p is not None:
             self.p2p.check()
         return v / self.mesh.dp
+
+    # -- host pipelining: read step t's loss while step t+1 is already queued --------------
+    def loss_handle(self):
+        """Queue a copy of this step's loss to pinned host memory (2-slot ring) + an event.
+
+        With the step replayed from a graph, the host can enqueue step t+1 (its H2D batch copy
+        and graph launch) before blocking on step t's loss, so the GPU never idles on the host
+        between steps; every step's loss is still read (one step later)."""
+        if self.device.type != "cuda":
+            return self.loss_value()
+        if not hasattr(self, "_loss_host"):
+            self._loss_host = [torch.zeros(1, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+            self._loss_slot = 0
+        slot = self._loss_host[self._loss_slot]
+        self._loss_slot ^= 1
+        slot.copy_(self.loss, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return slot, ev
+
+    def read_loss(self, handle) -> float:
+        if not isinstance(handle, tuple):
+            return handle
+        slot, ev = handle
+        ev.synchronize()
+        if self.p2p is not None:
+            self.p2p.check()
+        return float(slot.item()) / self.mesh.dp
 
     def grad_norm(self) -> float:
         return self.opt.grad_norm()

@@ -73,26 +73,46 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
     running, history, elapsed = [], [], []
     batch = next(data)
     t0 = time.perf_counter()
-    for step in range(1, train_config.steps + 1):
-        eng.set_batch(batch)
-        with tr.device_step(step):
-            eng.run_step()
-        if step < train_config.steps:
-            with tr.span("data"):
-                batch = next(data)  # host data for the next step overlaps this step's GPU work
+    # Host pipelining: step s+1 is enqueued before step s's loss is read (Engine.loss_handle), so
+    # the GPU does not idle on the host between steps.  Every step's loss is still read and
+    # logged, and its elapsed time is stamped when that read returns (as the reference's
+    # blocking float(loss), train/train.py:82-85).  A step that ends on a checkpoint is drained
+    # before the next one is enqueued, so the checkpoint holds exactly that step's state.
+    pending = None
+
+    def finish(s, handle):
+        nonlocal running
         with tr.span("loss sync"):
-            loss = eng.loss_value()
-        dog.beat(step)
+            loss = eng.read_loss(handle)
+        dog.beat(s)
         tr.collect()
         running.append(loss)
         history.append(loss)
         now = time.perf_counter()
         elapsed.append(now - t0)
-        if step % train_config.log_every == 0:
-            say(f"Step: {step} | Avg loss: {np.mean(running):.4f} | Average step time: {(now - t0) / step:.4f}")
+        if s % train_config.log_every == 0:
+            say(f"Step: {s} | Avg loss: {np.mean(running):.4f} | Average step time: {(now - t0) / s:.4f}")
             running = []
-        with tr.span("checkpoint"):
-            maybe_save(eng, train_config, start + train_config.warmup_steps + step)
+
+    for step in range(1, train_config.steps + 1):
+        eng.set_batch(batch)
+        with tr.device_step(step):
+            eng.run_step()
+        handle = eng.loss_handle()
+        if step < train_config.steps:
+            with tr.span("data"):
+                batch = next(data)  # host data for the next step overlaps this step's GPU work
+        if pending is not None:
+            finish(*pending)
+        pending = (step, handle)
+        gstep = start + train_config.warmup_steps + step
+        if train_config.ckpt_every and gstep % train_config.ckpt_every == 0:
+            finish(*pending)
+            pending = None
+            with tr.span("checkpoint"):
+                maybe_save(eng, train_config, gstep)
+    if pending is not None:
+        finish(*pending)
     t1 = time.perf_counter()
     dog.stop()
     say(f"Total time: {t1 - t0}")
