@@ -33,6 +33,30 @@ BASELINE_TOKENS_PER_S = {"dp": 27887.0, "tp": 27919.0, "pp": 19978.0}  # BASELIN
 METRIC = "avg step time (ms) + tokens/sec, GPT-2-small DP/TP/PP at 1/2/4/8 MI355X"
 
 
+def _overrides(items):
+    """KEY=VALUE strings -> TrainConfig kwargs (value parsed as the field's type)."""
+    import dataclasses
+
+    from distributed_training_compare_jax_amd.config.schema import TrainConfig
+
+    types = {f.name: f.type for f in dataclasses.fields(TrainConfig)}
+    out = {}
+    for it in items:
+        k, v = it.split("=", 1)
+        if k not in types:
+            raise SystemExit(f"unknown TrainConfig field {k!r}")
+        t = str(types[k])
+        if "bool" in t:
+            out[k] = v.lower() in ("1", "true", "yes")
+        elif "int" in t:
+            out[k] = int(v)
+        elif "float" in t:
+            out[k] = float(v)
+        else:
+            out[k] = v
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -43,6 +67,8 @@ def main():
     ap.add_argument("--batch_per_gpu", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--pp_schedule", default="1f1b")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra TrainConfig overrides for A/B runs, e.g. --set defer_optimizer=false")
     args = ap.parse_args()
 
     import torch
@@ -68,7 +94,7 @@ def main():
         global_batch, micro, scaling = args.batch_per_gpu, max(2, min(args.batch_per_gpu, 2 * world)), "strong"
     tc = TrainConfig(seed=0, parallel=args.parallel, batch=global_batch, steps=args.steps, log_every=10 ** 9,
                      output_dir="/tmp/bench", pp_microbatches=micro, use_graph=not args.no_graph,
-                     pp_schedule=args.pp_schedule)
+                     pp_schedule=args.pp_schedule, **_overrides(args.set))
     oc = OptimConfig(lr=3e-4, weight_decay=0.1, grad_clip=1.0)
     eng = Engine(mc, tc, oc, dinfo)
     data = get_batch_iterator(global_batch, mc.max_seq_len + 1, seed=0, row0=eng.feed_row0, nrows=eng.feed_rows)
@@ -95,6 +121,7 @@ def main():
             loss = eng.read_loss(pending)
         pending = handle
     loss = eng.read_loss(pending)
+    eng.flush_optimizer()  # the last step's deferred AdamW lands inside the timed region
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0

@@ -20,8 +20,12 @@ are optional and default to the reference behaviour:
   ``dp_bucket_mb`` / ``dp_tail_mb`` (DP grad bucket sizes; the last bucket is kept small
   because its all-reduce is exposed), ``dp_embed_gather`` (DP: all-gather the embedding
   output grads and rebuild wte/wpe grads locally instead of all-reducing the 103 MB table),
-  ``warmup_steps`` (reference hard-codes 5, ``train/train.py:64``),
-  ``grad_reduce_dtype``, ``ckpt_every``/``resume``.
+  ``warmup_steps`` (reference hard-codes 5, ``train/train.py:64``), ``ckpt_every``/``resume``,
+  ``tp_comm`` (``auto`` | ``p2p`` | ``rccl``: TP activation all-reduces as in-graph xGMI
+  peer-to-peer kernels, ``parallel/p2p.py``; ``auto`` = p2p on a GPU RCCL group),
+  ``defer_optimizer`` / ``defer_groups`` (run the non-embedding AdamW under the next step's
+  forward in that many layer groups; exact, off by default: measured neutral at the
+  reference size because the forward kernels slow down under the AdamW's HBM traffic).
 """
 
 from __future__ import annotations
@@ -110,10 +114,11 @@ class TrainConfig:
     profile: bool = False
     watchdog_s: float = 900.0
     tp_comm: str = "auto"
+    defer_optimizer: bool = False
+    defer_groups: int = 4
     dp_bucket_mb: float = 64.0
     dp_tail_mb: float = 16.0
     dp_embed_gather: bool = True
-    grad_reduce_dtype: str = "fp32"
     warmup_steps: int = 5
     ckpt_every: int = 0
     resume: bool = False

@@ -332,9 +332,10 @@ __global__ void sumsq_stage2(const float* __restrict__ part, int P, float* __res
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, bf16* __restrict__ mirror, long n, long n_mirror,
                              const int64_t* __restrict__ step, const float* __restrict__ sumsq, float lr, float b1,
-                             float b2, float eps, float wd, float max_norm) {
+                             float b2, float eps, float wd, float max_norm, const float* __restrict__ enable) {
   long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= n) return;
+  if (enable && enable[0] == 0.f) return;  // deferred update already applied (or none pending)
   const float norm = sqrtf(sumsq[0]);
   const float clip = (max_norm > 0.f && !(norm < max_norm)) ? max_norm / norm : 1.f;
   const float t = (float)step[0];
@@ -498,11 +499,11 @@ int dtc_sum_finish(const float* part, int P, float* out, int64_t* step, hipStrea
 }
 
 int dtc_adamw(float* p, const float* g, float* m, float* v, bf16* mirror, long n, long n_mirror, const int64_t* step,
-              const float* sumsq, float lr, float b1, float b2, float eps, float wd, float max_norm, float unused,
-              hipStream_t st) {
+              const float* sumsq, float lr, float b1, float b2, float eps, float wd, float max_norm,
+              const float* enable, hipStream_t st) {
   if (n % 4 || n_mirror % 4) return 3005;
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks_for(n / 4, 256)), dim3(256), 0, st, p, g, m, v, mirror, n, n_mirror,
-                     step, sumsq, lr, b1, b2, eps, wd, max_norm);
+                     step, sumsq, lr, b1, b2, eps, wd, max_norm, enable);
   DTC_CHECK_LAUNCH();
   return 0;
 }

@@ -114,6 +114,9 @@ class GPTStage:
         self.cfg = cfg
         self.side = SideStream(flat.device, side_stream)
         self._bias_fused = set()  # layers whose fc2.b grad an upstream LN backward already produced
+        # deferred optimizer (train/engine.py): params of layer l / "head" become valid when this
+        # side-stream event fires; the forward waits on it right before first use
+        self.param_ready: Dict = {}
         self.flat = flat
         self.layout = layout
         self.tp = tp if tp is not None else NoComm()
@@ -165,7 +168,13 @@ class GPTStage:
         E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta, keys=keys)
 
     # ------------------------------------------------------------------ block
+    def _await_params(self, key):
+        ev = self.param_ready.pop(key, None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
     def block_forward(self, l: int, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
+        self._await_params(l)
         f, p = self.flat, f"h.{l}."
         tp = self.tp
         lead = tp.rank == 0  # row-parallel bias + residual are added by exactly one TP rank
@@ -243,6 +252,7 @@ class GPTStage:
         """Final LN + lm_head + CE (GPTModel.py:69-74; create_train_step.py:32-34).
 
         Returns a device scalar ``loss_scale · Σ_tokens CE`` (1-element fp32 tensor)."""
+        self._await_params("head")
         f = self.flat
         yf, muf, rsf = LN.layernorm_fwd(x, f.p("lnf.g"), f.p("lnf.b"), self.eps, self.act_dtype)
         lab = labels.reshape(-1)

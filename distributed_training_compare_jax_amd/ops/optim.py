@@ -81,13 +81,17 @@ def sum_finish(part: torch.Tensor, out: torch.Tensor, step: Optional[torch.Tenso
 
 def adamw_flat(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                mirror: Optional[torch.Tensor], n_mirror: int, step: torch.Tensor, sumsq: torch.Tensor,
-               lr: float, b1: float, b2: float, eps: float, wd: float, max_norm: float):
+               lr: float, b1: float, b2: float, eps: float, wd: float, max_norm: float,
+               enable: Optional[torch.Tensor] = None):
     """In-place AdamW on flat fp32 buffers; ``mirror[:n_mirror] = bf16(p[:n_mirror])``.
 
     ``step`` (int64 [1], already incremented) gives t for the bias correction; ``sumsq``
-    (fp32 [1]) is the global Σg² for the clip."""
+    (fp32 [1]) is the global Σg² for the clip.  ``enable`` (fp32 [1], optional): the update is
+    skipped when ``enable[0] == 0`` (device-side switch for the deferred optimizer)."""
     n = p.numel()
     if not p.is_cuda:
+        if enable is not None and float(enable.item()) == 0.0:
+            return
         t = float(step.item())
         norm = float(sumsq.item()) ** 0.5
         scale = 1.0 if (max_norm <= 0 or norm < max_norm) else max_norm / norm
@@ -101,7 +105,7 @@ def adamw_flat(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tenso
             mirror[:n_mirror].copy_(p[:n_mirror])
         return
     N.check(N.lib().dtc_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), N.ptr(mirror), n, n_mirror,
-                              step.data_ptr(), sumsq.data_ptr(), lr, b1, b2, eps, wd, max_norm, 0.0,
+                              step.data_ptr(), sumsq.data_ptr(), lr, b1, b2, eps, wd, max_norm, N.ptr(enable),
                               N.stream_ptr(p.device)), "dtc_adamw")
 
 

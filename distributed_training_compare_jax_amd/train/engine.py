@@ -121,6 +121,33 @@ class Engine:
             self.recv_dx_c = [torch.zeros(self.mb_rows * T, D, dtype=self.act_dtype, device=self.device)
                               for _ in range(self.n_micro)] if self.act_dtype != torch.float32 else self.recv_dx
         self.steps_done = 0
+        # Deferred optimizer (pp == 1, GPU): the step ends with the global norm and the AdamW of
+        # the embedding tables only; the rest of the update runs at the START of the next step
+        # on the side stream, in forward order and in a few layer groups, each group signalling
+        # an event the forward waits on before its first layer.  The HBM-bound AdamW (~2.2 GB of
+        # traffic) then overlaps the compute-bound forward instead of idling the MFMAs at the
+        # end of the step.  Semantics are unchanged (same norm, same update, before each use);
+        # :meth:`flush_optimizer` completes a pending update (checkpoint, end of run, bench).
+        self.defer_opt = bool(on_gpu and pp == 1 and train_cfg.defer_optimizer and self.stage.side.stream is not None)
+        if self.defer_opt:
+            # device-side "an update is pending" switch: the graph always contains the deferred
+            # launch, the kernels skip when nothing is pending (first step, after a flush)
+            self._pending_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
+            L = list(self.layout.layers)
+            bk = self.buckets
+            lo_emb = self.flat.range_of([n for n in ("wte", "wpe") if n in self.flat.slots])[0] \
+                if self.layout.has_embed else self.flat.numel
+            self._emb_range = (lo_emb, self.flat.numel)
+            ng = max(1, min(train_cfg.defer_groups, len(L)))
+            per = (len(L) + ng - 1) // ng
+            self._opt_groups = []  # (first layer, [(lo, hi), ...]) in forward order
+            for gi in range(0, len(L), per):
+                ls = L[gi:gi + per]
+                lo = min(self.flat.range_of([n for n in self.flat.slots if n.startswith(f"h.{l}.")])[0] for l in ls)
+                hi = max(bk.layer_end_offset(l) for l in ls)
+                self._opt_groups.append((ls[0], [(lo, hi)]))
+            if self.layout.has_head:
+                self._opt_groups.append(("head", [(0, bk.head_end_offset())]))
         if on_gpu:
             self._reserve_workspaces()
 
@@ -153,8 +180,41 @@ class Engine:
             self.labels.copy_(h[1], non_blocking=True)
 
     # ------------------------------------------------------------------ step bodies
+    def _launch_deferred_update(self):
+        """Queue the pending AdamW (all but the embedding tables) on the side stream, group by group."""
+        if not self.defer_opt:
+            return
+        st, flag = self.stage, self._pending_dev
+        for key, ranges in self._opt_groups:
+            def upd(ranges=ranges):
+                for lo, hi in ranges:
+                    self.opt.update_range(lo, hi, enable=flag)
+            st.side.run(upd)
+            ev = torch.cuda.Event()
+            ev.record(st.side.stream)
+            st.param_ready[key] = ev
+
+    def _finish_optimizer(self):
+        if self.defer_opt:
+            self.opt.norm()
+            self.opt.update_range(*self._emb_range)
+            O.fill_(self._pending_dev, 1.0)
+        else:
+            self.opt.step()
+
+    def flush_optimizer(self):
+        """Complete a deferred update now (before reading/saving params or ending a run); the
+        next step's in-graph launch then finds nothing pending."""
+        if self.defer_opt:
+            for _, ranges in self._opt_groups:
+                for lo, hi in ranges:
+                    self.opt.update_range(lo, hi, enable=self._pending_dev)
+            O.fill_(self._pending_dev, 0.0)
+            self.stage.param_ready.clear()
+
     def _step_fn_dp_tp(self):
         st, T, b = self.stage, self.T, self.b_local
+        self._launch_deferred_update()
         dp = self.mesh.dp
         ctx: Dict = {}
         step = self.opt.step_t
@@ -194,7 +254,7 @@ class Engine:
         bk.ready_all()
         bk.wait_all()
         self._loss_allreduce()
-        self.opt.step()
+        self._finish_optimizer()
         return self.loss
 
     def _loss_allreduce(self):

@@ -113,6 +113,7 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
                 maybe_save(eng, train_config, gstep)
     if pending is not None:
         finish(*pending)
+    eng.flush_optimizer()  # complete the last step's deferred update (timed)
     t1 = time.perf_counter()
     dog.stop()
     say(f"Total time: {t1 - t0}")

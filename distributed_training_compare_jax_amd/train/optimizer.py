@@ -90,8 +90,9 @@ class FusedAdamW:
             if hi <= offset:
                 self.chunk_ready(i, runner)
 
-    def step(self):
-        f, c = self.flat, self.cfg
+    def norm(self):
+        """Global Σg² (all chunks, fixed order) + step counter bump (+ TP/PP all-reduce)."""
+        f = self.flat
         if self.chunks:
             for i in range(len(self.chunks)):
                 self.chunk_ready(i)
@@ -107,8 +108,21 @@ class FusedAdamW:
             g = self.pp_group
             s = self.sumsq
             self.program.comm(lambda: dist.all_reduce(s, group=g))
-        O.adamw_flat(f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.mirror, f.n_mirror if f.use_mirror else 0,
-                     self.step_t, self.sumsq, c.lr, c.b1, c.b2, c.eps, c.weight_decay, c.grad_clip)
+
+    def update_range(self, lo: int, hi: int, enable=None):
+        """Clip + AdamW over flat[lo:hi] (4-aligned) with the norm/step of the last :meth:`norm`
+        (skipped on device when ``enable[0] == 0``)."""
+        f, c = self.flat, self.cfg
+        if hi <= lo:
+            return
+        nm = (min(max(f.n_mirror - lo, 0), hi - lo) if f.use_mirror else 0)
+        O.adamw_flat(f.params[lo:hi], f.grads[lo:hi], f.exp_avg[lo:hi], f.exp_avg_sq[lo:hi],
+                     f.mirror[lo:lo + max(nm, 4)] if nm > 0 else None, nm, self.step_t, self.sumsq, c.lr, c.b1, c.b2,
+                     c.eps, c.weight_decay, c.grad_clip, enable=enable)
+
+    def step(self):
+        self.norm()
+        self.update_range(0, self.flat.numel)
 
     def grad_norm(self) -> float:
         return float(self.sumsq.item()) ** 0.5

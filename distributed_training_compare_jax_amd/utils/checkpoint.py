@@ -24,6 +24,8 @@ def _dir(output_dir: str, step: int) -> str:
 
 
 def save(eng, output_dir: str, step: int):
+    if hasattr(eng, "flush_optimizer"):
+        eng.flush_optimizer()  # a deferred AdamW must land before params are read
     d = _dir(output_dir, step)
     os.makedirs(d, exist_ok=True)
     f = eng.flat

@@ -109,3 +109,26 @@ def test_profile_device_step_times(cuda, tmp_path):
     assert len(r["device_step_ms"]) == 4 and all(0 < t < 1e4 for t in r["device_step_ms"])
     tr = json.load(open(os.path.join(tmp_path, "trace", "rank0.json")))
     assert any(e["name"].startswith("device step") for e in tr["traceEvents"])
+
+
+def test_deferred_optimizer_matches_immediate(cuda):
+    """defer_optimizer (AdamW under the next step's forward) is an exact reordering: same losses and
+    bit-identical parameters / Adam state after a flush, incl. a flush mid-run (then more steps)."""
+    runs = []
+    for defer in (False, True):
+        eng, mc = _engine(cuda, use_graph=True, preset="ref", vocab=50258, batch=8, defer_optimizer=defer)
+        it = get_batch_iterator(8, mc.max_seq_len + 1)
+        out = []
+        for i in range(6):
+            eng.set_batch(next(it))
+            eng.run_step()
+            out.append(eng.loss_value())
+            if i == 3:
+                eng.flush_optimizer()  # e.g. a checkpoint: the next replay must not re-apply it
+        eng.flush_optimizer()
+        torch.cuda.synchronize()
+        runs.append((out, eng.flat.params.clone(), eng.flat.exp_avg.clone(), eng.flat.mirror.clone()))
+        del eng
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1:], runs[1][1:]):
+        assert torch.equal(a, b)
