@@ -15,6 +15,7 @@
 // one workgroup per 64-key block sweeping the queries; dQ with one workgroup per 64-query
 // block sweeping the keys.  P is recomputed from the saved LSE.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -374,12 +375,322 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
   }
 }
 
+
+// ============================================================================ resident variants
+// For short sequences (T * (hd row + tr image) fits LDS: the reference T = 512, hd = 32) the whole
+// (b, h) K/V (forward, dQ) or Q/dO (dK/dV) panel is loaded into LDS ONCE, then every wave walks
+// its own 16-row group against it with no further barriers: the tiled kernels above pay a
+// global-load + barrier round trip per 64-key tile and are latency-bound on the long causal rows
+// (23 us fwd / 60 us bwd at the reference shape).  Two 1024-thread blocks per (b, h), wave w of
+// block s owning 16-row group 2w+s, so causal work is balanced across the pair and each SIMD
+// interleaves 4 waves.
+constexpr int RES_THREADS = 1024;
+
+template <int LD>
+__device__ __forceinline__ void stage_rows(bf16* lds, const bf16* __restrict__ base, long tok_stride, int T, int HDv,
+                                           int tid) {
+  const int cpr = HDv / 8;
+  for (int c = tid; c < T * cpr; c += RES_THREADS) {
+    const int r = c / cpr, col = (c % cpr) * 8;
+    *(u32x4*)(lds + r * LD + col) = *(const u32x4*)(base + (long)r * tok_stride + col);
+  }
+}
+
+template <int HD>
+__global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+                                                                  float* __restrict__ lse, int B, int T, int H,
+                                                                  float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
+  const int Tp = (T + 63) / 64 * 64;
+  bf16* sK = lds;
+  bf16* sV = lds + Tp * L::KLD;
+  const long ts = 3L * H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  stage_rows<L::KLD>(sK, Kb, ts, T, HD, tid);
+  stage_rows<L::VLD>(sV, Vb, ts, T, HD, tid);
+  for (int c = T * (HD / 8) + tid; c < Tp * (HD / 8); c += RES_THREADS) {  // zero the ragged tail
+    const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
+    *(u32x4*)(sK + r * L::KLD + col) = u32x4{0, 0, 0, 0};
+    *(u32x4*)(sV + r * L::VLD + col) = u32x4{0, 0, 0, 0};
+  }
+  __syncthreads();
+  const int qg = 2 * w + half;
+  if (qg * 16 >= T) return;  // no barrier below
+  const int q = qg * 16 + j;
+  bf16x8 qf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) qf[kc] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + kc * 32 + 8 * g) : bf16x8{};
+  const float c = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 acc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntile = (qg * 16 + 16 + 63) / 64;
+  for (int kt = 0; kt < ntile; ++kt) {
+    const bf16* tK = sK + kt * 64 * L::KLD;
+    const bf16* tV = sV + kt * 64 * L::VLD;
+    const bool diag = kt == ntile - 1;  // only the last tile reaches past the query
+    f32x4 sc[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      sc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) sc[st] = mfma(row_frag(tK, L::KLD, st * 16, kc * 32, lane), qf[kc], sc[st]);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = sc[st][r] * c;
+        if (diag) {
+          const int key = kt * 64 + st * 16 + 4 * g + r;
+          x = (key <= q && key < T) ? x : -INFINITY;
+        }
+        sc[st][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ls = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = exp2f(sc[st][r] - mn);
+        sc[st][r] = pv;
+        ls += pv;
+      }
+    l = l * alpha + ls;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) acc[t] *= alpha;
+    const bf16x8 pf0 = pack_p(sc[0], sc[1]), pf1 = pack_p(sc[2], sc[3]);
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      acc[t] = mfma(tr_frag(tV, L::VLD, 0, t * 16, lane), pf0, acc[t]);
+      acc[t] = mfma(tr_frag(tV, L::VLD, 32, t * 16, lane), pf1, acc[t]);
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (q < T) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long)b * T + q) * H * HD + h * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+      *(bf16x4*)(orow + t * 16 + 4 * g) =
+          bf16x4{f2bf(acc[t][0] * inv), f2bf(acc[t][1] * inv), f2bf(acc[t][2] * inv), f2bf(acc[t][3] * inv)};
+    if (g == 0) lse[((long)b * H + h) * T + q] = (m + __log2f(l)) * LN2;
+  }
+}
+
+// dK, dV with Q and dO resident: wave owns 16 keys (key on the lane), walks queries >= its keys
+template <int HD>
+__global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
+  const int Tp = (T + 63) / 64 * 64 + 64;  // + one tile of slack: query tiles start at 16-row offsets
+  bf16* sQ = lds;
+  bf16* sD = lds + Tp * L::VLD;
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const float* lseb = lse + ((long)b * H + h) * T;
+  const float* delb = delta + ((long)b * H + h) * T;
+  stage_rows<L::VLD>(sQ, Qb, ts, T, HD, tid);
+  stage_rows<L::VLD>(sD, dOb, dts, T, HD, tid);
+  for (int c = T * (HD / 8) + tid; c < Tp * (HD / 8); c += RES_THREADS) {
+    const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
+    *(u32x4*)(sQ + r * L::VLD + col) = u32x4{0, 0, 0, 0};
+    *(u32x4*)(sD + r * L::VLD + col) = u32x4{0, 0, 0, 0};
+  }
+  __syncthreads();
+  const int kg = 2 * w + half;
+  if (kg * 16 >= T) return;
+  const int key = kg * 16 + j;
+  bf16x8 kf[KC], vf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    kf[kc] = key < T ? *(const bf16x8*)(Kb + (long)key * ts + kc * 32 + 8 * g) : bf16x8{};
+    vf[kc] = key < T ? *(const bf16x8*)(Vb + (long)key * ts + kc * 32 + 8 * g) : bf16x8{};
+  }
+  const float c = scale * LOG2E;
+  f32x4 dk[HT], dv[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) { dk[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
+  for (int q0 = kg * 16; q0 < T; q0 += 64) {
+    const bf16* tQ = sQ + q0 * L::VLD;
+    const bf16* tD = sD + q0 * L::VLD;
+    const bool diag = q0 == kg * 16;
+    f32x4 p[4], ds[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        sc = mfma(row_frag(tQ, L::VLD, qt * 16, kc * 32, lane), kf[kc], sc);
+        dp = mfma(row_frag(tD, L::VLD, qt * 16, kc * 32, lane), vf[kc], dp);
+      }
+      const int qr = q0 + qt * 16 + 4 * g;
+      f32x4 l4 = {0.f, 0.f, 0.f, 0.f}, d4 = {0.f, 0.f, 0.f, 0.f};
+      if (qr + 4 <= T) { l4 = *(const f32x4*)(lseb + qr); d4 = *(const f32x4*)(delb + qr); }
+      else for (int r = 0; r < 4; ++r) if (qr + r < T) { l4[r] = lseb[qr + r]; d4[r] = delb[qr + r]; }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qr + r;
+        const bool ok = diag ? (key <= qq && qq < T) : (qq < T);
+        const float pv = ok ? exp2f(sc[r] * c - l4[r] * LOG2E) : 0.f;
+        p[qt][r] = pv;
+        ds[qt][r] = pv * (dp[r] - d4[r]);
+      }
+    }
+#pragma unroll
+    for (int hq = 0; hq < 2; ++hq) {
+      const bf16x8 pb = pack_p(p[2 * hq], p[2 * hq + 1]), dsb = pack_p(ds[2 * hq], ds[2 * hq + 1]);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        dv[t] = mfma(tr_frag(tD, L::VLD, 32 * hq, t * 16, lane), pb, dv[t]);
+        dk[t] = mfma(tr_frag(tQ, L::VLD, 32 * hq, t * 16, lane), dsb, dk[t]);
+      }
+    }
+  }
+  if (key < T) {
+    bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
+    bf16* pv = dqkv + ((long)b * T + key) * ts + (2 * H + h) * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      *(bf16x4*)(pk + t * 16 + 4 * g) = bf16x4{f2bf(dk[t][0] * scale), f2bf(dk[t][1] * scale), f2bf(dk[t][2] * scale),
+                                               f2bf(dk[t][3] * scale)};
+      *(bf16x4*)(pv + t * 16 + 4 * g) = bf16x4{f2bf(dv[t][0]), f2bf(dv[t][1]), f2bf(dv[t][2]), f2bf(dv[t][3])};
+    }
+  }
+}
+
+// dQ with K and V resident: wave owns 16 queries, walks keys <= its queries
+template <int HD>
+__global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
+  const int Tp = (T + 63) / 64 * 64;
+  bf16* sK = lds;
+  bf16* sV = lds + Tp * L::VLD;
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  stage_rows<L::VLD>(sK, Kb, ts, T, HD, tid);
+  stage_rows<L::VLD>(sV, Vb, ts, T, HD, tid);
+  for (int c = T * (HD / 8) + tid; c < Tp * (HD / 8); c += RES_THREADS) {
+    const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
+    *(u32x4*)(sK + r * L::VLD + col) = u32x4{0, 0, 0, 0};
+    *(u32x4*)(sV + r * L::VLD + col) = u32x4{0, 0, 0, 0};
+  }
+  __syncthreads();
+  const int qg = 2 * w + half;
+  if (qg * 16 >= T) return;
+  const int q = qg * 16 + j;
+  bf16x8 qf[KC], df[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    qf[kc] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + kc * 32 + 8 * g) : bf16x8{};
+    df[kc] = q < T ? *(const bf16x8*)(dOb + (long)q * dts + kc * 32 + 8 * g) : bf16x8{};
+  }
+  const float lq = q < T ? lse[((long)b * H + h) * T + q] * LOG2E : 0.f;
+  const float dq_ = q < T ? delta[((long)b * H + h) * T + q] : 0.f;
+  const float c = scale * LOG2E;
+  f32x4 acc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntile = (qg * 16 + 16 + 63) / 64;
+  for (int kt = 0; kt < ntile; ++kt) {
+    const bf16* tK = sK + kt * 64 * L::VLD;
+    const bf16* tV = sV + kt * 64 * L::VLD;
+    const bool diag = kt == ntile - 1;
+    f32x4 ds[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        sc = mfma(row_frag(tK, L::VLD, st * 16, kc * 32, lane), qf[kc], sc);
+        dp = mfma(row_frag(tV, L::VLD, st * 16, kc * 32, lane), df[kc], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = kt * 64 + st * 16 + 4 * g + r;
+        const bool ok = diag ? (kk <= q && kk < T && q < T) : (q < T);
+        const float pv = ok ? exp2f(sc[r] * c - lq) : 0.f;
+        ds[st][r] = pv * (dp[r] - dq_);
+      }
+    }
+#pragma unroll
+    for (int hk = 0; hk < 2; ++hk) {
+      const bf16x8 dsb = pack_p(ds[2 * hk], ds[2 * hk + 1]);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) acc[t] = mfma(tr_frag(tK, L::VLD, 32 * hk, t * 16, lane), dsb, acc[t]);
+    }
+  }
+  if (q < T) {
+    bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+      *(bf16x4*)(pq + t * 16 + 4 * g) = bf16x4{f2bf(acc[t][0] * scale), f2bf(acc[t][1] * scale),
+                                               f2bf(acc[t][2] * scale), f2bf(acc[t][3] * scale)};
+  }
+}
+
+// LDS bytes of the resident kernels; 0 if the sequence does not fit (then the tiled kernels run)
+inline long res_lds_fwd(int T, int HD) { const long Tp = (T + 63) / 64 * 64; return Tp * (AttnLds<32>::KLD + HD + 16) * 2; }
+inline long res_lds_dkdv(int T, int HD) { const long Tp = (T + 63) / 64 * 64 + 64; return 2 * Tp * (HD + 16) * 2; }
+inline long res_lds_dq(int T, int HD) { const long Tp = (T + 63) / 64 * 64; return 2 * Tp * (HD + 16) * 2; }
+constexpr long LDS_MAX = 160 * 1024;
+
+bool use_resident(int T, int HD) {
+  static const int enabled = [] { const char* v = getenv("DTC_ATTN_RESIDENT"); return v ? atoi(v) : 1; }();
+  return enabled && HD == 32 && T <= RES_THREADS / 64 * 2 * 16 && res_lds_fwd(T, HD) <= LDS_MAX &&
+         res_lds_dkdv(T, HD) <= LDS_MAX && res_lds_dq(T, HD) <= LDS_MAX;
+}
+
+template <typename K>
+void allow_lds(K kernel, long bytes) {  // > 64 KB of dynamic LDS must be opted into per kernel
+  (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 }  // namespace
 
 extern "C" {
 
 int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int HD, long flags, float scale,
                  hipStream_t st) {
+  if (use_resident(T, HD)) {
+    allow_lds(attn_fwd_res_kernel<32>, res_lds_fwd(T, HD));
+    hipLaunchKernelGGL(attn_fwd_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_fwd(T, HD), st, qkv, o,
+                       lse, B, T, H, scale);
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
   int nqb = (T + 63) / 64;
   dim3 grid(B * H * nqb);
   if (HD == 32) hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, st, qkv, o, lse, B, T, H, scale);
@@ -397,7 +708,15 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
   long n = (long)B * T * H;
   int nb = (T + 63) / 64;
   dim3 grid(B * H * nb);
-  if (HD == 32) {
+  if (use_resident(T, HD)) {
+    hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
+    allow_lds(attn_bwd_dkdv_res_kernel<32>, res_lds_dkdv(T, HD));
+    allow_lds(attn_bwd_dq_res_kernel<32>, res_lds_dq(T, HD));
+    hipLaunchKernelGGL(attn_bwd_dkdv_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_dkdv(T, HD), st, qkv,
+                       dout, lse, ws, dqkv, B, T, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_dq(T, HD), st, qkv,
+                       dout, lse, ws, dqkv, B, T, H, scale);
+  } else if (HD == 32) {
     hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<32>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
