@@ -385,14 +385,42 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
 // block s owning 16-row group 2w+s, so causal work is balanced across the pair and each SIMD
 // interleaves 4 waves.
 constexpr int RES_THREADS = 1024;
+constexpr int RES_MAXT = 512;  // 16 waves x 2 blocks x 16 rows
 
-template <int LD>
-__device__ __forceinline__ void stage_rows(bf16* lds, const bf16* __restrict__ base, long tok_stride, int T, int HDv,
+// raw v_exp_f32 (softmax arguments are <= 0: no overflow range handling needed; the libm exp2f
+// wraps every call in ldexp/compare/select denormal scaffolding)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// max / sum over the 4 lane groups (lanes j, j+16, j+32, j+48) with the gfx950 row swaps instead
+// of ds_bpermute round trips through LDS
+__device__ __forceinline__ float group_max(float x) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float group_sum(float x) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// whole-sequence [T][HD] panel -> LDS [T][LD]: every load of the thread in flight before any store
+template <int LD, int HD, int MAXT>
+__device__ __forceinline__ void stage_rows(bf16* lds, const bf16* __restrict__ base, long tok_stride, int T, int Tp,
                                            int tid) {
-  const int cpr = HDv / 8;
-  for (int c = tid; c < T * cpr; c += RES_THREADS) {
-    const int r = c / cpr, col = (c % cpr) * 8;
-    *(u32x4*)(lds + r * LD + col) = *(const u32x4*)(base + (long)r * tok_stride + col);
+  constexpr int CPR = HD / 8, PER = (MAXT * CPR + RES_THREADS - 1) / RES_THREADS;
+  u32x4 v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = tid + i * RES_THREADS, r = c / CPR, col = (c % CPR) * 8;
+    v[i] = r < T ? *(const u32x4*)(base + (long)r * tok_stride + col) : u32x4{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = tid + i * RES_THREADS, r = c / CPR, col = (c % CPR) * 8;
+    if (r < Tp) *(u32x4*)(lds + r * LD + col) = v[i];  // rows T..Tp-1 zero-filled
   }
 }
 
@@ -403,7 +431,8 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
   const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64;
   bf16* sK = lds;
@@ -412,13 +441,8 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
   const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
   const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
-  stage_rows<L::KLD>(sK, Kb, ts, T, HD, tid);
-  stage_rows<L::VLD>(sV, Vb, ts, T, HD, tid);
-  for (int c = T * (HD / 8) + tid; c < Tp * (HD / 8); c += RES_THREADS) {  // zero the ragged tail
-    const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
-    *(u32x4*)(sK + r * L::KLD + col) = u32x4{0, 0, 0, 0};
-    *(u32x4*)(sV + r * L::VLD + col) = u32x4{0, 0, 0, 0};
-  }
+  stage_rows<L::KLD, HD, RES_MAXT>(sK, Kb, ts, T, Tp, tid);  // rows >= T are zero-filled
+  stage_rows<L::VLD, HD, RES_MAXT>(sV, Vb, ts, T, Tp, tid);
   __syncthreads();
   const int qg = 2 * w + half;
   if (qg * 16 >= T) return;  // no barrier below
@@ -456,17 +480,16 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
         sc[st][r] = x;
         mt = fmaxf(mt, x);
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = group_max(mt);
     const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);
+    const float alpha = fast_exp2(m - mn);
     m = mn;
     float ls = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(sc[st][r] - mn);
+        const float pv = fast_exp2(sc[st][r] - mn);
         sc[st][r] = pv;
         ls += pv;
       }
@@ -480,8 +503,7 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
       acc[t] = mfma(tr_frag(tV, L::VLD, 32, t * 16, lane), pf1, acc[t]);
     }
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = group_sum(l);
   if (q < T) {
     const float inv = 1.f / l;
     bf16* orow = o + ((long)b * T + q) * H * HD + h * HD;
@@ -501,7 +523,8 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
   const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64 + 64;  // + one tile of slack: query tiles start at 16-row offsets
   bf16* sQ = lds;
@@ -513,13 +536,8 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
   const bf16* dOb = dout + (long)b * T * dts + h * HD;
   const float* lseb = lse + ((long)b * H + h) * T;
   const float* delb = delta + ((long)b * H + h) * T;
-  stage_rows<L::VLD>(sQ, Qb, ts, T, HD, tid);
-  stage_rows<L::VLD>(sD, dOb, dts, T, HD, tid);
-  for (int c = T * (HD / 8) + tid; c < Tp * (HD / 8); c += RES_THREADS) {
-    const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
-    *(u32x4*)(sQ + r * L::VLD + col) = u32x4{0, 0, 0, 0};
-    *(u32x4*)(sD + r * L::VLD + col) = u32x4{0, 0, 0, 0};
-  }
+  stage_rows<L::VLD, HD, RES_MAXT + 64>(sQ, Qb, ts, T, Tp, tid);
+  stage_rows<L::VLD, HD, RES_MAXT + 64>(sD, dOb, dts, T, Tp, tid);
   __syncthreads();
   const int kg = 2 * w + half;
   if (kg * 16 >= T) return;
@@ -548,14 +566,14 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
         dp = mfma(row_frag(tD, L::VLD, qt * 16, kc * 32, lane), vf[kc], dp);
       }
       const int qr = q0 + qt * 16 + 4 * g;
-      f32x4 l4 = {0.f, 0.f, 0.f, 0.f}, d4 = {0.f, 0.f, 0.f, 0.f};
-      if (qr + 4 <= T) { l4 = *(const f32x4*)(lseb + qr); d4 = *(const f32x4*)(delb + qr); }
-      else for (int r = 0; r < 4; ++r) if (qr + r < T) { l4[r] = lseb[qr + r]; d4[r] = delb[qr + r]; }
+      // T % 4 == 0 (use_resident): a 4-row group is entirely in or out of range -> selects, no branch
+      const int qc = min(qr, T - 4);
+      f32x4 l4 = *(const f32x4*)(lseb + qc), d4 = *(const f32x4*)(delb + qc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qr + r;
         const bool ok = diag ? (key <= qq && qq < T) : (qq < T);
-        const float pv = ok ? exp2f(sc[r] * c - l4[r] * LOG2E) : 0.f;
+        const float pv = ok ? fast_exp2(sc[r] * c - l4[r] * LOG2E) : 0.f;
         p[qt][r] = pv;
         ds[qt][r] = pv * (dp[r] - d4[r]);
       }
@@ -590,7 +608,8 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
   const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64;
   bf16* sK = lds;
@@ -600,13 +619,8 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
   const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
   const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
   const bf16* dOb = dout + (long)b * T * dts + h * HD;
-  stage_rows<L::VLD>(sK, Kb, ts, T, HD, tid);
-  stage_rows<L::VLD>(sV, Vb, ts, T, HD, tid);
-  for (int c = T * (HD / 8) + tid; c < Tp * (HD / 8); c += RES_THREADS) {
-    const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
-    *(u32x4*)(sK + r * L::VLD + col) = u32x4{0, 0, 0, 0};
-    *(u32x4*)(sV + r * L::VLD + col) = u32x4{0, 0, 0, 0};
-  }
+  stage_rows<L::VLD, HD, RES_MAXT>(sK, Kb, ts, T, Tp, tid);
+  stage_rows<L::VLD, HD, RES_MAXT>(sV, Vb, ts, T, Tp, tid);
   __syncthreads();
   const int qg = 2 * w + half;
   if (qg * 16 >= T) return;
@@ -641,7 +655,7 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
       for (int r = 0; r < 4; ++r) {
         const int kk = kt * 64 + st * 16 + 4 * g + r;
         const bool ok = diag ? (kk <= q && kk < T && q < T) : (q < T);
-        const float pv = ok ? exp2f(sc[r] * c - lq) : 0.f;
+        const float pv = ok ? fast_exp2(sc[r] * c - lq) : 0.f;
         ds[st][r] = pv * (dp[r] - dq_);
       }
     }
@@ -669,7 +683,7 @@ constexpr long LDS_MAX = 160 * 1024;
 
 bool use_resident(int T, int HD) {
   static const int enabled = [] { const char* v = getenv("DTC_ATTN_RESIDENT"); return v ? atoi(v) : 1; }();
-  return enabled && HD == 32 && T <= RES_THREADS / 64 * 2 * 16 && res_lds_fwd(T, HD) <= LDS_MAX &&
+  return enabled && HD == 32 && T % 4 == 0 && T <= RES_MAXT && res_lds_fwd(T, HD) <= LDS_MAX &&
          res_lds_dkdv(T, HD) <= LDS_MAX && res_lds_dq(T, HD) <= LDS_MAX;
 }
 
