@@ -801,11 +801,22 @@ Plan make_plan(int M, int N, int K, int allow_split) {
     p.split = (int)std::max(1L, std::min((long)nk / 64, (512 + t128 - 1) / t128));
     return p;
   }
+  static const int wgrad_tile = [] { const char* v = getenv("DTC_WGRAD_TILE"); return v ? atoi(v) : 64; }();
+  if (allow_split == 1 && wgrad_tile == 128 && t128 < 256) {  // weight gradients: 128^2 tiles + split-K
+    static const int target = [] { const char* v = getenv("DTC_WGRAD_BLOCKS"); return v ? atoi(v) : 256; }();
+    while (t128 * p.split < target && nk / (p.split * 2) >= 8) p.split *= 2;
+    return p;
+  }
   if (t128 < 256) {
     p.bm = p.bn = 64;
     const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
     if (allow_split == 1)
-      while (t64 * p.split < 512 && nk / (p.split * 2) >= 4) p.split *= 2;
+    {
+      // weight gradients run on the backward side stream next to the dgrad chain: a grid that
+      // fills every CU starves the critical path, so their split-K targets DTC_WGRAD_BLOCKS blocks
+      static const int target = [] { const char* v = getenv("DTC_WGRAD_BLOCKS"); return v ? atoi(v) : 512; }();
+      while (t64 * p.split < target && nk / (p.split * 2) >= 4) p.split *= 2;
+    }
   }
   return p;
 }

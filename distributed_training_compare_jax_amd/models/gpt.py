@@ -39,6 +39,9 @@ from ..parallel.buffers import FlatParams
 import os as _os
 
 _LMHEAD_WGRAD_MAIN = _os.environ.get("DTC_LMHEAD_WGRAD", "side") == "main"
+# side-stream schedule: 1 = the previous layer's weight gradients are forked one at a time between
+# this layer's dgrad GEMMs; 0 = one fork per layer after its dgrad chain
+_SIDE_INTERLEAVE = _os.environ.get("DTC_SIDE_INTERLEAVE", "0") == "1"  # measured: 1 is slower
 
 
 class NoComm:
@@ -91,6 +94,12 @@ class SideStream:
             return
         fns, self._pending = self._pending, []
         self.run(lambda: [f() for f in fns])
+
+    def flush_one(self):
+        """Fork just the oldest queued item (interleaves the previous layer's weight gradients with
+        this layer's dgrad chain in capture order, which is what lets hipGraph replay overlap them)."""
+        if self._pending:
+            self.run(self._pending.pop(0))
 
     def join(self):
         self.flush()
@@ -210,19 +219,23 @@ class GPTStage:
             side.defer(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), G.colsum(dx3, f.g(p + "fc2.b"), beta)),
                      dx3_c, gact, dx3)
         du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
+        side.flush_one()
         side.defer(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta), G.colsum(du, f.g(p + "fc1.b"), beta)), du, y2)
         dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
+        side.flush_one()
         tp.all_reduce_(dy2)
         # LN2 backward also emits out_proj.b's gradient (Σ_rows dx2)
         dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
         # attention
         side.defer(lambda: G.wgrad(dx2_c, o, f.g(p + "out.w"), beta), dx2_c, o)
         do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
+        side.flush_one()
         dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                           self.heads_local).view(batch * T, -1)
         side.defer(lambda: (G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta), G.colsum(dqkv, f.g(p + "qkv.b"), beta)),
                  dqkv, y1)
         dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
+        side.flush_one()
         tp.all_reduce_(dy1)
         return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
 
@@ -295,7 +308,8 @@ class GPTStage:
             dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta)
             if hook is not None:
                 hook(l)
-            self.side.flush()  # one fork per layer: its wgrads (+ anything the hook queued)
+            if not _SIDE_INTERLEAVE:
+                self.side.flush()  # one fork per layer: its wgrads (+ anything the hook queued)
         return dx, dx_c
 
 
