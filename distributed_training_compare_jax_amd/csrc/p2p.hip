@@ -91,9 +91,60 @@ __global__ void p2p_all_gather_kernel(PeerTable t, int world, long n4, long half
   }
 }
 
+// ---------------------------------------------------------------- intra-device stream flags
+// Cross-stream dependencies between two separately captured hipGraphs (main / side) on the SAME
+// device: a producer stream bumps flags[k] to its replay epoch (agent-scope release, after all of
+// its prior kernels completed in queue order); the consumer spins until flags[k] >= its own
+// epoch (agent-scope acquire).  Each graph bumps its epoch once per replay, so the two stay in
+// lock step without host involvement.  Spins are bounded (~10 s -> error word, then proceed).
+__global__ void epoch_inc_kernel(uint32_t* __restrict__ epoch) {
+  if (threadIdx.x == 0) epoch[0] += 1;
+}
+
+__global__ void flag_set_kernel(uint32_t* __restrict__ flags, int k, const uint32_t* __restrict__ epoch) {
+  if (threadIdx.x == 0) {
+    __threadfence();
+    __hip_atomic_store(flags + k, epoch[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void flag_wait_kernel(const uint32_t* __restrict__ flags, int k, const uint32_t* __restrict__ epoch,
+                                 int* __restrict__ err) {
+  if (threadIdx.x == 0) {
+    const uint32_t e = epoch[0];
+    const uint64_t t0 = wall_clock();
+    while (__hip_atomic_load(flags + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock() - t0 > 1000000000ull) {
+        atomicExch(err, 2000 + k);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 }  // namespace
 
 extern "C" {
+
+int dtc_epoch_inc(uint32_t* epoch, hipStream_t st) {
+  hipLaunchKernelGGL(epoch_inc_kernel, dim3(1), dim3(64), 0, st, epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_flag_set(uint32_t* flags, int k, const uint32_t* epoch, hipStream_t st) {
+  hipLaunchKernelGGL(flag_set_kernel, dim3(1), dim3(64), 0, st, flags, k, epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_flag_wait(const uint32_t* flags, int k, const uint32_t* epoch, int* err, hipStream_t st) {
+  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, st, flags, k, epoch, err);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
 
 long dtc_p2p_flag_bytes() { return FLAG_BYTES; }
 

@@ -75,6 +75,9 @@ def _declare(lib):
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, vp], i),
         "dtc_colsum_workspace_bytes": ([i, i], l),
         "dtc_embed_fwd": ([vp, vp, vp, vp, i, i, i, i, f, l, vp, l, vp], i),
+        "dtc_epoch_inc": ([vp, vp], i),
+        "dtc_flag_set": ([vp, i, vp, vp], i),
+        "dtc_flag_wait": ([vp, i, vp, vp, vp], i),
         "dtc_p2p_flag_bytes": ([], l),
         "dtc_p2p_alloc": ([l, vp, vp], i),
         "dtc_p2p_open": ([vp, vp], i),
