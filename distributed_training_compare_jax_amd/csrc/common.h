@@ -36,6 +36,31 @@ struct GemmArgs {
   float* label_out;
   void* workspace; long ws_bytes;
   int split_k;
+  int defer_reduce;  // layout 2 with split-K > 1: leave the fp32 slabs in `workspace` (the caller's
+                     // batched reducer sums them later) instead of launching splitk_reduce
+};
+
+// Batched deferred reductions (csrc/norm_reduce.hip reduce_tasks_kernel): one launch finishes
+// every split-K slab / partial-slab reduction and grad-norm partial a backward layer queued.
+enum { RED_WIDE = 0, RED_TALL = 1, RED_SUMSQ = 2 };
+struct RedTask {
+  const float* src;  // WIDE/TALL: partial p, column c at src[p*pstride + c]; SUMSQ: data
+  float* dst;        // WIDE/TALL: dst[c] = beta*dst[c] + sum_p (p ascending)
+  float* part;       // SUMSQ: part[block] = weight * sum x^2 over the block's share
+  long C;            // columns (SUMSQ: elements)
+  long pstride;
+  int P;
+  int mode;
+  int blk0;          // first block of this task in the launch (tasks sorted by blk0)
+  int nblk;
+  float beta;
+  float weight;
+};
+constexpr int RED_MAX_TASKS = 24;
+struct RedBatch {
+  int ntasks;
+  int nblocks;
+  RedTask t[RED_MAX_TASKS];
 };
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_LMHEAD = 4, EPI_NONE = 99 /* microbench: no store */ };

@@ -873,7 +873,7 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   else
     return 1007;
   DTC_CHECK_LAUNCH();
-  if (p.split > 1) {
+  if (p.split > 1 && !a.defer_reduce) {
     long MN = (long)a.M * a.N;
     int blocks = (int)((MN / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, p.split, MN,
@@ -930,7 +930,7 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
                      (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
                      (float*)a.workspace, e);
   DTC_CHECK_LAUNCH();
-  if (split > 1) {
+  if (split > 1 && !a.defer_reduce) {
     long MN = (long)a.M * a.N;
     int blocks = (int)((MN / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, split, MN,
@@ -945,6 +945,12 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
 extern "C" {
 
 int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }
+
+// split-K factor dtc_gemm will use for a weight-gradient (layout 2) problem (1 = none)
+int dtc_gemm_wgrad_split(int M, int N, int K) {
+  if (big_split(2, M, N, K)) return 1;
+  return make_plan(M, N, K, 1).split;
+}
 
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   Plan p = make_plan(M, N, K, layout == 2 ? 1 : (layout == 1 ? 2 : 0));

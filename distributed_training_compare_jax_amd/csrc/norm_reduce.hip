@@ -209,6 +209,75 @@ __global__ void __launch_bounds__(256) colsum_stage1(const void* __restrict__ dy
   }
 }
 
+// One launch for a whole backward layer's deferred reductions (split-K weight-gradient slabs,
+// LayerNorm dgamma/dbeta partials, bias column partials) and grad-norm partials.  Each per-op
+// reduce kernel it replaces is tiny, so its cost was the ~5 us per-launch floor of a replayed
+// graph node, paid ~9 times per layer.  Every output element is summed by one thread in a fixed
+// partial order (p ascending), so results are bitwise reproducible and equal the per-op path.
+//  WIDE  (few partials, many columns; split-K slabs): 1024 columns per block, f32x4 per thread.
+//  TALL  (many partials, few columns; LN / colsum partials): 16 columns x 16 partial groups per
+//        block, fixed-order LDS combine (the slab_reduce scheme).
+//  SUMSQ (grad-norm chunk): part[b] = weight * sum x^2 over a grid-stride share of the range.
+__global__ void __launch_bounds__(256) reduce_tasks_kernel(RedBatch batch) {
+  int t = 0;
+  while (t + 1 < batch.ntasks && (int)blockIdx.x >= batch.t[t + 1].blk0) ++t;
+  const RedTask& T = batch.t[t];
+  const int b = blockIdx.x - T.blk0;
+  const int tid = threadIdx.x;
+  if (T.mode == RED_WIDE) {
+    const long c = ((long)b * 256 + tid) * 4;
+    if (c >= T.C) return;
+    if (c + 4 <= T.C) {
+      f32x4 s = *(const f32x4*)(T.src + c);
+      for (int p = 1; p < T.P; ++p) s += *(const f32x4*)(T.src + (long)p * T.pstride + c);
+      f32x4* o = (f32x4*)(T.dst + c);
+      if (T.beta != 0.f) s += T.beta * *o;
+      *o = s;
+    } else {
+      for (long cc = c; cc < T.C; ++cc) {
+        float s = T.src[cc];
+        for (int p = 1; p < T.P; ++p) s += T.src[(long)p * T.pstride + cc];
+        T.dst[cc] = T.beta != 0.f ? T.beta * T.dst[cc] + s : s;
+      }
+    }
+  } else if (T.mode == RED_TALL) {
+    const int tx = tid % SR_COLS, ty = tid / SR_COLS;
+    const long c = (long)b * SR_COLS + tx;
+    float s = 0.f;
+    if (c < T.C) {
+#pragma unroll 4
+      for (int p = ty; p < T.P; p += SR_GROUPS) s += T.src[(long)p * T.pstride + c];
+    }
+    __shared__ float red[SR_GROUPS][SR_COLS];
+    red[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && c < T.C) {
+      float u = 0.f;
+#pragma unroll
+      for (int gq = 0; gq < SR_GROUPS; ++gq) u += red[gq][tx];
+      T.dst[c] = T.beta != 0.f ? T.beta * T.dst[c] + u : u;
+    }
+  } else {
+    float acc = 0.f;
+    const long n4 = T.C / 4, stride = (long)T.nblk * 256;
+    const f32x4* x4 = (const f32x4*)T.src;
+    long i = (long)b * 256 + tid;
+    for (; i + 3 * stride < n4; i += 4 * stride) {  // 4 independent 16-B loads in flight
+      f32x4 v0 = x4[i], v1 = x4[i + stride], v2 = x4[i + 2 * stride], v3 = x4[i + 3 * stride];
+      f32x4 q = v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+      acc += (q[0] + q[1]) + (q[2] + q[3]);
+    }
+    for (; i < n4; i += stride) { f32x4 v = x4[i] * x4[i]; acc += (v[0] + v[1]) + (v[2] + v[3]); }
+    if (b == 0)
+      for (long i = n4 * 4 + tid; i < T.C; i += 256) acc += T.src[i] * T.src[i];
+    acc = warp_sum(acc);
+    __shared__ float wred[4];
+    if ((tid & 63) == 0) wred[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) T.part[b] = T.weight * ((wred[0] + wred[1]) + (wred[2] + wred[3]));
+  }
+}
+
 }  // namespace
 
 #define DTC_NV_SWITCH(NV_, ...)                                              \
@@ -241,7 +310,7 @@ long dtc_layernorm_bwd_workspace_bytes(int M, int D) {
 
 int dtc_layernorm_bwd(const void* dy, int dy_f32, const float* x, const float* g, const float* mean, const float* rstd,
                       const float* dres, float* dx, bf16* dx_c, float* dg, float* db, float* dbias, int M, int D,
-                      int accumulate, float* ws, long ws_bytes, hipStream_t st) {
+                      int accumulate, float* ws, long ws_bytes, int defer, hipStream_t st) {
   if (D % 4 || D > 1024) return 2002;  // dgamma/dbeta block reduce holds D <= 1024 in LDS
   int blocks = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
   if (ws_bytes < dtc_layernorm_bwd_workspace_bytes(M, D)) return 2003;
@@ -250,6 +319,7 @@ int dtc_layernorm_bwd(const void* dy, int dy_f32, const float* x, const float* g
   DTC_NV_SWITCH(nv, hipLaunchKernelGGL(ln_bwd_kernel<NVC>, dim3(blocks), dim3(256), 0, st, dy, dy_f32, x, g, mean, rstd,
                                        dres, dx, dx_c, ws, nslab, M, D));
   DTC_CHECK_LAUNCH();
+  if (defer) return 0;  // partials stay in ws: [blocks][nslab][D] (a RED_TALL task per slab)
   hipLaunchKernelGGL(slab_reduce, dim3((nslab * D + SR_COLS - 1) / SR_COLS), dim3(256), 0, st, ws, blocks, nslab * D, dg, db, dbias,
                      D, accumulate ? 1.f : 0.f);
   DTC_CHECK_LAUNCH();
@@ -259,14 +329,26 @@ int dtc_layernorm_bwd(const void* dy, int dy_f32, const float* x, const float* g
 long dtc_colsum_workspace_bytes(int M, int N) { return (long)((M + CS_ROWS - 1) / CS_ROWS) * N * 4; }
 
 int dtc_colsum(const void* dy, int is_f32, int M, int N, long ld, float* out, float beta, float* ws, long ws_bytes,
-               hipStream_t st) {
+               int defer, hipStream_t st) {
   int P = (M + CS_ROWS - 1) / CS_ROWS;
   if (ws_bytes < dtc_colsum_workspace_bytes(M, N)) return 2004;
   if (ld % 4) return 2005;
   dim3 g1((N + 255) / 256, P);
   hipLaunchKernelGGL(colsum_stage1, g1, dim3(256), 0, st, dy, is_f32, M, N, ld, ws);
   DTC_CHECK_LAUNCH();
+  if (defer) return 0;  // partials stay in ws: [P][N]
   hipLaunchKernelGGL(slab_reduce, dim3((N + SR_COLS - 1) / SR_COLS), dim3(256), 0, st, ws, P, N, out, out, out, N, beta);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_red_max_tasks() { return RED_MAX_TASKS; }
+int dtc_red_task_bytes() { return (int)sizeof(RedTask); }
+
+int dtc_reduce_tasks(const RedBatch* b, hipStream_t st) {
+  if (b->ntasks <= 0) return 0;
+  if (b->ntasks > RED_MAX_TASKS) return 2010;
+  hipLaunchKernelGGL(reduce_tasks_kernel, dim3(b->nblocks), dim3(256), 0, st, *b);
   DTC_CHECK_LAUNCH();
   return 0;
 }

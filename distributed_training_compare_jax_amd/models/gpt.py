@@ -31,6 +31,7 @@ from ..ops import embedding as E
 from ..ops import gemm as G
 from ..ops import layernorm as LN
 from ..ops import xent as X
+from ..ops.reduce import GradReducer
 from ..parallel.buffers import FlatParams
 
 
@@ -122,6 +123,11 @@ class GPTStage:
                  dropout_seed: int = 0, act_dtype: torch.dtype = torch.bfloat16, side_stream: bool = True):
         self.cfg = cfg
         self.side = SideStream(flat.device, side_stream)
+        # single-stream GPU backward: every off-critical-path reduction of a layer (split-K weight
+        # gradient slabs, LN dgamma/dbeta partials, bias column partials, grad-norm chunks) goes
+        # into ONE batched launch per layer (ops/reduce.py); with the side stream, per-op kernels
+        dev = torch.device(flat.device)
+        self.red = GradReducer(dev) if (dev.type == "cuda" and self.side.stream is None) else None
         self._bias_fused = set()  # layers whose fc2.b grad an upstream LN backward already produced
         # deferred optimizer (train/engine.py): params of layer l / "head" become valid when this
         # side-stream event fires; the forward waits on it right before first use
@@ -207,32 +213,32 @@ class GPTStage:
         tp = self.tp
         x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch = ctx.pop(l)
         T = x.shape[0] // batch
-        side = self.side
+        side, red = self.side, self.red
         # fc2.b's gradient = Σ_rows dx3 was already emitted by the LayerNorm backward that produced
         # dx3 (lnf or the next block's ln1) unless dx3 arrived from another pipeline stage
         fc2b_fused = l in self._bias_fused
         self._bias_fused.discard(l)
         # MLP (dgrad chain on the main stream, weight grads on the side stream)
         if fc2b_fused:
-            side.defer(lambda: G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), dx3_c, gact)
+            side.defer(lambda: G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta, red=red), dx3_c, gact)
         else:
-            side.defer(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta), G.colsum(dx3, f.g(p + "fc2.b"), beta)),
+            side.defer(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta, red=red), G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)),
                      dx3_c, gact, dx3)
         du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
         side.flush_one()
-        side.defer(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta), G.colsum(du, f.g(p + "fc1.b"), beta)), du, y2)
+        side.defer(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta, red=red), G.colsum(du, f.g(p + "fc1.b"), beta, red=red)), du, y2)
         dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
         side.flush_one()
         tp.all_reduce_(dy2)
         # LN2 backward also emits out_proj.b's gradient (Σ_rows dx2)
         dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
         # attention
-        side.defer(lambda: G.wgrad(dx2_c, o, f.g(p + "out.w"), beta), dx2_c, o)
+        side.defer(lambda: G.wgrad(dx2_c, o, f.g(p + "out.w"), beta, red=red), dx2_c, o)
         do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
         side.flush_one()
         dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                           self.heads_local).view(batch * T, -1)
-        side.defer(lambda: (G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta), G.colsum(dqkv, f.g(p + "qkv.b"), beta)),
+        side.defer(lambda: (G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta, red=red), G.colsum(dqkv, f.g(p + "qkv.b"), beta, red=red)),
                  dqkv, y1)
         dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
         side.flush_one()
@@ -251,7 +257,7 @@ class GPTStage:
         dx_c = None if self.act_dtype == torch.float32 else torch.empty(dy.shape, dtype=self.act_dtype,
                                                                         device=dy.device)
         dx = LN.layernorm_bwd(dy, x, f.p(ln + ".g"), mu, rs, dres, f.g(ln + ".g"), f.g(ln + ".b"), beta,
-                              out_c=dx_c, dbias=None if bias_grad is None else f.g(bias_grad))
+                              out_c=dx_c, dbias=None if bias_grad is None else f.g(bias_grad), red=self.red)
         return dx, (dx if dx_c is None else dx_c)
 
     def stage_forward(self, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
@@ -288,8 +294,9 @@ class GPTStage:
         # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
         # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
         dyf = G.matmul_nn(dlogits, f.w("lm_head.w"))
-        wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta),
-                                                G.colsum(cp, f.g("lm_head.b"), beta))
+        red = self.red
+        wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
+                                                G.colsum(cp, f.g("lm_head.b"), beta, red=red))
         if _LMHEAD_WGRAD_MAIN:
             wg()
         else:
@@ -300,12 +307,20 @@ class GPTStage:
         out = self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
                            bias_grad=None if last is None else self._prev_fc2b(last))
         self.side.flush()
+        self.flush_reductions()
         return out
+
+    def flush_reductions(self):
+        """Launch the batched reductions queued since the last flush (no-op without a reducer)."""
+        if self.red is not None:
+            self.red.flush()
 
     def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None):
         """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist."""
         for l in reversed(list(self.layout.layers)):
             dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta)
+            self.side.flush()
+            self.flush_reductions()  # layer l's grads are final after this launch
             if hook is not None:
                 hook(l)
             if not _SIDE_INTERLEAVE:

@@ -52,6 +52,7 @@ class GemmArgs(ctypes.Structure):
         ("label_out", c_vp),     # fp32 [M]
         ("workspace", c_vp), ("ws_bytes", c_long),
         ("split_k", c_int),      # 0 = auto
+        ("defer_reduce", c_int),  # wgrad split-K: leave the slabs in `workspace` (ops/reduce.py)
     ]
 
 
@@ -70,9 +71,13 @@ def _declare(lib):
         "dtc_gemm_workspace_bytes": ([i, i, i, i], l),
         "dtc_lmhead_nparts": ([i, i, i], i),
         "dtc_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
-        "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, vp], i),
+        "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, i, vp], i),
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
-        "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, vp], i),
+        "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, i, vp], i),
+        "dtc_gemm_wgrad_split": ([i, i, i], i),
+        "dtc_reduce_tasks": ([vp, vp], i),
+        "dtc_red_max_tasks": ([], i),
+        "dtc_red_task_bytes": ([], i),
         "dtc_colsum_workspace_bytes": ([i, i], l),
         "dtc_embed_fwd": ([vp, vp, vp, vp, i, i, i, i, f, l, vp, l, vp], i),
         "dtc_epoch_inc": ([vp, vp], i),

@@ -85,10 +85,13 @@ def reserve_workspace(device, nbytes: int, role: str = "main"):
 def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, *,
                  epi: int = N.EPI_STORE, bias=None, aux=None, ldaux: int = 0, aux_out=None,
                  alpha: float = 1.0, beta: float = 0.0, labels=None, vocab_start: int = 0,
-                 n_valid: int = 0, part=None, label_out=None):
+                 n_valid: int = 0, part=None, label_out=None, workspace=None, defer_reduce: int = 0):
     L = N.lib()
-    ws_need = int(L.dtc_gemm_workspace_bytes(layout, M, N_, K))
-    ws = _workspace(c.device, ws_need) if ws_need > 0 else None
+    if workspace is not None:
+        ws = workspace.view(torch.uint8) if workspace.dtype != torch.uint8 else workspace
+    else:
+        ws_need = int(L.dtc_gemm_workspace_bytes(layout, M, N_, K))
+        ws = _workspace(c.device, ws_need) if ws_need > 0 else None
     args = N.GemmArgs(
         layout=layout, M=M, N=N_, K=K,
         A=a.data_ptr(), lda=lda, B=b.data_ptr(), ldb=ldb, C=c.data_ptr(), ldc=ldc,
@@ -96,7 +99,7 @@ def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int,
         bias=N.ptr(bias), aux=N.ptr(aux), ldaux=ldaux, aux_out=N.ptr(aux_out),
         alpha=alpha, beta=beta, labels=N.ptr(labels), vocab_start=vocab_start, n_valid=n_valid,
         part=N.ptr(part), label_out=N.ptr(label_out),
-        workspace=N.ptr(ws), ws_bytes=0 if ws is None else ws.numel(), split_k=0)
+        workspace=N.ptr(ws), ws_bytes=0 if ws is None else ws.numel(), split_k=0, defer_reduce=defer_reduce)
     N.check(L.dtc_gemm(args, N.stream_ptr(c.device)), "dtc_gemm")
 
 
@@ -198,8 +201,11 @@ def matmul_nn_dgelu(dy: torch.Tensor, w: torch.Tensor, u: torch.Tensor) -> torch
     return du
 
 
-def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
-    """dW[N,K] = β·dW + dY[M,N]ᵀ·X[M,K]  (fp32 ``dw`` is a view into the flat grad buffer)."""
+def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0, red=None) -> torch.Tensor:
+    """dW[N,K] = β·dW + dY[M,N]ᵀ·X[M,K]  (fp32 ``dw`` is a view into the flat grad buffer).
+
+    ``red`` (an ``ops.reduce.GradReducer``): a split-K GEMM leaves its fp32 slabs in the reducer's
+    arena and the final sum (+β·dW) happens in the reducer's next batched launch."""
     M, Nn = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and tuple(dw.shape) == (Nn, K)
@@ -212,12 +218,21 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
         return dw
     _check2d(dy, "dy"); _check2d(x, "x")
     assert dw.dtype == torch.float32 and dw.is_contiguous()
+    if red is not None:
+        split = int(N.lib().dtc_gemm_wgrad_split(Nn, K, M))
+        if split > 1:
+            slab = red.alloc(split * Nn * K)
+            _gemm_native(2, Nn, K, M, dy, dy.stride(0), x, x.stride(0), dw, K, beta=beta, workspace=slab,
+                         defer_reduce=1)
+            red.add_wide(slab, dw, split, beta)
+            return dw
     _gemm_native(2, Nn, K, M, dy, dy.stride(0), x, x.stride(0), dw, K, beta=beta)
     return dw
 
 
-def colsum(dy: torch.Tensor, db: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
-    """db[N] = β·db + Σ_m dY[m, :]  (deterministic two-stage reduction on GPU)."""
+def colsum(dy: torch.Tensor, db: torch.Tensor, beta: float = 0.0, red=None) -> torch.Tensor:
+    """db[N] = β·db + Σ_m dY[m, :]  (deterministic two-stage reduction on GPU; with ``red`` the
+    second stage is a task of the reducer's next batched launch)."""
     M, Nn = dy.shape
     if not dy.is_cuda:
         s = _f32(dy).sum(0)
@@ -227,8 +242,12 @@ def colsum(dy: torch.Tensor, db: torch.Tensor, beta: float = 0.0) -> torch.Tenso
             db.copy_(s)
         return db
     L = N.lib()
-    ws = _workspace(dy.device, int(L.dtc_colsum_workspace_bytes(M, Nn)))
+    nbytes = int(L.dtc_colsum_workspace_bytes(M, Nn))
+    ws = _workspace(dy.device, nbytes) if red is None else red.alloc(nbytes // 4)
     is_f32 = 1 if dy.dtype == torch.float32 else 0
     N.check(L.dtc_colsum(dy.data_ptr(), is_f32, M, Nn, dy.stride(0), db.data_ptr(), beta,
-                         ws.data_ptr(), ws.numel(), N.stream_ptr(dy.device)), "dtc_colsum")
+                         ws.data_ptr(), nbytes if red is not None else ws.numel(), 1 if red is not None else 0,
+                         N.stream_ptr(dy.device)), "dtc_colsum")
+    if red is not None:
+        red.add_tall(ws.data_ptr(), Nn, nbytes // 4 // Nn, db, beta)
     return db

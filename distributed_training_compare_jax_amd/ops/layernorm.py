@@ -41,7 +41,7 @@ def layernorm_fwd(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, g: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
                   dres: Optional[torch.Tensor], dg: torch.Tensor, db: torch.Tensor, beta: float = 0.0,
                   out: Optional[torch.Tensor] = None, out_c: Optional[torch.Tensor] = None,
-                  dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  dbias: Optional[torch.Tensor] = None, red=None) -> torch.Tensor:
     """Returns fp32 ``dx = dres + dLN/dx·dy``; writes ``dg/db = β·(dg/db) + Σ_rows`` (β ∈ {0, 1}).
 
     ``out`` may alias ``dres`` (in-place residual-gradient update); ``out_c`` (optional)
@@ -81,9 +81,16 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, g: torch.Tensor, mean: torc
     if out is None:
         out = torch.empty(M, D, dtype=torch.float32, device=x.device)
     L = N.lib()
-    ws = _workspace(x.device, int(L.dtc_layernorm_bwd_workspace_bytes(M, D)))
+    nbytes = int(L.dtc_layernorm_bwd_workspace_bytes(M, D))
+    ws = _workspace(x.device, nbytes) if red is None else red.alloc(nbytes // 4)
     N.check(L.dtc_layernorm_bwd(dy.data_ptr(), 1 if dy.dtype == torch.float32 else 0, x.data_ptr(), g.data_ptr(),
                                 mean.data_ptr(), rstd.data_ptr(), N.ptr(dres), out.data_ptr(), N.ptr(out_c),
                                 dg.data_ptr(), db.data_ptr(), N.ptr(dbias), M, D, 1 if beta != 0.0 else 0,
-                                ws.data_ptr(), ws.numel(), N.stream_ptr(x.device)), "dtc_layernorm_bwd")
+                                ws.data_ptr(), nbytes if red is not None else ws.numel(), 1 if red is not None else 0,
+                                N.stream_ptr(x.device)), "dtc_layernorm_bwd")
+    if red is not None:  # partials [blocks][nslab][D]: one ordered column reduction per slab
+        nslab = 3 if dbias is not None else 2
+        blocks = nbytes // 4 // (3 * D)
+        for s, dst in enumerate((dg, db, dbias)[:nslab]):
+            red.add_tall(ws.data_ptr() + s * D * 4, nslab * D, blocks, dst, 1.0 if beta != 0.0 else 0.0)
     return out

@@ -75,7 +75,7 @@ class Engine:
         self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program, p2p=self.p2p)
         self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
                               act_dtype=self.act_dtype,
-                              side_stream=on_gpu and os.environ.get("DTC_NO_SIDE_STREAM", "0") != "1")
+                              side_stream=on_gpu and os.environ.get("DTC_SIDE_STREAM", "0") == "1")
         self.program.before_comm.append(self.stage.side.join)
         # DP embedding-grad gather (pp == 1): instead of all-reducing the dense wte/wpe grads
         # (103 MB fp32 for the reference vocab, issued last -> fully exposed), all-gather the
@@ -87,6 +87,7 @@ class Engine:
                                    local_names=("wte", "wpe") if self.embed_gather else ())
         self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,
                               pp_global_clip=(train_cfg.pp_clip == "global"))
+        self.opt.reducer = self.stage.red
         if pp == 1:
             # incremental Σg²: with dp == 1 each layer's grads are final when its backward ends
             # (norm chunk per layer, reduced on the side stream); with dp > 1 only the locally
@@ -223,7 +224,8 @@ class Engine:
         h = st.stage_forward(h, b, ctx)
         st.head_forward(h, self.labels, 1.0 / (b * T), ctx, loss_out=self.loss)
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
-        bk, opt, side = self.buckets, self.opt, st.side.defer
+        bk, opt = self.buckets, self.opt
+        side = st.red if st.red is not None else st.side.defer  # where grad-norm chunks are queued
         if dp == 1:
             opt.ready_upto(bk.head_end_offset(), side)
             hook = lambda l: opt.ready_upto(bk.layer_end_offset(l), side)

@@ -18,6 +18,7 @@ import torch.distributed as dist
 
 from ..config.schema import OptimConfig
 from ..ops import optim as O
+from ..ops.reduce import GradReducer
 from ..parallel.buffers import FlatParams
 
 
@@ -51,11 +52,12 @@ class FusedAdamW:
         self.segments = O.make_segments(self._merged, dev)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.chunks = []  # incremental-norm chunks: [segments, lo, hi, partial view]
+        self.chunks = []  # incremental-norm chunks: [segments, lo, hi, partial view, reducer tasks]
         self._done = []
+        self.reducer = None  # GradReducer of the model stage (single-stream GPU backward)
 
     # -- incremental global norm ------------------------------------------------------
-    def set_chunks(self, cuts, total_blocks: int = 1024):
+    def set_chunks(self, cuts, elems_per_block: int = 16384):
         """Split Σg² into flat ranges [0,c0), [c0,c1), ... (cuts ascending, 4-aligned, last =
         numel).  A chunk whose grads are final can be reduced early (:meth:`ready_upto` /
         :meth:`chunk_ready`, typically on the backward side stream) so only the last chunk and a
@@ -66,39 +68,59 @@ class FusedAdamW:
         for hi in cuts:
             segs = [(max(o, lo), min(o + n, hi) - max(o, lo), wt) for (o, n, wt) in self._merged
                     if o < hi and o + n > lo]
-            nb = max(8, int(round(total_blocks * (hi - lo) / f.numel)))
-            specs.append((O.make_segments(segs, f.device), lo, hi, nb))
+            # partial slots per segment (a batched-reducer task each; one block per ~16K elements so
+            # no block of the batched launch streams more than 64 KB), >= 8 per chunk in total
+            nbs = [max(1, (n + elems_per_block - 1) // elems_per_block) for (_, n, _) in segs]
+            nbs[-1] += max(0, 8 - sum(nbs))
+            specs.append((segs, lo, hi, nbs))
             lo = hi
-        self.part = torch.zeros(sum(s[3] for s in specs), dtype=torch.float32, device=f.device)
+        self.part = torch.zeros(sum(sum(s[3]) for s in specs), dtype=torch.float32, device=f.device)
         self.chunks, off = [], 0
-        for segs, lo, hi, nb in specs:
-            self.chunks.append((segs, lo, hi, self.part[off:off + nb]))
+        for segs, lo, hi, nbs in specs:
+            nb = sum(nbs)
+            part = self.part[off:off + nb]
+            tasks, o2 = [], 0
+            for (o, n, w), k in zip(segs, nbs):
+                tasks.append((o, n, w, part[o2:o2 + k]))
+                o2 += k
+            self.chunks.append((O.make_segments(segs, f.device), lo, hi, part, tasks))
             off += nb
         self._done = [False] * len(self.chunks)
 
     def chunk_ready(self, i: int, runner=None):
+        """Σg² partials of chunk i (its grads must be final).  ``runner``: a ``GradReducer``
+        (queued into its next batched launch), a callable taking a thunk, or None (run now)."""
         if self._done[i]:
             return
-        segs, _, _, part = self.chunks[i]
+        segs, _, _, part, tasks = self.chunks[i]
         g = self.flat.grads
-        fn = lambda: O.sumsq_partial(g, segs, part)
-        runner(fn) if runner is not None else fn()
+        if isinstance(runner, GradReducer):
+            for o, n, w, pt in tasks:
+                runner.add_sumsq(g[o:o + n], w, pt)
+        else:
+            fn = lambda: O.sumsq_partial(g, segs, part)
+            runner(fn) if runner is not None else fn()
         self._done[i] = True
 
     def ready_upto(self, offset: int, runner=None):
-        for i, (_, _, hi, _) in enumerate(self.chunks):
-            if hi <= offset:
+        for i, ch in enumerate(self.chunks):
+            if ch[2] <= offset:
                 self.chunk_ready(i, runner)
 
     def norm(self):
         """Global Σg² (all chunks, fixed order) + step counter bump (+ TP/PP all-reduce)."""
         f = self.flat
+        red = self.reducer
         if self.chunks:
             for i in range(len(self.chunks)):
-                self.chunk_ready(i)
+                self.chunk_ready(i, red)
+            if red is not None:
+                red.flush_all()  # every remaining chunk in one launch
             O.sum_finish(self.part, self.sumsq, step=self.step_t)
             self._done = [False] * len(self.chunks)
         else:
+            if red is not None:
+                red.flush_all()  # grads must be final
             O.sumsq_segments(f.grads, self.segments, self.sumsq, step=self.step_t)
         if self.tp_size > 1:
             g = self.tp_group
