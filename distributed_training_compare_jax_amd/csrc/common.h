@@ -38,6 +38,8 @@ struct GemmArgs {
   int split_k;
   int defer_reduce;  // layout 2 with split-K > 1: leave the fp32 slabs in `workspace` (the caller's
                      // batched reducer sums them later) instead of launching splitk_reduce
+  float* colsum;     // layout 2 (register-staged kernel): colsum[z*M + m] = sum over split z's k-range
+                     // of A(k, m) — the bias gradient of the same dY, fused into its weight gradient
 };
 
 // Batched deferred reductions (csrc/norm_reduce.hip reduce_tasks_kernel): one launch finishes

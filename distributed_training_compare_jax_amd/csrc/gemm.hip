@@ -99,6 +99,36 @@ struct Tile {
   }
 };
 
+// Column sums of an MN-major operand tile held in registers (Tile::load layout): chunk
+// c = tid + i*NT covers row c / (R/8) and the 8 columns 8*(c % (R/8)).., the same 8 columns for
+// every i, so a thread accumulates 8 running sums (fused bias gradient of a wgrad GEMM).
+template <int R, int PT>
+__device__ __forceinline__ void colsum_acc(float (&cs)[8], const u32x4 (&reg)[PT]) {
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+    const bf16x8 v = __builtin_bit_cast(bf16x8, reg[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[j] += (float)v[j];
+  }
+}
+
+// Fixed-order block combine of colsum_acc sums -> out[0..R) (rows >= mlim skipped).  `red` is
+// scratch LDS of (NT/(R/8)) * R floats; must be called by all threads after the main loop.
+template <int R>
+__device__ __forceinline__ void colsum_store(const float (&cs)[8], float* red, float* out, int mlim, int tid) {
+  constexpr int CPR = R / 8, G = 256 / CPR;
+  const int grp = tid / CPR, col = (tid % CPR) * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[grp * R + col + j] = cs[j];
+  __syncthreads();
+  if (tid < R && tid < mlim) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) s += red[g * R + tid];
+    out[tid] = s;
+  }
+}
+
 struct Epi {
   int M, N;
   void* C; long ldc;
@@ -109,6 +139,7 @@ struct Epi {
   const int* labels; int vocab_start, n_valid;
   float* part; int nparts;
   float* label_out;
+  float* colsum;
 };
 
 template <int EPI, bool OUTF32>
@@ -310,6 +341,9 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
   };
   bf16* const s0 = smem;
   bf16* const s1 = smem + BUF;
+  // fused bias gradient (wgrad only: MN-major A = dY, first N-tile column of blocks)
+  const bool do_cs = !AK && e.colsum != nullptr && tn_idx == 0;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (BM * BN <= 64 * 64) {
     // small tiles (few MFMAs per k-step): 2-deep register prefetch.  While the MFMAs consume LDS
     // stage kt, tile kt+1's loads are a full k-step old and tile kt+2's are being issued (two
@@ -323,6 +357,7 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
     }
     TA::store(ra0, s0, tid);
     TB::store(rb0, s0 + TA::ELEMS, tid);
+    if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra0);
     __syncthreads();
     for (int kt = 0; kt < nk; kt += 2) {
       if (kt + 2 < nk) {
@@ -333,6 +368,7 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
       if (kt + 1 < nk) {
         TA::store(ra1, s1, tid);
         TB::store(rb1, s1 + TA::ELEMS, tid);
+        if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra1);
       }
       __syncthreads();
       if (kt + 1 >= nk) break;
@@ -344,6 +380,7 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
       if (kt + 2 < nk) {
         TA::store(ra0, s0, tid);
         TB::store(rb0, s0 + TA::ELEMS, tid);
+        if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra0);
       }
       __syncthreads();
     }
@@ -355,6 +392,7 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
     TB::load(rb, rsB, ldb, n0, kbeg, tid);
     TA::store(ra, s0, tid);
     TB::store(rb, s0 + TA::ELEMS, tid);
+    if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 1 < nk;
@@ -368,9 +406,15 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
       if (more) {
         TA::store(ra, nxt, tid);
         TB::store(rb, nxt + TA::ELEMS, tid);
+        if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra);
       }
       __syncthreads();
     }
+  }
+  if constexpr (!AK) {
+    // do_cs is block-uniform, so the combine's barrier is reached by every thread of the block;
+    // LDS is free after the main loop's final barrier
+    if (do_cs) colsum_store<BM>(cs, (float*)smem, e.colsum + (long)z * M + m0, M - m0, tid);
   }
 
   // ---------------- epilogue: lane holds C[m = .. + (lane&15)][n = .. + 4*(lane>>4) + r]
@@ -787,6 +831,13 @@ struct Plan {
   int bm, bn, bk, split;
 };
 
+// DTC_GEMM_DMA bit mask: 1 = 64x64 forward layout (default: measured fc2/out_proj fwd 22 -> 18.6
+// us), 2 = 64x64 dgrad/wgrad layouts (measured slower: off), 4 = 128x128 (measured no gain: off)
+inline int gemm_dma_mask() {
+  static const int m = [] { const char* v = getenv("DTC_GEMM_DMA"); return v ? atoi(v) : 1; }();
+  return m;
+}
+
 // allow_split: 1 = small-grid split (wgrad), 2 = huge-K only (dgrad through the lm_head)
 Plan make_plan(int M, int N, int K, int allow_split) {
   Plan p{128, 128, 64, 1};
@@ -833,6 +884,7 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
+  e.colsum = a.colsum;
   int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   e.nparts = tiles_n * 2;
   const int nk = a.K / p.bk;
@@ -843,10 +895,8 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
   dim3 grid(ntiles * p.split);
   const int ab = operand_bytes(AK, a.M, a.K, a.lda), bb = operand_bytes(BKM, a.N, a.K, a.ldb);
-  // DMA-pipelined variant, DTC_GEMM_DMA bit mask: 1 = 64x64 forward layout (default: measured
-  // fc2/out_proj fwd 22 -> 18.6 us), 2 = 64x64 dgrad/wgrad layouts (measured slower: off),
-  // 4 = 128x128 (stages from DTC_DMA_STAGES128, 2 or 3; measured no gain: off)
-  static const int dma_mask = [] { const char* v = getenv("DTC_GEMM_DMA"); return v ? atoi(v) : 1; }();
+  // DMA-pipelined variant when gemm_dma_mask() allows (128x128 stages from DTC_DMA_STAGES128)
+  const int dma_mask = gemm_dma_mask();
   static const int st128 = [] { const char* v = getenv("DTC_DMA_STAGES128"); return v ? atoi(v) : 2; }();
   const int dma_bit = BM == 64 ? ((AK && BKM) ? 1 : 2) : 4;
   if (p.bk == 64 && (dma_mask & dma_bit)) {
@@ -919,6 +969,7 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
+  e.colsum = nullptr;
   const int tiles_m = (a.M + BIG - 1) / BIG, tiles_n = (a.N + BIG - 1) / BIG;
   e.nparts = tiles_n * 4;
   const int ntiles = tiles_m * tiles_n;
@@ -950,6 +1001,15 @@ int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N 
 int dtc_gemm_wgrad_split(int M, int N, int K) {
   if (big_split(2, M, N, K)) return 1;
   return make_plan(M, N, K, 1).split;
+}
+
+// 1 if the weight-gradient GEMM runs on the register-staged kernel, which can fuse the bias
+// gradient (GemmArgs.colsum); the 256^2 and DMA kernels cannot
+int dtc_gemm_wgrad_fuses_colsum(int M, int N, int K) {
+  if (big_split(2, M, N, K)) return 0;
+  const Plan p = make_plan(M, N, K, 1);
+  if (p.bk != 64) return 1;
+  return (gemm_dma_mask() & (p.bm == 64 ? 2 : 4)) ? 0 : 1;
 }
 
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
@@ -1006,6 +1066,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->layout == 2) {
     if (a->M % 8 || a->N % 8) return 1004;
     if (epi != EPI_STORE || !f32 || a->bias) return 1003;
+    if (a->colsum && !dtc_gemm_wgrad_fuses_colsum(a->M, a->N, a->K)) return 1009;
     if (big_split(2, a->M, a->N, a->K)) return launch_big<false, false, EPI_STORE, true>(*a, 1, st);
     Plan p = make_plan(a->M, a->N, a->K, 1);
     if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;

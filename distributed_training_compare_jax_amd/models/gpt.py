@@ -226,7 +226,7 @@ class GPTStage:
                      dx3_c, gact, dx3)
         du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
         side.flush_one()
-        side.defer(lambda: (G.wgrad(du, y2, f.g(p + "fc1.w"), beta, red=red), G.colsum(du, f.g(p + "fc1.b"), beta, red=red)), du, y2)
+        side.defer(lambda: G.wgrad(du, y2, f.g(p + "fc1.w"), beta, red=red, db=f.g(p + "fc1.b")), du, y2)
         dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
         side.flush_one()
         tp.all_reduce_(dy2)
@@ -238,7 +238,7 @@ class GPTStage:
         side.flush_one()
         dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                           self.heads_local).view(batch * T, -1)
-        side.defer(lambda: (G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta, red=red), G.colsum(dqkv, f.g(p + "qkv.b"), beta, red=red)),
+        side.defer(lambda: G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta, red=red, db=f.g(p + "qkv.b")),
                  dqkv, y1)
         dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
         side.flush_one()

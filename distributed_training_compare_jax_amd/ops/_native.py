@@ -53,6 +53,7 @@ class GemmArgs(ctypes.Structure):
         ("workspace", c_vp), ("ws_bytes", c_long),
         ("split_k", c_int),      # 0 = auto
         ("defer_reduce", c_int),  # wgrad split-K: leave the slabs in `workspace` (ops/reduce.py)
+        ("colsum", c_vp),        # wgrad: fp32 [split][M] bias-gradient partials (fused colsum)
     ]
 
 
@@ -75,6 +76,7 @@ def _declare(lib):
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, i, vp], i),
         "dtc_gemm_wgrad_split": ([i, i, i], i),
+        "dtc_gemm_wgrad_fuses_colsum": ([i, i, i], i),
         "dtc_reduce_tasks": ([vp, vp], i),
         "dtc_red_max_tasks": ([], i),
         "dtc_red_task_bytes": ([], i),

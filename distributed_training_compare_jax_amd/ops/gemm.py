@@ -85,7 +85,8 @@ def reserve_workspace(device, nbytes: int, role: str = "main"):
 def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, *,
                  epi: int = N.EPI_STORE, bias=None, aux=None, ldaux: int = 0, aux_out=None,
                  alpha: float = 1.0, beta: float = 0.0, labels=None, vocab_start: int = 0,
-                 n_valid: int = 0, part=None, label_out=None, workspace=None, defer_reduce: int = 0):
+                 n_valid: int = 0, part=None, label_out=None, workspace=None, defer_reduce: int = 0,
+                 colsum=None):
     L = N.lib()
     if workspace is not None:
         ws = workspace.view(torch.uint8) if workspace.dtype != torch.uint8 else workspace
@@ -99,7 +100,8 @@ def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int,
         bias=N.ptr(bias), aux=N.ptr(aux), ldaux=ldaux, aux_out=N.ptr(aux_out),
         alpha=alpha, beta=beta, labels=N.ptr(labels), vocab_start=vocab_start, n_valid=n_valid,
         part=N.ptr(part), label_out=N.ptr(label_out),
-        workspace=N.ptr(ws), ws_bytes=0 if ws is None else ws.numel(), split_k=0, defer_reduce=defer_reduce)
+        workspace=N.ptr(ws), ws_bytes=0 if ws is None else ws.numel(), split_k=0, defer_reduce=defer_reduce,
+        colsum=N.ptr(colsum))
     N.check(L.dtc_gemm(args, N.stream_ptr(c.device)), "dtc_gemm")
 
 
@@ -201,11 +203,14 @@ def matmul_nn_dgelu(dy: torch.Tensor, w: torch.Tensor, u: torch.Tensor) -> torch
     return du
 
 
-def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0, red=None) -> torch.Tensor:
-    """dW[N,K] = β·dW + dY[M,N]ᵀ·X[M,K]  (fp32 ``dw`` is a view into the flat grad buffer).
+def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0, red=None,
+          db: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dW[N,K] = β·dW + dY[M,N]ᵀ·X[M,K]  (fp32 ``dw`` is a view into the flat grad buffer);
+    with ``db``: also db[N] = β·db + Σ_m dY[m, :] (the layer's bias gradient).
 
     ``red`` (an ``ops.reduce.GradReducer``): a split-K GEMM leaves its fp32 slabs in the reducer's
-    arena and the final sum (+β·dW) happens in the reducer's next batched launch."""
+    arena and the final sum (+β·dW) happens in the reducer's next batched launch; the bias
+    gradient is then summed inside the GEMM (column sums of the dY tiles it already loads)."""
     M, Nn = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and tuple(dw.shape) == (Nn, K)
@@ -215,18 +220,32 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
             dw.mul_(beta).add_(g)
         else:
             dw.copy_(g)
+        if db is not None:
+            colsum(dy, db, beta)
         return dw
     _check2d(dy, "dy"); _check2d(x, "x")
     assert dw.dtype == torch.float32 and dw.is_contiguous()
     if red is not None:
-        split = int(N.lib().dtc_gemm_wgrad_split(Nn, K, M))
+        L = N.lib()
+        split = int(L.dtc_gemm_wgrad_split(Nn, K, M))
+        cs = None
+        if db is not None and L.dtc_gemm_wgrad_fuses_colsum(Nn, K, M):
+            cs = red.alloc(split * Nn)
+        elif db is not None:
+            colsum(dy, db, beta, red=red)
         if split > 1:
             slab = red.alloc(split * Nn * K)
             _gemm_native(2, Nn, K, M, dy, dy.stride(0), x, x.stride(0), dw, K, beta=beta, workspace=slab,
-                         defer_reduce=1)
+                         defer_reduce=1, colsum=cs)
             red.add_wide(slab, dw, split, beta)
-            return dw
+        else:
+            _gemm_native(2, Nn, K, M, dy, dy.stride(0), x, x.stride(0), dw, K, beta=beta, colsum=cs)
+        if cs is not None:
+            red.add_wide(cs, db, split, beta)
+        return dw
     _gemm_native(2, Nn, K, M, dy, dy.stride(0), x, x.stride(0), dw, K, beta=beta)
+    if db is not None:
+        colsum(dy, db, beta)
     return dw
 
 

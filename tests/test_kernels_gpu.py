@@ -283,3 +283,20 @@ def test_batched_reducer_matches_per_op(cuda):
     red.flush_all()
     ref = 0.5 * (data.double() ** 2).sum()
     assert abs(part.double().sum().item() - ref.item()) <= 1e-5 * ref.item()
+
+
+@pytest.mark.parametrize("Mtok,N,K", [(4096, 2048, 512), (4096, 1536, 512), (4096, 512, 512), (256, 200, 96)])
+def test_wgrad_fused_bias_grad(cuda, Mtok, N, K):
+    """wgrad(..., db=) sums the bias gradient inside the GEMM (register-staged path) — equals the
+    standalone colsum to fp32 reassociation, dW unchanged."""
+    from distributed_training_compare_jax_amd.ops.reduce import GradReducer
+
+    red = GradReducer(cuda, arena_mb=64)
+    dy, x = _r(Mtok, N, seed=31), _r(Mtok, K, seed=32)
+    for beta in (0.0, 1.0):
+        dw, db = _r(N, K, dtype=torch.float32, seed=33), _r(N, dtype=torch.float32, seed=34)
+        dw0, db0 = dw.clone(), db.clone()
+        G.wgrad(dy, x, dw, beta=beta, red=red, db=db)
+        red.flush()
+        _close(dw, beta * dw0 + dy.float().t() @ x.float(), 2e-3, "dW")
+        _close(db, beta * db0 + dy.float().sum(0), 1e-5, "db")
