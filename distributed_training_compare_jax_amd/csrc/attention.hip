@@ -15,6 +15,7 @@
 // one workgroup per 64-key block sweeping the queries; dQ with one workgroup per 64-query
 // block sweeping the keys.  P is recomputed from the saved LSE.
 #include "common.h"
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -515,29 +516,63 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
   }
 }
 
+// delta = rowsum(dO * O) of one 8-wide chunk pair, combined over the 4 chunks of a 32-wide head
+// row in the order (c0 + c2) + (c1 + c3) — the dQ (group_sum) and dK/dV (xor shuffles) paths
+// produce bitwise identical values
+__device__ __forceinline__ float dot8(bf16x8 a, bf16x8 c) {
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) s += (float)a[r] * (float)c[r];
+  return s;
+}
+
+// dO panel -> LDS [Tp][LD] like stage_rows (HD = 32: 4 chunks per row, 4 adjacent threads per
+// row), plus delta[r] = rowsum(dO*O) -> sDel[r] (0 for padding rows)
+template <int LD, int MAXT>
+__device__ __forceinline__ void stage_dout_delta(bf16* lds, float* sDel, const bf16* __restrict__ dOb,
+                                                 const bf16* __restrict__ Ob, long tok_stride, int T, int Tp, int tid) {
+  constexpr int HD = 32, CPR = HD / 8, PER = (MAXT * CPR + RES_THREADS - 1) / RES_THREADS;
+  static_assert(RES_THREADS % CPR == 0, "a row's chunks must sit in adjacent lanes");
+  u32x4 v[PER], ov[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = tid + i * RES_THREADS, r = c / CPR, col = (c % CPR) * 8;
+    v[i] = r < T ? *(const u32x4*)(dOb + (long)r * tok_stride + col) : u32x4{0, 0, 0, 0};
+    ov[i] = r < T ? *(const u32x4*)(Ob + (long)r * tok_stride + col) : u32x4{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = tid + i * RES_THREADS, r = c / CPR, col = (c % CPR) * 8;
+    if (r < Tp) *(u32x4*)(lds + r * LD + col) = v[i];
+    float d = dot8(__builtin_bit_cast(bf16x8, v[i]), __builtin_bit_cast(bf16x8, ov[i]));
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 1, 64);
+    if ((c % CPR) == 0 && r < Tp) sDel[r] = d;
+  }
+}
+
 // dK, dV with Q and dO resident: wave owns 16 keys (key on the lane), walks queries >= its keys
 template <int HD>
-__global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+__device__ __forceinline__ void attn_bwd_dkdv_res_body(
+    bf16* lds, int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
-  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
-  const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
+  const int half = bid & 1, bh = bid >> 1, b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64 + 64;  // + one tile of slack: query tiles start at 16-row offsets
   bf16* sQ = lds;
   bf16* sD = lds + Tp * L::VLD;
+  float* sDel = (float*)(sD + Tp * L::VLD);
   const long ts = 3L * H * HD, dts = (long)H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
   const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
   const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
   const bf16* dOb = dout + (long)b * T * dts + h * HD;
   const float* lseb = lse + ((long)b * H + h) * T;
-  const float* delb = delta + ((long)b * H + h) * T;
   stage_rows<L::VLD, HD, RES_MAXT + 64>(sQ, Qb, ts, T, Tp, tid);
-  stage_rows<L::VLD, HD, RES_MAXT + 64>(sD, dOb, dts, T, Tp, tid);
+  stage_dout_delta<L::VLD, RES_MAXT + 64>(sD, sDel, dOb, o + (long)b * T * dts + h * HD, dts, T, Tp, tid);
   __syncthreads();
   const int kg = 2 * w + half;
   if (kg * 16 >= T) return;
@@ -568,7 +603,7 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
       const int qr = q0 + qt * 16 + 4 * g;
       // T % 4 == 0 (use_resident): a 4-row group is entirely in or out of range -> selects, no branch
       const int qc = min(qr, T - 4);
-      f32x4 l4 = *(const f32x4*)(lseb + qc), d4 = *(const f32x4*)(delb + qc);
+      f32x4 l4 = *(const f32x4*)(lseb + qc), d4 = *(const f32x4*)(sDel + qc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qr + r;
@@ -602,15 +637,14 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
 
 // dQ with K and V resident: wave owns 16 queries, walks keys <= its queries
 template <int HD>
-__global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+__device__ __forceinline__ void attn_bwd_dq_res_body(
+    bf16* lds, int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
-  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
-  const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
+  const int half = bid & 1, bh = bid >> 1, b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64;
   bf16* sK = lds;
   bf16* sV = lds + Tp * L::VLD;
@@ -625,14 +659,16 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
   const int qg = 2 * w + half;
   if (qg * 16 >= T) return;
   const int q = qg * 16 + j;
-  bf16x8 qf[KC], df[KC];
+  bf16x8 qf[KC], df[KC], of[KC];
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc) {
     qf[kc] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + kc * 32 + 8 * g) : bf16x8{};
     df[kc] = q < T ? *(const bf16x8*)(dOb + (long)q * dts + kc * 32 + 8 * g) : bf16x8{};
+    of[kc] = q < T ? *(const bf16x8*)(o + ((long)b * T + q) * dts + h * HD + kc * 32 + 8 * g) : bf16x8{};
   }
   const float lq = q < T ? lse[((long)b * H + h) * T + q] * LOG2E : 0.f;
-  const float dq_ = q < T ? delta[((long)b * H + h) * T + q] : 0.f;
+  static_assert(KC == 1, "fused delta assumes head_dim 32");
+  const float dq_ = group_sum(dot8(df[0], of[0]));  // delta = rowsum(dO*O) (same order as dK/dV)
   const float c = scale * LOG2E;
   f32x4 acc[HT];
 #pragma unroll
@@ -675,9 +711,37 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
   }
 }
 
+// One launch for the whole resident backward: blocks [0, 2BH) compute dK/dV, [2BH, 4BH) dQ.
+// delta = rowsum(dO*O) is computed inside both (no separate delta kernel / launch).
+template <int HD>
+__global__ void __launch_bounds__(RES_THREADS) attn_bwd_res_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int nkv = 2 * B * H;
+  if ((int)blockIdx.x < nkv) attn_bwd_dkdv_res_body<HD>(lds, blockIdx.x, qkv, o, dout, lse, dqkv, B, T, H, scale);
+  else attn_bwd_dq_res_body<HD>(lds, blockIdx.x - nkv, qkv, o, dout, lse, dqkv, B, T, H, scale);
+}
+
+// split variant (DTC_ATTN_MERGED=0): the same bodies as two launches
+template <int HD>
+__global__ void __launch_bounds__(RES_THREADS) attn_bwd_dkdv_res_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  attn_bwd_dkdv_res_body<HD>(lds, blockIdx.x, qkv, o, dout, lse, dqkv, B, T, H, scale);
+}
+template <int HD>
+__global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  attn_bwd_dq_res_body<HD>(lds, blockIdx.x, qkv, o, dout, lse, dqkv, B, T, H, scale);
+}
+
 // LDS bytes of the resident kernels; 0 if the sequence does not fit (then the tiled kernels run)
 inline long res_lds_fwd(int T, int HD) { const long Tp = (T + 63) / 64 * 64; return Tp * (AttnLds<32>::KLD + HD + 16) * 2; }
-inline long res_lds_dkdv(int T, int HD) { const long Tp = (T + 63) / 64 * 64 + 64; return 2 * Tp * (HD + 16) * 2; }
+inline long res_lds_dkdv(int T, int HD) { const long Tp = (T + 63) / 64 * 64 + 64; return 2 * Tp * (HD + 16) * 2 + Tp * 4; }
 inline long res_lds_dq(int T, int HD) { const long Tp = (T + 63) / 64 * 64; return 2 * Tp * (HD + 16) * 2; }
 constexpr long LDS_MAX = 160 * 1024;
 
@@ -722,14 +786,19 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
   long n = (long)B * T * H;
   int nb = (T + 63) / 64;
   dim3 grid(B * H * nb);
-  if (use_resident(T, HD)) {
-    hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
+  static const int merged = [] { const char* v = getenv("DTC_ATTN_MERGED"); return v ? atoi(v) : 1; }();
+  if (use_resident(T, HD) && !merged) {
     allow_lds(attn_bwd_dkdv_res_kernel<32>, res_lds_dkdv(T, HD));
     allow_lds(attn_bwd_dq_res_kernel<32>, res_lds_dq(T, HD));
     hipLaunchKernelGGL(attn_bwd_dkdv_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_dkdv(T, HD), st, qkv,
-                       dout, lse, ws, dqkv, B, T, H, scale);
-    hipLaunchKernelGGL(attn_bwd_dq_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_dq(T, HD), st, qkv,
-                       dout, lse, ws, dqkv, B, T, H, scale);
+                       o, dout, lse, dqkv, B, T, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_dq(T, HD), st, qkv, o,
+                       dout, lse, dqkv, B, T, H, scale);
+  } else if (use_resident(T, HD)) {
+    const long lds_b = std::max(res_lds_dkdv(T, HD), res_lds_dq(T, HD));
+    allow_lds(attn_bwd_res_kernel<32>, lds_b);
+    hipLaunchKernelGGL(attn_bwd_res_kernel<32>, dim3(B * H * 4), dim3(RES_THREADS), lds_b, st, qkv, o, dout, lse,
+                       dqkv, B, T, H, scale);
   } else if (HD == 32) {
     hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<32>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
