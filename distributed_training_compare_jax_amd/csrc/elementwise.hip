@@ -186,23 +186,50 @@ __global__ void wpe_bwd_kernel(const float* __restrict__ dh, float* __restrict__
 
 // ---------------------------------------------------------------- cross-entropy
 // per row: (max, sum exp) over P partials (strided), optional lse, rowstat outputs.
-__global__ void ce_combine_rows(const float* __restrict__ part, int M, int P, long srow, long spart,
-                                float* __restrict__ lse_out, float* __restrict__ rowstat) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+// lse[row] = mx + log sum_p s_p * exp(m_p - mx) over P partial (max, sum exp) pairs at
+// part[(row*srow + p*spart)*2].  Block = 16 rows x 16 partial lanes with the ROW on the fast lane
+// index: for the part-major GEMM partials (srow 1, spart M) lanes 0-15 read 16 consecutive rows'
+// pairs (one 128-B line) per partial — the one-wave-per-row mapping read 8 B per line.  Two passes
+// (row max, then the rescaled sum), each combined over the 16 lanes in fixed order.
+constexpr int CC_ROWS = 16, CC_LANES = 16;
+__global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__ part, int M, int P, long srow, long spart,
+                                                       float* __restrict__ lse_out, float* __restrict__ rowstat) {
+  const int r = threadIdx.x % CC_ROWS, pl = threadIdx.x / CC_ROWS;
+  const int row = blockIdx.x * CC_ROWS + r;
+  __shared__ float red[CC_LANES][CC_ROWS];
+  __shared__ float rmax[CC_ROWS];
   float mx = -INFINITY;
-  for (int p = lane; p < P; p += 64) mx = fmaxf(mx, part[(row * srow + p * spart) * 2]);
-  mx = warp_max(mx);
-  float s = 0.f;
-  for (int p = lane; p < P; p += 64) {
-    const float* q = part + (row * srow + p * spart) * 2;
-    if (q[1] > 0.f) s += q[1] * __expf(q[0] - mx);
+  if (row < M) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += CC_LANES) mx = fmaxf(mx, part[(row * srow + p * spart) * 2]);
   }
-  s = warp_sum(s);
-  if (lane == 0) {
-    if (lse_out) lse_out[row] = mx + __logf(s);
-    if (rowstat) { rowstat[2 * row] = mx; rowstat[2 * row + 1] = s; }
+  red[pl][r] = mx;
+  __syncthreads();
+  if (pl == 0) {
+    float m = red[0][r];
+#pragma unroll
+    for (int q = 1; q < CC_LANES; ++q) m = fmaxf(m, red[q][r]);
+    rmax[r] = m;
+  }
+  __syncthreads();
+  mx = rmax[r];
+  float s = 0.f;
+  if (row < M) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += CC_LANES) {
+      const f32x2 q = *(const f32x2*)(part + (row * srow + p * spart) * 2);
+      if (q[1] > 0.f) s += q[1] * __expf(q[0] - mx);
+    }
+  }
+  __syncthreads();
+  red[pl][r] = s;
+  __syncthreads();
+  if (pl == 0 && row < M) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < CC_LANES; ++q) t += red[q][r];
+    if (lse_out) lse_out[row] = mx + __logf(t);
+    if (rowstat) { rowstat[2 * row] = mx; rowstat[2 * row + 1] = t; }
   }
 }
 
@@ -442,7 +469,8 @@ int dtc_ce_combine(const float* part, int M, int P, long srow, long spart, const
                    float* rowstat_out, float loss_scale, float* loss_out, int accumulate, hipStream_t st) {
   float* lse = lse_out;
   if (loss_out && !lse) return 3002;
-  hipLaunchKernelGGL(ce_combine_rows, dim3((M + 3) / 4), dim3(256), 0, st, part, M, P, srow, spart, lse, rowstat_out);
+  hipLaunchKernelGGL(ce_combine_rows, dim3((M + CC_ROWS - 1) / CC_ROWS), dim3(256), 0, st, part, M, P, srow, spart, lse,
+                     rowstat_out);
   DTC_CHECK_LAUNCH();
   if (loss_out) {
     hipLaunchKernelGGL(ce_loss_reduce, dim3(1), dim3(1024), 0, st, lse, label_logit, M, loss_scale, loss_out, accumulate);

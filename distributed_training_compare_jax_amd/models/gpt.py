@@ -148,11 +148,17 @@ class GPTStage:
 
     # ------------------------------------------------------------------ embed
     def embed_forward(self, ids: torch.Tensor, step: torch.Tensor, row0: int, ctx: Dict,
-                      want_keys: bool = True) -> torch.Tensor:
-        """ids int32 [b, T] → h fp32 [b*T, D]  (wte gather + wpe + dropout, GPTModel.py:30-38)."""
+                      want_keys: bool = True, keys: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """ids int32 [b, T] → h fp32 [b*T, D]  (wte gather + wpe + dropout, GPTModel.py:30-38).
+
+        ``keys``: the backward's sort keys, already computed on the host (``E.embed_sort_keys_host``);
+        otherwise (``want_keys``) they are sorted on the device."""
         f = self.flat
         h = E.embed_fwd(ids, f.p("wte"), f.p("wpe"), self.cfg.dropout, self.seed, step, row0)
-        ctx["embed"] = (ids, row0, self.embed_keys(ids) if want_keys else None)
+        if keys is not None:
+            ctx["embed"] = (ids, row0, (keys, None))
+        else:
+            ctx["embed"] = (ids, row0, self.embed_keys(ids) if want_keys else None)
         return h
 
     def embed_keys(self, ids: torch.Tensor):
@@ -275,13 +281,14 @@ class GPTStage:
         f = self.flat
         yf, muf, rsf = LN.layernorm_fwd(x, f.p("lnf.g"), f.p("lnf.b"), self.eps, self.act_dtype)
         lab = labels.reshape(-1)
+        tp1 = self.tp.size == 1
         logits, rowstat, lab_logit = X.lmhead_logits_partials(yf, f.w("lm_head.w"), f.p("lm_head.b"), lab,
-                                                              self.v_start, self.v_valid)
-        if self.tp.size > 1:
+                                                              self.v_start, self.v_valid, combine=not tp1)
+        if not tp1:
             rowstats = self.tp.all_gather_stack(rowstat)  # [tp, M, 2]
             self.tp.all_reduce_(lab_logit)
         else:
-            rowstats = rowstat.unsqueeze(0)
+            rowstats = rowstat  # the GEMM's per-tile partials [P, M, 2]: combined once, in ce_finalize
         lse, loss = X.ce_finalize(rowstats, lab_logit, loss_scale, loss_out, accumulate)
         ctx["head"] = (x, yf, muf, rsf, logits, lse, lab)
         return loss

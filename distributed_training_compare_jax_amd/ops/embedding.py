@@ -113,6 +113,28 @@ def embed_bwd(ids: torch.Tensor, dh: torch.Tensor, dwte: torch.Tensor, dwpe: tor
 SORT_MAX = 32768  # keys one LDS bitonic sort handles (csrc/elementwise.hip)
 
 
+def sort_bits(n: int) -> int:
+    """Token-index bits of a sort key (``dtc_embed_sort_bits``)."""
+    nb = 1
+    while (1 << nb) < n:
+        nb += 1
+    return nb
+
+
+def embed_sort_keys_host(ids: np.ndarray, out: np.ndarray = None) -> np.ndarray:
+    """Host-side version of :func:`embed_sort_keys` (same keys: the sorted order of unique keys
+    is unique).  The training loop computes them while the GPU runs the previous step and ships
+    them with the batch, so no sort kernel sits in the step."""
+    flat = np.ascontiguousarray(ids, dtype=np.int32).reshape(-1)
+    n = flat.size
+    keys = (flat.astype(np.uint32) << np.uint32(sort_bits(n))) | np.arange(n, dtype=np.uint32)
+    keys.sort()
+    if out is not None:
+        out[:] = keys.view(np.int32)
+        return out
+    return keys.view(np.int32)
+
+
 def embed_sort_keys(ids: torch.Tensor, vocab: int, out: torch.Tensor = None) -> torch.Tensor:
     """Sorted ``id << nb | token`` keys (int32 storage of uint32) for the deterministic backward.
 

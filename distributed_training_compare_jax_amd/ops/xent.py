@@ -22,11 +22,13 @@ from . import _native as N
 
 
 def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, labels: torch.Tensor,
-                           vocab_start: int, n_valid: int):
+                           vocab_start: int, n_valid: int, combine: bool = True):
     """Returns ``(logits [M,Vl], rowstat [M,2] (max,Σexp), label_logit [M])`` for the local vocab shard.
 
     ``n_valid`` = number of real (non-pad) columns in this shard; ``label_logit`` is 0 for rows
-    whose label is outside the shard."""
+    whose label is outside the shard.  ``combine=False`` returns the GEMM's raw per-tile partials
+    ``[P, M, 2]`` instead of ``rowstat`` (a single-shard loss feeds them straight to
+    :func:`ce_finalize`: one combine launch instead of two)."""
     M, D = h.shape
     Vl = w.shape[0]
     if not h.is_cuda:
@@ -38,7 +40,8 @@ def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, la
         loc = labels.long() - vocab_start
         inside = (loc >= 0) & (loc < n_valid)
         lab = torch.where(inside, logits.gather(1, loc.clamp(0, Vl - 1)[:, None])[:, 0], torch.zeros(M))
-        return logits.to(h.dtype), torch.stack([mx, se], -1), lab
+        rs = torch.stack([mx, se], -1)
+        return logits.to(h.dtype), (rs if combine else rs.unsqueeze(0)), lab
     L = N.lib()
     P = int(L.dtc_lmhead_nparts(M, Vl, D))
     logits = torch.empty(M, Vl, dtype=torch.bfloat16, device=h.device)
@@ -48,6 +51,8 @@ def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, la
 
     _gemm_native(0, M, Vl, D, h, h.stride(0), w, w.stride(0), logits, Vl, epi=N.EPI_LMHEAD, bias=b,
                  labels=labels, vocab_start=vocab_start, n_valid=n_valid, part=part, label_out=lab)
+    if not combine:
+        return logits, part, lab
     rowstat = torch.empty(M, 2, dtype=torch.float32, device=h.device)
     N.check(L.dtc_ce_combine(part.data_ptr(), M, P, 1, M, None, None, rowstat.data_ptr(), 0.0, None, 0,
                              N.stream_ptr(h.device)), "dtc_ce_combine")

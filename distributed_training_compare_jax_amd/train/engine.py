@@ -20,6 +20,7 @@ import torch.distributed as dist
 from ..config.schema import ModelConfig, OptimConfig, TrainConfig
 from ..models.gpt import GPTStage, StageLayout
 from ..models.params import stage_param_specs
+from ..ops import embedding as E
 from ..ops import optim as O
 from ..parallel.buffers import FlatParams
 from ..parallel.dist import DistInfo
@@ -113,6 +114,12 @@ class Engine:
         pin = on_gpu
         self._host = [torch.zeros(2, self.feed_rows, T, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self._host_i = 0
+        # the embedding backward's sort keys of the fed ids, sorted on the host while the GPU runs the
+        # previous step (a one-block device sort would sit serially in the step: ~48 us)
+        self.host_keys = bool(on_gpu and pp == 1 and self.feed_rows * T <= E.SORT_MAX)
+        if self.host_keys:
+            self._host_keys = [torch.zeros(self.feed_rows * T, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+            self.keys = torch.zeros(self.feed_rows * T, dtype=torch.int32, device=self.device)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
         if pp > 1:
             self.recv_x = [torch.zeros(self.mb_rows * T, D, dtype=torch.float32, device=self.device)
@@ -169,6 +176,10 @@ class Engine:
         rows, or the whole global batch under the DP embedding gather) → static device ids/labels."""
         assert batch_np.shape[0] == self.feed_rows, (batch_np.shape, self.feed_rows)
         h = self._host[self._host_i]
+        if self.host_keys:
+            hk = self._host_keys[self._host_i]
+            E.embed_sort_keys_host(batch_np[:, :-1], out=hk.numpy())
+            self.keys.copy_(hk, non_blocking=True)
         self._host_i ^= 1
         h[0].copy_(torch.from_numpy(batch_np[:, :-1]))
         h[1].copy_(torch.from_numpy(batch_np[:, 1:]))
@@ -219,8 +230,12 @@ class Engine:
         dp = self.mesh.dp
         ctx: Dict = {}
         step = self.opt.step_t
-        h = st.embed_forward(self.ids, step, self.row0, ctx, want_keys=not self.embed_gather)
-        gathered = (self.ids_all, 0, st.embed_keys(self.ids_all)) if self.embed_gather else None
+        hk = self.keys if self.host_keys else None
+        h = st.embed_forward(self.ids, step, self.row0, ctx, want_keys=not self.embed_gather,
+                             keys=None if self.embed_gather else hk)
+        gathered = None
+        if self.embed_gather:
+            gathered = (self.ids_all, 0, (hk, None) if hk is not None else st.embed_keys(self.ids_all))
         h = st.stage_forward(h, b, ctx)
         st.head_forward(h, self.labels, 1.0 / (b * T), ctx, loss_out=self.loss)
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)

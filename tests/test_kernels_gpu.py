@@ -300,3 +300,15 @@ def test_wgrad_fused_bias_grad(cuda, Mtok, N, K):
         red.flush()
         _close(dw, beta * dw0 + dy.float().t() @ x.float(), 2e-3, "dW")
         _close(db, beta * db0 + dy.float().sum(0), 1e-5, "db")
+
+
+def test_host_sort_keys_match_device(cuda):
+    """The host-side embedding sort keys (shipped with the batch) equal the device bitonic sort."""
+    import numpy as np
+
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, 50258, (8, 512), generator=g, dtype=torch.int32)
+    ids[0, :100] = 7  # long run of one id
+    dev = E.embed_sort_keys(ids.to(cuda), 50258)
+    host = E.embed_sort_keys_host(ids.numpy())
+    assert np.array_equal(dev.cpu().numpy(), host)
