@@ -341,6 +341,21 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
   };
   bf16* const s0 = smem;
   bf16* const s1 = smem + BUF;
+  // dGELU epilogue operand u (bf16, the fragment layout): loaded before the main loop so its
+  // latency hides under the MFMAs instead of stalling the epilogue (measured +8.6 us at fc2 dgrad)
+  constexpr bool PRE_U = (EPI == EPI_DGELU) && (WN == 64);
+  bf16x4 upre[PRE_U ? TN : 1][PRE_U ? TM : 1];
+  if constexpr (PRE_U) {
+    const int g4p = 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm * WM + j * 16 + (lane & 15), n = n0 + wn * WN + i * 16 + g4p;
+        upre[i][j] = (m < M && n + 4 <= N) ? *(const bf16x4*)((const bf16*)e.aux + (long)m * e.ldaux + n)
+                                           : bf16x4{};
+      }
+  }
   // fused bias gradient (wgrad only: MN-major A = dY, first N-tile column of blocks)
   const bool do_cs = !AK && e.colsum != nullptr && tn_idx == 0;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -439,6 +454,41 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
     EpiPre<TN, TM> pre;
     epi_prefetch<TN, TM>(e, m0 + wm * WM, n0 + wn * WN, lane, true, pre);
     lmhead_epilogue<TN, TM>(acc, e, m0 + wm * WM, n0 + wn * WN, tn_idx * 2 + wn, lane, pre);
+    return;
+  }
+  if constexpr ((EPI == EPI_GELU || EPI == EPI_DGELU) && !OUTF32 && WN == 64) {
+    // bf16 outputs through a per-wave LDS stage so global stores leave as full 128-B rows (the
+    // fragment layout writes 16 rows x 32 B per instruction); LDS is free after the last barrier
+    bf16* stg = smem + wave * (WM * 64);
+    const int mb = m0 + wm * WM, nb = n0 + wn * WN;
+    f32x4 bb[TN];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = nb + i * 16 + g4;
+      bb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e.bias) {
+        if (n + 4 <= N) bb[i] = *(const f32x4*)(e.bias + n);
+        else for (int r = 0; r < 4; ++r) if (n + r < N) bb[i][r] = e.bias[n + r];
+      }
+    }
+#pragma unroll
+    for (int pass = 0; pass < (EPI == EPI_GELU ? 2 : 1); ++pass) {
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int i = 0; i < TN; ++i) {
+          bf16x4 ob;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = e.alpha * acc[i][j][r] + bb[i][r];
+            if constexpr (EPI == EPI_GELU) { if (pass == 1) v = gelu_tanh_f(v); }
+            if constexpr (EPI == EPI_DGELU) v *= gelu_tanh_grad_f((float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r]);
+            ob[r] = f2bf(v);
+          }
+          stage_put(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
+        }
+      stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
+    }
     return;
   }
 #pragma unroll
@@ -852,7 +902,7 @@ Plan make_plan(int M, int N, int K, int allow_split) {
     p.split = (int)std::max(1L, std::min((long)nk / 64, (512 + t128 - 1) / t128));
     return p;
   }
-  static const int wgrad_tile = [] { const char* v = getenv("DTC_WGRAD_TILE"); return v ? atoi(v) : 64; }();
+  static const int wgrad_tile = [] { const char* v = getenv("DTC_WGRAD_TILE"); return v ? atoi(v) : 128; }();  // single-stream A/B: 128 (256 blocks) 5.99 vs 64 6.05 ms
   if (allow_split == 1 && wgrad_tile == 128 && t128 < 256) {  // weight gradients: 128^2 tiles + split-K
     static const int target = [] { const char* v = getenv("DTC_WGRAD_BLOCKS"); return v ? atoi(v) : 256; }();
     while (t128 * p.split < target && nk / (p.split * 2) >= 8) p.split *= 2;
