@@ -69,8 +69,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
 #pragma unroll
   for (int i = 0; i < NV; ++i) { ag[i] = f32x4{0.f, 0.f, 0.f, 0.f}; ab[i] = ag[i]; ao[i] = ag[i]; }
   const int r0 = blockIdx.x * LN_BWD_ROWS + wave * 2;
-  f32x4 xh[2][NV], d[2][NV], rs_[2];
+  f32x4 xh[2][NV], d[2][NV], rv[2][NV], gv[NV];
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, rsv[2] = {0.f, 0.f};
+  // every global load of the block (x, dy, the residual gradient, gamma) is issued before the first
+  // use: the residual-gradient read used to sit after the row reductions, fully exposed
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    gv[i] = c < D4 ? ((const f32x4*)g)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int row = r0 + q;
@@ -80,14 +87,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
-      f32x4 xv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+      f32x4 xv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f}, rr = {0.f, 0.f, 0.f, 0.f};
       if (ok && c < D4) {
         xv = ((const f32x4*)(x + (long)row * D))[c];
         if (dy_f32) dv = ((const f32x4*)((const float*)dy + (long)row * D))[c];
         else { bf16x4 t = ((const bf16x4*)((const bf16*)dy + (long)row * D))[c]; dv = f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]}; }
+        if (dres) rr = ((const f32x4*)(dres + (long)row * D))[c];
       }
       xh[q][i] = (xv - mu) * rsv[q];
       d[q][i] = dv;
+      rv[q][i] = rr;
     }
   }
 #pragma unroll
@@ -96,7 +105,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
     for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       if (c < D4) {
-        f32x4 gd = d[q][i] * ((const f32x4*)g)[c];
+        f32x4 gd = d[q][i] * gv[i];
         s1[q] += gd[0] + gd[1] + gd[2] + gd[3];
         f32x4 t2 = gd * xh[q][i];
         s2[q] += t2[0] + t2[1] + t2[2] + t2[3];
@@ -113,16 +122,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
     for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       if (c < D4) {
-        f32x4 gd = d[q][i] * ((const f32x4*)g)[c];
+        f32x4 gd = d[q][i] * gv[i];
         f32x4 o = (gd - c1 - xh[q][i] * c2) * rsv[q];
-        if (dres) o += ((const f32x4*)(dres + (long)row * D))[c];
+        if (dres) o += rv[q][i];
         ((f32x4*)(dx + (long)row * D))[c] = o;
         if (dx_c) ((bf16x4*)(dx_c + (long)row * D))[c] = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
         ao[i] += o;
       }
     }
   }
-  (void)rs_;
   // block reduce of the column partials over the 4 waves (fixed order); part[block][nslab][D]
   __shared__ __attribute__((aligned(16))) float red[4][3][NV * 256];
 #pragma unroll
