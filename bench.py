@@ -138,7 +138,7 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": scaling,
-            "vs_baseline": round(value / base, 3) if base else None, "dtype": "bf16",
+            "vs_baseline": round(value / base, 3) if base else None, "dtype": tc.dtype,
             "data": "synthetic (FineWeb-shaped token stream, random-init weights)",
             "config": {"model": f"{mc.name} (d{mc.d_model} L{mc.n_layers} H{mc.n_heads} F{mc.d_ff} "
                                 f"T{mc.max_seq_len} V{mc.vocab_size})",

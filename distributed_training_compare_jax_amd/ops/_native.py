@@ -134,6 +134,16 @@ def lib():
     return _LIB
 
 
+def library_path(t: torch.Tensor) -> bool:
+    """True when an op runs its torch implementation: CPU tensors (the fp32 oracle / gloo path) and
+    the GPU exact-fp32 parity mode (``TrainConfig.dtype: fp32``), whose GEMM-shaped ops
+    (Dense layers, attention scores, lm_head) run as fp32 library GEMMs (rocBLAS via torch; MI355X
+    has no reduced-precision fp32 MFMA, so they are exact) — every bf16 tensor takes the HIP
+    kernels.  LayerNorm, embedding/dropout, cross-entropy combine, reductions and AdamW run their
+    HIP kernels in both GPU precisions."""
+    return (not t.is_cuda) or t.dtype == torch.float32
+
+
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 

@@ -26,10 +26,10 @@ def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None):
     B, T, C3 = qkv.shape
     hd = C3 // (3 * n_heads)
     scale = scale if scale is not None else hd ** -0.5
-    if not qkv.is_cuda:
+    if N.library_path(qkv):
         q, k, v = qkv.float().view(B, T, 3, n_heads, hd).unbind(2)
         s = torch.einsum("bthd,bshd->bhts", q, k) * scale
-        mask = torch.ones(T, T, dtype=torch.bool).tril()
+        mask = torch.ones(T, T, dtype=torch.bool, device=qkv.device).tril()
         s = s.masked_fill(~mask, float("-inf"))
         lse = torch.logsumexp(s, -1)
         p = torch.exp(s - lse[..., None])
@@ -51,11 +51,11 @@ def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Te
     B, T, C3 = qkv.shape
     hd = C3 // (3 * n_heads)
     scale = scale if scale is not None else hd ** -0.5
-    if not qkv.is_cuda:
+    if N.library_path(qkv):
         q, k, v = qkv.float().view(B, T, 3, n_heads, hd).unbind(2)
         dof = do.float().view(B, T, n_heads, hd)
         s = torch.einsum("bthd,bshd->bhts", q, k) * scale
-        mask = torch.ones(T, T, dtype=torch.bool).tril()
+        mask = torch.ones(T, T, dtype=torch.bool, device=qkv.device).tril()
         s = s.masked_fill(~mask, float("-inf"))
         p = torch.exp(s - lse[..., None])
         dv = torch.einsum("bhts,bthd->bshd", p, dof)

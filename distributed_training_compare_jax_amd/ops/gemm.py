@@ -123,7 +123,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     Nn = w.shape[0]
     assert w.shape[1] == K
     out_dtype = out_dtype or x.dtype
-    if not x.is_cuda:
+    if N.library_path(x):
         y = _f32(x) @ _f32(w).t()
         if bias is not None:
             y = y + bias.float()
@@ -139,7 +139,7 @@ def linear_resid(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
     """fp32 ``out = resid + x·Wᵀ + bias`` (resid/bias optional; ``out`` may alias ``resid``)."""
     M, K = x.shape
     Nn = w.shape[0]
-    if not x.is_cuda:
+    if N.library_path(x):
         y = _f32(x) @ _f32(w).t()
         if bias is not None:
             y = y + bias.float()
@@ -165,7 +165,7 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]):
     """Returns ``(u, g)``: pre-activation and ``gelu_tanh(u)`` (both activation dtype)."""
     M, K = x.shape
     Nn = w.shape[0]
-    if not x.is_cuda:
+    if N.library_path(x):
         u = _f32(x) @ _f32(w).t()
         if bias is not None:
             u = u + bias.float()
@@ -183,7 +183,7 @@ def matmul_nn(dy: torch.Tensor, w: torch.Tensor, out_dtype=torch.float32) -> tor
     M, Nn = dy.shape
     K = w.shape[1]
     assert w.shape[0] == Nn
-    if not dy.is_cuda:
+    if N.library_path(dy):
         return (_f32(dy) @ _f32(w)).to(out_dtype)
     _check2d(dy, "dy"); _check2d(w, "w")
     dx = torch.empty(M, K, dtype=out_dtype, device=dy.device)
@@ -195,7 +195,7 @@ def matmul_nn_dgelu(dy: torch.Tensor, w: torch.Tensor, u: torch.Tensor) -> torch
     """dU = (dY·W) ⊙ gelu_tanh'(u)   (fc2 dgrad fused with the GELU backward)."""
     M, Nn = dy.shape
     K = w.shape[1]
-    if not dy.is_cuda:
+    if N.library_path(dy):
         return ((_f32(dy) @ _f32(w)) * gelu_tanh_grad(_f32(u))).to(u.dtype)
     _check2d(dy, "dy"); _check2d(w, "w")
     du = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
@@ -214,7 +214,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
     M, Nn = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and tuple(dw.shape) == (Nn, K)
-    if not dy.is_cuda:
+    if N.library_path(dy):
         g = _f32(dy).t() @ _f32(x)
         if beta != 0.0:
             dw.mul_(beta).add_(g)

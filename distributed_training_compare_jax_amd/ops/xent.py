@@ -31,7 +31,7 @@ def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, la
     :func:`ce_finalize`: one combine launch instead of two)."""
     M, D = h.shape
     Vl = w.shape[0]
-    if not h.is_cuda:
+    if N.library_path(h):
         logits = h.float() @ w.float().t() + b.float()
         if n_valid < Vl:
             logits[:, n_valid:] = float("-inf")
@@ -39,7 +39,7 @@ def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, la
         se = torch.exp(logits - mx[:, None]).sum(-1)
         loc = labels.long() - vocab_start
         inside = (loc >= 0) & (loc < n_valid)
-        lab = torch.where(inside, logits.gather(1, loc.clamp(0, Vl - 1)[:, None])[:, 0], torch.zeros(M))
+        lab = torch.where(inside, logits.gather(1, loc.clamp(0, Vl - 1)[:, None])[:, 0], torch.zeros(M, device=h.device))
         rs = torch.stack([mx, se], -1)
         return logits.to(h.dtype), (rs if combine else rs.unsqueeze(0)), lab
     L = N.lib()
@@ -92,14 +92,15 @@ def ce_backward_inplace(logits: torch.Tensor, lse: torch.Tensor, labels: torch.T
     ``colpart=True`` also returns fp32 column partial sums of dlogits ``[R, V]`` (R row chunks)
     from the same pass — the lm_head bias gradient is their column sum (``gemm.colsum``)."""
     M, Vl = logits.shape
-    if not logits.is_cuda:
+    if N.library_path(logits):
         p = torch.exp(logits.float() - lse[:, None])
         if n_valid < Vl:
             p[:, n_valid:] = 0.0
         loc = labels.long() - vocab_start
         inside = (loc >= 0) & (loc < n_valid)
-        rows = torch.nonzero(inside)[:, 0]
-        p[rows, loc[rows]] -= 1.0
+        # one-hot subtraction without a data-dependent shape (graph-capturable on the GPU fp32 path)
+        rows = torch.arange(M, device=logits.device)
+        p.index_put_((rows, loc.clamp(0, Vl - 1)), -inside.to(p.dtype), accumulate=True)
         logits.copy_((p * grad_scale).to(logits.dtype))
         if colpart:
             return logits, (p * grad_scale).sum(0, keepdim=True)

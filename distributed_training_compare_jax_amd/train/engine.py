@@ -41,8 +41,6 @@ class Engine:
         m = self.mesh
         on_gpu = self.device.type == "cuda"
         self.act_dtype = torch.bfloat16 if (on_gpu and train_cfg.dtype == "bf16") else torch.float32
-        if on_gpu and self.act_dtype == torch.float32:
-            raise NotImplementedError("fp32 compute on GPU: use dtype: bf16 (fp32 parity mode runs on the CPU path)")
 
         # ---- batch geometry (reference: `batch` is the global batch, train_config_*.yaml:1)
         T = model_cfg.max_seq_len
