@@ -291,21 +291,26 @@ __device__ __forceinline__ void lmhead_epilogue(const f32x4 (&acc)[TN][TM], cons
   if (stage) stage_out<TM * 16>(stage, (bf16*)e.C, e.ldc, m_base, n_base, e.M, e.N, lane);
 }
 
+// LDS elements of the register-staged kernel (two stages of A and B tiles)
+template <int BM, int BN, int BK, bool AK, bool BKM>
+constexpr int gemm_smem_elems() { return 2 * (Tile<BM, BK, AK>::ELEMS + Tile<BN, BK, BKM>::ELEMS); }
+
+// The register-staged GEMM tile program; `bid` is the block's id within ITS problem (so two
+// problems can share one launch: gemm_pair_kernel) and `smem` its LDS.
 template <int BM, int BN, int BK, bool AK, bool BKM, int EPI, bool OUTF32>
-__global__ void __launch_bounds__(NT, 2)
-gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __restrict__ B, long ldb, int b_bytes, int M,
-            int N, int K,
-            int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+__device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __restrict__ A, long lda, int a_bytes,
+                                          const bf16* __restrict__ B, long ldb, int b_bytes, int M, int N, int K,
+                                          int tiles_m, int tiles_n, int gm, int split, int k_per_split,
+                                          float* __restrict__ slab, const Epi& e) {
   using TA = Tile<BM, BK, AK>;
   using TB = Tile<BN, BK, BKM>;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (TA::ELEMS + TB::ELEMS)];
   constexpr int BUF = TA::ELEMS + TB::ELEMS;  // one stage: A tile then B tile
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   const int ntiles = tiles_m * tiles_n;
-  const int lid = xcd_remap(blockIdx.x, ntiles * split);
+  const int lid = xcd_remap(bid, ntiles * split);
   const int tile = lid % ntiles, z = lid / ntiles;
   // grouped tile order: groups of `gm` M-tiles sweep all N-tiles, so the run of tiles one XCD
   // receives touches few A rows AND few B columns (per-XCD L2 footprint; gm = tiles_m -> M fastest)
@@ -499,6 +504,44 @@ gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __res
       int n = n0 + wn * WN + i * 16 + g4;
       if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
     }
+}
+
+template <int BM, int BN, int BK, bool AK, bool BKM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(NT, 2)
+gemm_kernel(const bf16* __restrict__ A, long lda, int a_bytes, const bf16* __restrict__ B, long ldb, int b_bytes, int M,
+            int N, int K, int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[gemm_smem_elems<BM, BN, BK, AK, BKM>()];
+  gemm_body<BM, BN, BK, AK, BKM, EPI, OUTF32>(smem, blockIdx.x, A, lda, a_bytes, B, ldb, b_bytes, M, N, K, tiles_m,
+                                               tiles_n, gm, split, k_per_split, slab, e);
+}
+
+// One register-staged problem, fully planned (operands, grid geometry, epilogue).
+struct GemmLaunch {
+  const bf16* A; long lda; int a_bytes;
+  const bf16* B; long ldb; int b_bytes;
+  int M, N, K, tiles_m, tiles_n, gm, split, kps, nblocks;
+  float* slab;
+  Epi e;
+};
+
+template <int BM, int BN, int BK, bool AK, bool BKM, int EPI, bool OUTF32>
+struct GemmCfg {
+  static constexpr int SMEM = gemm_smem_elems<BM, BN, BK, AK, BKM>();
+  __device__ __forceinline__ static void run(bf16* smem, int bid, const GemmLaunch& g) {
+    gemm_body<BM, BN, BK, AK, BKM, EPI, OUTF32>(smem, bid, g.A, g.lda, g.a_bytes, g.B, g.ldb, g.b_bytes, g.M, g.N, g.K,
+                                                 g.tiles_m, g.tiles_n, g.gm, g.split, g.kps, g.slab, g.e);
+  }
+};
+
+// Two independent GEMMs in ONE launch (a layer's dgrad and weight gradient read the same dY):
+// blocks [0, nb1) run problem 1, the rest problem 2.  Saves a dependent kernel boundary and lets
+// the second problem's blocks fill the CUs the first one's last wave leaves idle.  nb1 % 8 == 0
+// keeps both problems' XCD-aware tile maps (blockIdx % 8) intact.
+template <class C1, class C2>
+__global__ void __launch_bounds__(NT, 2) gemm_pair_kernel(GemmLaunch g1, GemmLaunch g2) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[C1::SMEM > C2::SMEM ? C1::SMEM : C2::SMEM];
+  if ((int)blockIdx.x < g1.nblocks) C1::run(smem, blockIdx.x, g1);
+  else C2::run(smem, blockIdx.x - g1.nblocks, g2);
 }
 
 
@@ -928,6 +971,33 @@ inline int operand_bytes(bool kmajor, int rows, int K, long ld) {
   return (int)std::min(n * 2, (long)0x7FFFFFF0);
 }
 
+// Plan a register-staged launch of problem `a` with tile BMxBN (grid geometry, operand extents,
+// epilogue) — shared by the single and the paired launch paths.
+template <int BM, int BN, bool AK, bool BKM>
+GemmLaunch make_launch(const GemmArgs& a, const Plan& p) {
+  GemmLaunch g;
+  Epi& e = g.e;
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
+  e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
+  e.colsum = a.colsum;
+  g.tiles_m = (a.M + BM - 1) / BM;
+  g.tiles_n = (a.N + BN - 1) / BN;
+  e.nparts = g.tiles_n * 2;
+  const int nk = a.K / p.bk;
+  g.kps = ((nk + p.split - 1) / p.split) * p.bk;
+  const int ntiles = g.tiles_m * g.tiles_n;
+  g.gm = g.tiles_m;
+  if (g.tiles_n <= 16) g.gm = std::max(1, std::min(g.tiles_m, (ntiles / 8 + g.tiles_n - 1) / g.tiles_n));
+  g.split = p.split;
+  g.nblocks = ntiles * p.split;
+  g.A = (const bf16*)a.A; g.lda = a.lda; g.a_bytes = operand_bytes(AK, a.M, a.K, a.lda);
+  g.B = (const bf16*)a.B; g.ldb = a.ldb; g.b_bytes = operand_bytes(BKM, a.N, a.K, a.ldb);
+  g.M = a.M; g.N = a.N; g.K = a.K;
+  g.slab = (float*)a.workspace;
+  return g;
+}
+
 template <int BM, int BN, bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   Epi e;
@@ -1041,9 +1111,57 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   return 0;
 }
 
+// Paired launch: a1 = dgrad (layout 1, whole-K tiles), a2 = weight gradient (layout 2, split-K slabs
+// left for the caller's batched reducer when split > 1).  Only register-staged, BK = 64 plans pair.
+template <class C1, class C2, int BM1, int BM2>
+int launch_pair_t(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const Plan& p2, hipStream_t st) {
+  const GemmLaunch g1 = make_launch<BM1, BM1, true, false>(a1, p1);
+  const GemmLaunch g2 = make_launch<BM2, BM2, false, false>(a2, p2);
+  if (g1.nblocks % 8) return 1100;  // XCD maps would disagree: not pairable
+  hipLaunchKernelGGL((gemm_pair_kernel<C1, C2>), dim3(g1.nblocks + g2.nblocks), dim3(NT), 0, st, g1, g2);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int EPI1, bool F1>
+int launch_pair_w(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const Plan& p2, hipStream_t st) {
+  using W128 = GemmCfg<128, 128, 64, false, false, EPI_STORE, true>;
+  using W64 = GemmCfg<64, 64, 64, false, false, EPI_STORE, true>;
+  if (p1.bm == 128) {
+    using D = GemmCfg<128, 128, 64, true, false, EPI1, F1>;
+    return p2.bm == 128 ? launch_pair_t<D, W128, 128, 128>(a1, p1, a2, p2, st)
+                        : launch_pair_t<D, W64, 128, 64>(a1, p1, a2, p2, st);
+  }
+  using D = GemmCfg<64, 64, 64, true, false, EPI1, F1>;
+  return p2.bm == 128 ? launch_pair_t<D, W128, 64, 128>(a1, p1, a2, p2, st)
+                      : launch_pair_t<D, W64, 64, 64>(a1, p1, a2, p2, st);
+}
+
 }  // namespace
 
 extern "C" {
+
+// dgrad (a1: layout 1, epi STORE or DGELU) and weight gradient (a2: layout 2, fp32, defer_reduce
+// when split) of one Dense in one launch.  Returns 1100 when the pair cannot share a launch (the
+// caller then issues the two GEMMs separately).
+int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
+  if (a1->layout != 1 || a2->layout != 2) return 1100;
+  if (a1->K % 64 || a2->K % 64 || a1->N % 8 || a2->M % 8 || a2->N % 8) return 1100;
+  if (a1->lda % 8 || a1->ldb % 8 || a1->ldc % 4 || a2->lda % 8 || a2->ldb % 8 || a2->ldc % 4) return 1100;
+  if (a1->M <= 0 || a1->N <= 0 || a2->M <= 0 || a2->N <= 0) return 1100;
+  if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
+  if (big_split(1, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
+  const Plan p1 = make_plan(a1->M, a1->N, a1->K, (a1->epi == EPI_STORE && a1->c_f32) ? 2 : 0);
+  const Plan p2 = make_plan(a2->M, a2->N, a2->K, 1);
+  if (p1.split != 1 || p1.bk != 64 || p2.bk != 64) return 1100;
+  if (p2.split > 1 && (!a2->defer_reduce || a2->ws_bytes < (long)p2.split * a2->M * a2->N * 4)) return 1100;
+  const int dma = gemm_dma_mask();
+  if ((dma & (p1.bm == 64 ? 2 : 4)) || (dma & (p2.bm == 64 ? 2 : 4))) return 1100;
+  if (a1->epi == EPI_DGELU && !a1->c_f32) return launch_pair_w<EPI_DGELU, false>(*a1, p1, *a2, p2, st);
+  if (a1->epi == EPI_STORE && a1->c_f32) return launch_pair_w<EPI_STORE, true>(*a1, p1, *a2, p2, st);
+  if (a1->epi == EPI_STORE && !a1->c_f32) return launch_pair_w<EPI_STORE, false>(*a1, p1, *a2, p2, st);
+  return 1100;
+}
 
 int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }
 

@@ -82,11 +82,16 @@ def reserve_workspace(device, nbytes: int, role: str = "main"):
         _workspace(torch.device(device), nbytes)
 
 
-def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, *,
-                 epi: int = N.EPI_STORE, bias=None, aux=None, ldaux: int = 0, aux_out=None,
-                 alpha: float = 1.0, beta: float = 0.0, labels=None, vocab_start: int = 0,
-                 n_valid: int = 0, part=None, label_out=None, workspace=None, defer_reduce: int = 0,
-                 colsum=None):
+def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, **kw):
+    args = _gemm_args(layout, M, N_, K, a, lda, b, ldb, c, ldc, **kw)
+    N.check(N.lib().dtc_gemm(args, N.stream_ptr(c.device)), "dtc_gemm")
+
+
+def _gemm_args(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, *,
+               epi: int = N.EPI_STORE, bias=None, aux=None, ldaux: int = 0, aux_out=None,
+               alpha: float = 1.0, beta: float = 0.0, labels=None, vocab_start: int = 0,
+               n_valid: int = 0, part=None, label_out=None, workspace=None, defer_reduce: int = 0,
+               colsum=None) -> "N.GemmArgs":
     L = N.lib()
     if workspace is not None:
         ws = workspace.view(torch.uint8) if workspace.dtype != torch.uint8 else workspace
@@ -102,7 +107,7 @@ def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int,
         part=N.ptr(part), label_out=N.ptr(label_out),
         workspace=N.ptr(ws), ws_bytes=0 if ws is None else ws.numel(), split_k=0, defer_reduce=defer_reduce,
         colsum=N.ptr(colsum))
-    N.check(L.dtc_gemm(args, N.stream_ptr(c.device)), "dtc_gemm")
+    return args
 
 
 def _check2d(t: torch.Tensor, name: str):
@@ -247,6 +252,59 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
     if db is not None:
         colsum(dy, db, beta)
     return dw
+
+
+_PAIR = __import__("os").environ.get("DTC_GEMM_PAIR", "1") == "1"  # A/B knob for the paired launch
+
+
+def linear_backward(dy: torch.Tensor, w: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0,
+                    red=None, db: Optional[torch.Tensor] = None, dgelu_u: Optional[torch.Tensor] = None,
+                    out_dtype=torch.float32, pair: bool = True) -> torch.Tensor:
+    """Both backward GEMMs of a Dense ``y = x·Wᵀ (+b)``: returns dX = dY·W (⊙ gelu'(u) when
+    ``dgelu_u`` is given — the fc2 dgrad fused with the GELU backward) and accumulates
+    dW = β·dW + dYᵀ·X (+ db = β·db + Σ_rows dY).
+
+    On the GPU with a batched reducer both GEMMs go out as ONE launch (``dtc_gemm_pair``: they
+    read the same dY, the weight gradient's blocks fill the CUs the dgrad's last wave leaves
+    idle, one dependent kernel boundary less); otherwise two calls."""
+    if N.library_path(dy) or red is None or not (_PAIR and pair):
+        dx = matmul_nn_dgelu(dy, w, dgelu_u) if dgelu_u is not None else matmul_nn(dy, w, out_dtype=out_dtype)
+        wgrad(dy, x, dw, beta, red=red, db=db)
+        return dx
+    _check2d(dy, "dy"); _check2d(w, "w"); _check2d(x, "x")
+    assert dw.dtype == torch.float32 and dw.is_contiguous()
+    L = N.lib()
+    M, Nn = dy.shape
+    K = w.shape[1]
+    Kx = x.shape[1]
+    assert w.shape[0] == Nn and x.shape[0] == M and tuple(dw.shape) == (Nn, Kx)
+    if dgelu_u is not None:
+        dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+        a1 = _gemm_args(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), dx, K, epi=N.EPI_DGELU, aux=dgelu_u, ldaux=K)
+    else:
+        dx = torch.empty(M, K, dtype=out_dtype, device=dy.device)
+        a1 = _gemm_args(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), dx, K)
+    split = int(L.dtc_gemm_wgrad_split(Nn, Kx, M))
+    fuse_cs = db is not None and bool(L.dtc_gemm_wgrad_fuses_colsum(Nn, Kx, M))
+    mark = red.off
+    cs = red.alloc(split * Nn) if fuse_cs else None
+    slab = red.alloc(split * Nn * Kx) if split > 1 else None
+    a2 = _gemm_args(2, Nn, Kx, M, dy, dy.stride(0), x, x.stride(0), dw, Kx, beta=beta, workspace=slab,
+                    defer_reduce=1 if split > 1 else 0, colsum=cs)
+    rc = L.dtc_gemm_pair(a1, a2, N.stream_ptr(dy.device))
+    if rc == 1100:  # not pairable (tile plans): two launches
+        red.off = mark
+        N.check(L.dtc_gemm(a1, N.stream_ptr(dy.device)), "dtc_gemm")
+        wgrad(dy, x, dw, beta, red=red, db=db)
+        return dx
+    N.check(rc, "dtc_gemm_pair")
+    if slab is not None:
+        red.add_wide(slab, dw, split, beta)
+    if cs is not None:
+        red.add_wide(cs, db, split, beta)
+    elif db is not None:
+        colsum(dy, db, beta, red=red)
+    return dx
 
 
 def colsum(dy: torch.Tensor, db: torch.Tensor, beta: float = 0.0, red=None) -> torch.Tensor:

@@ -312,3 +312,30 @@ def test_host_sort_keys_match_device(cuda):
     dev = E.embed_sort_keys(ids.to(cuda), 50258)
     host = E.embed_sort_keys_host(ids.numpy())
     assert np.array_equal(dev.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("M,Nout,Kin,mode", [(4096, 512, 2048, "dgelu"), (4096, 2048, 512, "f32"),
+                                              (4096, 512, 512, "bf16"), (4096, 1536, 512, "f32"),
+                                              (512, 384, 256, "f32")])
+def test_linear_backward_pair(cuda, M, Nout, Kin, mode):
+    """G.linear_backward (dgrad + weight gradient [+ bias gradient] in one paired launch) equals the
+    two separate GEMMs bitwise (same tile programs, same summation orders)."""
+    from distributed_training_compare_jax_amd.ops.reduce import GradReducer
+
+    red = GradReducer(cuda, arena_mb=128)
+    dy, w, x = _r(M, Nout, seed=41), _r(Nout, Kin, scale=0.05, seed=42), _r(M, Kin, seed=43)
+    u = _r(M, Kin, seed=44) if mode == "dgelu" else None
+    od = torch.bfloat16 if mode == "bf16" else torch.float32
+    for beta in (0.0, 1.0):
+        dw_a, db_a = _r(Nout, Kin, dtype=torch.float32, seed=45), _r(Nout, dtype=torch.float32, seed=46)
+        dw_b, db_b = dw_a.clone(), db_a.clone()
+        dx_b = G.linear_backward(dy, w, x, dw_b, beta, red=red, db=db_b, dgelu_u=u, out_dtype=od)
+        red.flush()
+        dx_a = G.matmul_nn_dgelu(dy, w, u) if u is not None else G.matmul_nn(dy, w, out_dtype=od)
+        G.wgrad(dy, x, dw_a, beta, red=red, db=db_a)
+        red.flush()
+        assert torch.equal(dx_a, dx_b), "dgrad"
+        assert torch.equal(dw_a, dw_b), "wgrad"
+        assert torch.equal(db_a, db_b), "bias grad"
+    ref = dy.float().t() @ x.float()  # last iteration: beta = 1 onto the seed-45 tensor
+    _close(dw_b, _r(Nout, Kin, dtype=torch.float32, seed=45) + ref, 2e-3, "wgrad vs fp32")
