@@ -23,7 +23,8 @@ _LIB = None
 _LOCK = threading.Lock()
 LIB_NAME = "_dtc_kernels.so"
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+# DTC_KERNEL_LIB: alternative build of the same library (A/B of compile-time kernel variants)
+LIB_PATH = os.environ.get("DTC_KERNEL_LIB") or os.path.join(PKG_DIR, LIB_NAME)
 
 c_int = ctypes.c_int
 c_long = ctypes.c_long
