@@ -69,7 +69,7 @@ class GradReducer:
         """fp32 scratch for one task's partials (valid until the next flush)."""
         nbytes = (int(nfloats) * 4 + 255) // 256 * 256
         if self.arena is None or self.off + nbytes > self.arena.numel():
-            if torch.cuda.is_current_stream_capturing():
+            if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("GradReducer arena exhausted during graph capture (raise arena_mb)")
             if self.arena is not None and self.off > 0:
                 raise RuntimeError(f"GradReducer window needs more than {self.arena.numel() >> 20} MB (raise arena_mb)")
