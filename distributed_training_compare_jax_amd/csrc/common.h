@@ -95,6 +95,13 @@ __device__ __forceinline__ float gelu_tanh_f(float u) {
   float t = fast_tanh(k0 * (u + k1 * u * u * u));
   return 0.5f * u * (1.f + t);
 }
+// gelu(u) and gelu'(u) sharing one tanh (the fc1 epilogue stores gelu'(u) for the backward)
+__device__ __forceinline__ void gelu_tanh_and_grad_f(float u, float& gv, float& dgv) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float t = fast_tanh(k0 * (u + k1 * u * u * u));
+  gv = 0.5f * u * (1.f + t);
+  dgv = 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
+}
 __device__ __forceinline__ float gelu_tanh_grad_f(float u) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float t = fast_tanh(k0 * (u + k1 * u * u * u));

@@ -158,10 +158,10 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
     if (full) { f32x4 rr = *(const f32x4*)res; for (int r = 0; r < 4; ++r) o[r] += rr[r]; }
     else { for (int r = 0; r < 4; ++r) if (n + r < e.N) o[r] += res[r]; }
   }
-  if (EPI == EPI_DGELU) {
+  if (EPI == EPI_DGELU) {  // aux = gelu'(u), stored by the forward's EPI_GELU epilogue
     const bf16* u = (const bf16*)e.aux + (long)m * e.ldaux + n;
-    if (full) { bf16x4 uu = *(const bf16x4*)u; for (int r = 0; r < 4; ++r) o[r] *= gelu_tanh_grad_f((float)uu[r]); }
-    else { for (int r = 0; r < 4; ++r) if (n + r < e.N) o[r] *= gelu_tanh_grad_f((float)u[r]); }
+    if (full) { bf16x4 uu = *(const bf16x4*)u; for (int r = 0; r < 4; ++r) o[r] *= (float)uu[r]; }
+    else { for (int r = 0; r < 4; ++r) if (n + r < e.N) o[r] *= (float)u[r]; }
   }
   if (EPI == EPI_STORE && OUTF32 && e.beta != 0.f) {
     const float* c = (const float*)e.C + (long)m * e.ldc + n;
@@ -173,12 +173,21 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
     else for (int r = 0; r < 4; ++r) if (n + r < e.N) c[r] = o[r];
   } else {
     bf16* c = (bf16*)e.C + (long)m * e.ldc + n;
+    bf16x4 gb;
+    if (EPI == EPI_GELU) {  // C = gelu'(u) (the backward's dGELU factor), aux_out = gelu(u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float gv, dgv;
+        gelu_tanh_and_grad_f(o[r], gv, dgv);
+        o[r] = dgv;
+        gb[r] = f2bf(gv);
+      }
+    }
     bf16x4 ob = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
     if (full) *(bf16x4*)c = ob;
     else for (int r = 0; r < 4; ++r) if (n + r < e.N) c[r] = ob[r];
     if (EPI == EPI_GELU) {
       bf16* g = (bf16*)e.aux_out + (long)m * e.ldc + n;
-      bf16x4 gb = {f2bf(gelu_tanh_f(o[0])), f2bf(gelu_tanh_f(o[1])), f2bf(gelu_tanh_f(o[2])), f2bf(gelu_tanh_f(o[3]))};
       if (full) *(bf16x4*)g = gb;
       else for (int r = 0; r < 4; ++r) if (n + r < e.N) g[r] = gb[r];
     }
@@ -489,8 +498,12 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = e.alpha * acc[i][j][r] + bb[i][r];
-            if constexpr (EPI == EPI_GELU) { if (pass == 1) v = gelu_tanh_f(v); }
-            if constexpr (EPI == EPI_DGELU) v *= gelu_tanh_grad_f((float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r]);
+            if constexpr (EPI == EPI_GELU) {  // pass 0: C = gelu'(u), pass 1: aux_out = gelu(u)
+              float gv, dgv;
+              gelu_tanh_and_grad_f(v, gv, dgv);
+              v = pass == 1 ? gv : dgv;
+            }
+            if constexpr (EPI == EPI_DGELU) v *= (float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r];
             ob[r] = f2bf(v);
           }
           stage_put(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);

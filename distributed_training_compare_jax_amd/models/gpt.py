@@ -207,7 +207,7 @@ class GPTStage:
         x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
         tp.all_reduce_(x2)
         y2, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
-        u, gact = G.linear_gelu(y2, f.w(p + "fc1.w"), f.p(p + "fc1.b"))
+        u, gact = G.linear_gelu(y2, f.w(p + "fc1.w"), f.p(p + "fc1.b"))  # u = gelu'(pre-activation)
         x3 = G.linear_resid(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b") if lead else None, x2 if lead else None)
         tp.all_reduce_(x3)
         ctx[l] = (x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch)

@@ -60,8 +60,8 @@ class GemmArgs(ctypes.Structure):
 
 EPI_STORE = 0       # C = alpha*acc (+bias) (+beta*C if fp32)
 EPI_RESID = 1       # C(f32) = aux(f32) + acc + bias
-EPI_GELU = 2        # C(bf16) = u = acc+bias ; aux_out(bf16) = gelu_tanh(u)
-EPI_DGELU = 3       # C(bf16) = acc * gelu_tanh'(aux)
+EPI_GELU = 2        # u = acc+bias: C(bf16) = gelu_tanh'(u) ; aux_out(bf16) = gelu_tanh(u)
+EPI_DGELU = 3       # C(bf16) = acc * aux   (aux = gelu_tanh'(u) from EPI_GELU)
 EPI_LMHEAD = 4      # C(bf16) = acc+bias, pad cols -inf; per-row partial (max,sumexp); label logit
 
 

@@ -8,9 +8,10 @@ in ``csrc/gemm.hip`` (bf16 in, fp32 accumulate) with fused epilogues:
 
 * ``linear``         y = x·Wᵀ + b                       (bf16 out)
 * ``linear_resid``   x_out = resid + x·Wᵀ + b           (fp32 residual stream)
-* ``linear_gelu``    u = x·Wᵀ + b ; g = gelu_tanh(u)     (fc1 + ``nn.gelu``, MLP.py:14)
+* ``linear_gelu``    u = x·Wᵀ + b → (gelu_tanh'(u), gelu_tanh(u))  (fc1 + ``nn.gelu``, MLP.py:14;
+  the derivative is what the backward needs, computed here from the shared tanh)
 * ``matmul_nn``      dX = dY·W                           (dgrad, fp32 out)
-* ``matmul_nn_dgelu`` dU = (dY·W) ⊙ gelu'(u)             (fc2 dgrad fused with GELU bwd)
+* ``matmul_nn_dgelu`` dU = (dY·W) ⊙ d,  d = gelu'(u)      (fc2 dgrad fused with GELU bwd)
 * ``wgrad``          dW = β·dW + dYᵀ·X                    (fp32, written straight into the flat grad buffer)
 * ``colsum``         db = β·db + Σ_rows dY                (bias grads)
 
@@ -167,14 +168,15 @@ def linear_resid(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
 
 
 def linear_gelu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]):
-    """Returns ``(u, g)``: pre-activation and ``gelu_tanh(u)`` (both activation dtype)."""
+    """Returns ``(d, g)`` for ``u = x·Wᵀ + b``: ``d = gelu_tanh'(u)`` (the dGELU factor the fc2 dgrad
+    multiplies by: the backward needs no transcendental) and ``g = gelu_tanh(u)`` (activation dtype)."""
     M, K = x.shape
     Nn = w.shape[0]
     if N.library_path(x):
         u = _f32(x) @ _f32(w).t()
         if bias is not None:
             u = u + bias.float()
-        return u.to(x.dtype), gelu_tanh(u).to(x.dtype)
+        return gelu_tanh_grad(u).to(x.dtype), gelu_tanh(u).to(x.dtype)
     _check2d(x, "x"); _check2d(w, "w")
     u = torch.empty(M, Nn, dtype=torch.bfloat16, device=x.device)
     g = torch.empty_like(u)
@@ -197,11 +199,12 @@ def matmul_nn(dy: torch.Tensor, w: torch.Tensor, out_dtype=torch.float32) -> tor
 
 
 def matmul_nn_dgelu(dy: torch.Tensor, w: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
-    """dU = (dY·W) ⊙ gelu_tanh'(u)   (fc2 dgrad fused with the GELU backward)."""
+    """dU = (dY·W) ⊙ u  with ``u = gelu_tanh'(pre-activation)`` from :func:`linear_gelu`
+    (fc2 dgrad fused with the GELU backward)."""
     M, Nn = dy.shape
     K = w.shape[1]
     if N.library_path(dy):
-        return ((_f32(dy) @ _f32(w)) * gelu_tanh_grad(_f32(u))).to(u.dtype)
+        return ((_f32(dy) @ _f32(w)) * _f32(u)).to(u.dtype)
     _check2d(dy, "dy"); _check2d(w, "w")
     du = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
     _gemm_native(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), du, K, epi=N.EPI_DGELU, aux=u, ldaux=K)
