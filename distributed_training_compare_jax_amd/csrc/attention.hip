@@ -565,6 +565,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_res_body(
   bf16* sQ = lds;
   bf16* sD = lds + Tp * L::VLD;
   float* sDel = (float*)(sD + Tp * L::VLD);
+  float* sLse = sDel + Tp;  // lse (log2 units) of every query row: read per tile from LDS, not L2
   const long ts = 3L * H * HD, dts = (long)H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
   const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
@@ -573,6 +574,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_res_body(
   const float* lseb = lse + ((long)b * H + h) * T;
   stage_rows<L::VLD, HD, RES_MAXT + 64>(sQ, Qb, ts, T, Tp, tid);
   stage_dout_delta<L::VLD, RES_MAXT + 64>(sD, sDel, dOb, o + (long)b * T * dts + h * HD, dts, T, Tp, tid);
+  for (int r = tid; r < Tp; r += RES_THREADS) sLse[r] = r < T ? lseb[r] * LOG2E : 0.f;
   __syncthreads();
   const int kg = 2 * w + half;
   if (kg * 16 >= T) return;
@@ -603,12 +605,12 @@ __device__ __forceinline__ void attn_bwd_dkdv_res_body(
       const int qr = q0 + qt * 16 + 4 * g;
       // T % 4 == 0 (use_resident): a 4-row group is entirely in or out of range -> selects, no branch
       const int qc = min(qr, T - 4);
-      f32x4 l4 = *(const f32x4*)(lseb + qc), d4 = *(const f32x4*)(sDel + qc);
+      f32x4 l4 = *(const f32x4*)(sLse + qc), d4 = *(const f32x4*)(sDel + qc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qr + r;
         const bool ok = diag ? (key <= qq && qq < T) : (qq < T);
-        const float pv = ok ? fast_exp2(sc[r] * c - l4[r] * LOG2E) : 0.f;
+        const float pv = ok ? fast_exp2(sc[r] * c - l4[r]) : 0.f;  // sLse holds lse * log2(e)
         p[qt][r] = pv;
         ds[qt][r] = pv * (dp[r] - d4[r]);
       }
@@ -741,7 +743,7 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
 
 // LDS bytes of the resident kernels; 0 if the sequence does not fit (then the tiled kernels run)
 inline long res_lds_fwd(int T, int HD) { const long Tp = (T + 63) / 64 * 64; return Tp * (AttnLds<32>::KLD + HD + 16) * 2; }
-inline long res_lds_dkdv(int T, int HD) { const long Tp = (T + 63) / 64 * 64 + 64; return 2 * Tp * (HD + 16) * 2 + Tp * 4; }
+inline long res_lds_dkdv(int T, int HD) { const long Tp = (T + 63) / 64 * 64 + 64; return 2 * Tp * (HD + 16) * 2 + Tp * 8; }
 inline long res_lds_dq(int T, int HD) { const long Tp = (T + 63) / 64 * 64; return 2 * Tp * (HD + 16) * 2; }
 constexpr long LDS_MAX = 160 * 1024;
 
