@@ -75,8 +75,15 @@ struct Tile {
         int row = c / (BK / 8), col = (c % (BK / 8)) * 8;
         int grp = col & ~31, a0 = (col & 31) >> 2;  // a0 even: segments a0, a0+1
         bf16* rp = lds + row * LD + grp;
-        *(u32x2*)(rp + 8 * (a0 & 3) + 4 * (a0 >> 2)) = u32x2{reg[i][0], reg[i][1]};
-        *(u32x2*)(rp + 8 * ((a0 + 1) & 3) + 4 * ((a0 + 1) >> 2)) = u32x2{reg[i][2], reg[i][3]};
+        // the a0 segments of every row fill one bank-pair set (mod 32) and the a0+1 segments the
+        // other, and a ds_write_b64 lane group spans two rows: odd rows store their segments in
+        // the opposite order, so each group of 16 lanes hits 16 distinct bank pairs (was 2-way)
+        bf16* p0 = rp + 8 * (a0 & 3) + 4 * (a0 >> 2);
+        bf16* p1 = rp + 8 * ((a0 + 1) & 3) + 4 * ((a0 + 1) >> 2);
+        const u32x2 v0 = u32x2{reg[i][0], reg[i][1]}, v1 = u32x2{reg[i][2], reg[i][3]};
+        const bool odd = row & 1;
+        *(u32x2*)(odd ? p1 : p0) = odd ? v1 : v0;
+        *(u32x2*)(odd ? p0 : p1) = odd ? v0 : v1;
       } else {
         int krow = c / (R / 8), col = (c % (R / 8)) * 8;
         *(u32x4*)(lds + krow * LD + col) = reg[i];
