@@ -432,6 +432,35 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
     TA::store(ra, s0, tid);
     TB::store(rb, s0 + TA::ELEMS, tid);
     if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra);
+#ifndef DTC_WRITE_AFTER_BARRIER
+#define DTC_WRITE_AFTER_BARRIER 1
+#endif
+    if constexpr (DTC_WRITE_AFTER_BARRIER) {
+      // write-after-barrier (guide T14 as G15 writes it): tile kt+1, loaded one iteration ago, is
+      // written at the top of iteration kt (its buffer was last read before the previous barrier)
+      // and tile kt+2's loads go out right behind it, so each load has a whole compute phase AND a
+      // barrier to land instead of the compute phase alone
+      if (nk > 1) {
+        TA::load(ra, rsA, lda, m0, kbeg + BK, tid);
+        TB::load(rb, rsB, ldb, n0, kbeg + BK, tid);
+      }
+      __syncthreads();
+      for (int kt = 0; kt < nk; ++kt) {
+        bf16* cur = (kt & 1) ? s1 : s0;
+        bf16* nxt = (kt & 1) ? s0 : s1;
+        if (kt + 1 < nk) {
+          TA::store(ra, nxt, tid);
+          TB::store(rb, nxt + TA::ELEMS, tid);
+          if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra);
+          if (kt + 2 < nk) {
+            TA::load(ra, rsA, lda, m0, kbeg + (kt + 2) * BK, tid);
+            TB::load(rb, rsB, ldb, n0, kbeg + (kt + 2) * BK, tid);
+          }
+        }
+        compute(cur);
+        __syncthreads();
+      }
+    } else {
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 1 < nk;
@@ -449,6 +478,7 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
       }
       __syncthreads();
     }
+    }  // DTC_WRITE_AFTER_BARRIER == 0: write-before-barrier
   }
   if constexpr (!AK) {
     // do_cs is block-uniform, so the combine's barrier is reached by every thread of the block;
@@ -974,7 +1004,13 @@ Plan make_plan(int M, int N, int K, int allow_split) {
     while (t128 * p.split < target && nk / (p.split * 2) >= 8) p.split *= 2;
     return p;
   }
-  if (t128 < 256) {
+  if (t128 >= 256) {
+    // DTC_BK128=32: 128^2 tiles with BK 32 (40 KB LDS instead of 80 -> up to 4 blocks per CU)
+    static const int bk128 = [] { const char* v = getenv("DTC_BK128"); return v ? atoi(v) : 64; }();
+    if (bk128 == 32) p.bk = 32;
+    return p;
+  }
+  {
     p.bm = p.bn = 64;
     const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
     if (allow_split == 1)
@@ -1055,7 +1091,7 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
       hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, 2, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A,
                          a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
                          (float*)a.workspace, e);
-  } else if (BM == 64 && p.bk == 32)
+  } else if (p.bk == 32)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A, a.lda,
                        ab, (const bf16*)a.B, a.ldb, bb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
                        (float*)a.workspace, e);
