@@ -407,6 +407,23 @@ __device__ __forceinline__ float group_sum(float x) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Block -> ((b, h), half) for the resident kernels.  Both halves of a (b, h) stage the SAME panels;
+// blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one), so the two halves are placed
+// 8 ids apart: the second one's panel loads hit the XCD's L2 instead of HBM (staging was ~5-6 us of
+// each phase, HBM-bound with every CU staging at once).  Needs B*H % 8 == 0, else the plain map.
+#ifndef DTC_ATTN_XCD_PAIR
+#define DTC_ATTN_XCD_PAIR 1
+#endif
+__device__ __forceinline__ void res_block_map(int bid, int nbh, int& half, int& bh) {
+  if (DTC_ATTN_XCD_PAIR && nbh % 8 == 0) {
+    half = (bid >> 3) & 1;
+    bh = ((bid >> 4) << 3) | (bid & 7);
+  } else {
+    half = bid & 1;
+    bh = bid >> 1;
+  }
+}
+
 // whole-sequence [T][HD] panel -> LDS [T][LD]: every load of the thread in flight before any store
 template <int LD, int HD, int MAXT>
 __device__ __forceinline__ void stage_rows(bf16* lds, const bf16* __restrict__ base, long tok_stride, int T, int Tp,
@@ -434,7 +451,9 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
-  const int half = blockIdx.x & 1, bh = blockIdx.x >> 1, b = bh / H, h = bh % H;
+  int half, bh;
+  res_block_map(blockIdx.x, B * H, half, bh);
+  const int b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64;
   bf16* sK = lds;
   bf16* sV = lds + Tp * L::KLD;
@@ -551,6 +570,16 @@ __device__ __forceinline__ void stage_dout_delta(bf16* lds, float* sDel, const b
   }
 }
 
+// Diagnostic build only (-DDTC_ATTN_STAMPS, scripts/attn_stamps.py): per-block wall-clock stamps
+// (s_memrealtime, 100 MHz) at entry, after the panel staging barrier, and at each wave's end.
+#ifdef DTC_ATTN_STAMPS
+constexpr int STAMP_SLOTS = 18;
+__device__ unsigned long long g_attn_stamps[4096 * STAMP_SLOTS];
+#define ATTN_STAMP(slot) (g_attn_stamps[(size_t)blockIdx.x * STAMP_SLOTS + (slot)] = __builtin_amdgcn_s_memrealtime())
+#else
+#define ATTN_STAMP(slot) ((void)0)
+#endif
+
 // dK, dV with Q and dO resident: wave owns 16 keys (key on the lane), walks queries >= its keys
 template <int HD>
 __device__ __forceinline__ void attn_bwd_dkdv_res_body(
@@ -560,7 +589,9 @@ __device__ __forceinline__ void attn_bwd_dkdv_res_body(
   using L = AttnLds<HD>;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
-  const int half = bid & 1, bh = bid >> 1, b = bh / H, h = bh % H;
+  int half, bh;
+  res_block_map(bid, B * H, half, bh);
+  const int b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64 + 64;  // + one tile of slack: query tiles start at 16-row offsets
   bf16* sQ = lds;
   bf16* sD = lds + Tp * L::VLD;
@@ -576,6 +607,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_res_body(
   stage_dout_delta<L::VLD, RES_MAXT + 64>(sD, sDel, dOb, o + (long)b * T * dts + h * HD, dts, T, Tp, tid);
   for (int r = tid; r < Tp; r += RES_THREADS) sLse[r] = r < T ? lseb[r] * LOG2E : 0.f;
   __syncthreads();
+  if (threadIdx.x == 0) ATTN_STAMP(1);
   const int kg = 2 * w + half;
   if (kg * 16 >= T) return;
   const int key = kg * 16 + j;
@@ -646,7 +678,9 @@ __device__ __forceinline__ void attn_bwd_dq_res_body(
   using L = AttnLds<HD>;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop bounds
-  const int half = bid & 1, bh = bid >> 1, b = bh / H, h = bh % H;
+  int half, bh;
+  res_block_map(bid, B * H, half, bh);
+  const int b = bh / H, h = bh % H;
   const int Tp = (T + 63) / 64 * 64;
   bf16* sK = lds;
   bf16* sV = lds + Tp * L::VLD;
@@ -658,6 +692,7 @@ __device__ __forceinline__ void attn_bwd_dq_res_body(
   stage_rows<L::VLD, HD, RES_MAXT>(sK, Kb, ts, T, Tp, tid);
   stage_rows<L::VLD, HD, RES_MAXT>(sV, Vb, ts, T, Tp, tid);
   __syncthreads();
+  if (threadIdx.x == 0) ATTN_STAMP(1);
   const int qg = 2 * w + half;
   if (qg * 16 >= T) return;
   const int q = qg * 16 + j;
@@ -721,8 +756,10 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_res_kernel(
     const float* __restrict__ lse, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int nkv = 2 * B * H;
+  if (threadIdx.x == 0) ATTN_STAMP(0);
   if ((int)blockIdx.x < nkv) attn_bwd_dkdv_res_body<HD>(lds, blockIdx.x, qkv, o, dout, lse, dqkv, B, T, H, scale);
   else attn_bwd_dq_res_body<HD>(lds, blockIdx.x - nkv, qkv, o, dout, lse, dqkv, B, T, H, scale);
+  if ((threadIdx.x & 63) == 0) ATTN_STAMP(2 + (threadIdx.x >> 6));
 }
 
 // split variant (DTC_ATTN_MERGED=0): the same bodies as two launches
@@ -761,6 +798,17 @@ void allow_lds(K kernel, long bytes) {  // > 64 KB of dynamic LDS must be opted 
 }  // namespace
 
 extern "C" {
+
+// copies the diagnostic stamps (DTC_ATTN_STAMPS builds only; returns 4003 otherwise)
+int dtc_attn_stamps(unsigned long long* host, long n) {
+#ifdef DTC_ATTN_STAMPS
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+#else
+  (void)host; (void)n;
+  return 4003;
+#endif
+}
 
 int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int HD, long flags, float scale,
                  hipStream_t st) {
