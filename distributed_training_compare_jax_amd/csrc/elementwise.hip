@@ -367,7 +367,10 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   const float clip = (max_norm > 0.f && !(norm < max_norm)) ? max_norm / norm : 1.f;
   const float t = (float)step[0];
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
-  f32x4 pp = *(f32x4*)(p + i), gg = *(const f32x4*)(g + i) * clip, mm = *(f32x4*)(m + i), vv = *(f32x4*)(v + i);
+  // once-touched stream (2.7 GB per step): non-temporal loads/stores keep it out of L2/MALL
+  // (measured 5.42 -> 5.345 ms/step)
+  f32x4 pp = __builtin_nontemporal_load((f32x4*)(p + i)), gg = __builtin_nontemporal_load((const f32x4*)(g + i)) * clip;
+  f32x4 mm = __builtin_nontemporal_load((f32x4*)(m + i)), vv = __builtin_nontemporal_load((f32x4*)(v + i));
   mm = b1 * mm + (1.f - b1) * gg;
   vv = b2 * vv + (1.f - b2) * gg * gg;
 #pragma unroll
@@ -375,9 +378,9 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     float mh = mm[r] / bc1, vh = vv[r] / bc2;
     pp[r] -= lr * (mh / (sqrtf(vh) + eps) + wd * pp[r]);
   }
-  *(f32x4*)(p + i) = pp;
-  *(f32x4*)(m + i) = mm;
-  *(f32x4*)(v + i) = vv;
+  __builtin_nontemporal_store(pp, (f32x4*)(p + i));
+  __builtin_nontemporal_store(mm, (f32x4*)(m + i));
+  __builtin_nontemporal_store(vv, (f32x4*)(v + i));
   if (i < n_mirror) *(bf16x4*)(mirror + i) = bf16x4{f2bf(pp[0]), f2bf(pp[1]), f2bf(pp[2]), f2bf(pp[3])};
 }
 
