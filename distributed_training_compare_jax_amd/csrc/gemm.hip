@@ -149,6 +149,15 @@ struct Epi {
   float* colsum;
 };
 
+// Output stores of the GEMM epilogues.  DTC_NT_STORES: non-temporal (streamed past L2), so a
+// kernel's outputs drain to memory while other blocks still compute instead of being written back
+// from L2 at the kernel boundary.
+#ifdef DTC_NT_STORES
+#define DTC_OUT_STORE(ptr, val) __builtin_nontemporal_store((val), (ptr))
+#else
+#define DTC_OUT_STORE(ptr, val) (*(ptr) = (val))
+#endif
+
 template <int EPI, bool OUTF32>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4 v) {
   const bool full = (n + 4 <= e.N);
@@ -176,7 +185,7 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
   }
   if (OUTF32) {
     float* c = (float*)e.C + (long)m * e.ldc + n;
-    if (full) *(f32x4*)c = f32x4{o[0], o[1], o[2], o[3]};
+    if (full) DTC_OUT_STORE((f32x4*)c, (f32x4{o[0], o[1], o[2], o[3]}));
     else for (int r = 0; r < 4; ++r) if (n + r < e.N) c[r] = o[r];
   } else {
     bf16* c = (bf16*)e.C + (long)m * e.ldc + n;
@@ -191,11 +200,11 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
       }
     }
     bf16x4 ob = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
-    if (full) *(bf16x4*)c = ob;
+    if (full) DTC_OUT_STORE((bf16x4*)c, ob);
     else for (int r = 0; r < 4; ++r) if (n + r < e.N) c[r] = ob[r];
     if (EPI == EPI_GELU) {
       bf16* g = (bf16*)e.aux_out + (long)m * e.ldc + n;
-      if (full) *(bf16x4*)g = gb;
+      if (full) DTC_OUT_STORE((bf16x4*)g, gb);
       else for (int r = 0; r < 4; ++r) if (n + r < e.N) g[r] = gb[r];
     }
   }
@@ -221,7 +230,7 @@ __device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int
     if (m >= M) continue;
     bf16* c = C + (long)m * ldc + n;
     if (n + 8 <= N) {
-      *(u32x4*)c = v;
+      DTC_OUT_STORE((u32x4*)c, v);
     } else {
       const bf16x8 b = __builtin_bit_cast(bf16x8, v);
       for (int r = 0; r < 8; ++r) if (n + r < N) c[r] = b[r];
@@ -508,6 +517,13 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
     EpiPre<TN, TM> pre;
     epi_prefetch<TN, TM>(e, m0 + wm * WM, n0 + wn * WN, lane, true, pre);
     lmhead_epilogue<TN, TM>(acc, e, m0 + wm * WM, n0 + wn * WN, tn_idx * 2 + wn, lane, pre);
+    return;
+  }
+  if constexpr (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
   if constexpr ((EPI == EPI_GELU || EPI == EPI_DGELU) && !OUTF32 && WN == 64) {
