@@ -386,6 +386,25 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
                                            : bf16x4{};
       }
   }
+  // bias of the LDS-staged epilogues, loaded before the main loop for the same reason
+#ifndef DTC_STAGE_STORE
+#define DTC_STAGE_STORE 1  // plain bf16 stores through the LDS stage too
+#endif
+  constexpr bool STAGED = (EPI == EPI_GELU || EPI == EPI_DGELU || (DTC_STAGE_STORE && EPI == EPI_STORE)) && !OUTF32 &&
+                          WN == 64;
+  f32x4 bpre[STAGED ? TN : 1];
+  if constexpr (STAGED) {
+    const int g4p = 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wn * WN + i * 16 + g4p;
+      bpre[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e.bias) {
+        if (n + 4 <= N) bpre[i] = *(const f32x4*)(e.bias + n);
+        else for (int r = 0; r < 4; ++r) if (n + r < N) bpre[i][r] = e.bias[n + r];
+      }
+    }
+  }
   // fused bias gradient (wgrad only: MN-major A = dY, first N-tile column of blocks)
   const bool do_cs = !AK && e.colsum != nullptr && tn_idx == 0;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -526,21 +545,12 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
       for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  if constexpr ((EPI == EPI_GELU || EPI == EPI_DGELU) && !OUTF32 && WN == 64) {
+  if constexpr (STAGED) {
     // bf16 outputs through a per-wave LDS stage so global stores leave as full 128-B rows (the
     // fragment layout writes 16 rows x 32 B per instruction); LDS is free after the last barrier
     bf16* stg = smem + wave * (WM * 64);
     const int mb = m0 + wm * WM, nb = n0 + wn * WN;
-    f32x4 bb[TN];
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int n = nb + i * 16 + g4;
-      bb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (e.bias) {
-        if (n + 4 <= N) bb[i] = *(const f32x4*)(e.bias + n);
-        else for (int r = 0; r < 4; ++r) if (n + r < N) bb[i][r] = e.bias[n + r];
-      }
-    }
+    const f32x4(&bb)[TN] = bpre;
 #pragma unroll
     for (int pass = 0; pass < (EPI == EPI_GELU ? 2 : 1); ++pass) {
 #pragma unroll
