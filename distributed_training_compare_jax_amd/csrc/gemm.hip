@@ -238,6 +238,62 @@ __device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int
   }
 }
 
+// fp32 per-wave stage [ROWS][COLS] (COLS = 32 or 64): 16-B chunk c of row r at c ^ (r % (COLS/4)),
+// conflict-free for the fragment writes (8 rows per lane group) and the row reads.  stage_out_f32
+// writes whole rows (128/256 B per row, 8/4 rows per instruction) and adds the fp32 residual
+// (`res`) or beta*C on the way out, in the same order as epilogue_store.
+template <int COLS>
+__device__ __forceinline__ void stage_put_f32(float* st, int row, int chunk, f32x4 v) {
+  constexpr int CPR = COLS / 4;
+  *(f32x4*)(st + row * COLS + ((chunk ^ (row & (CPR - 1))) << 2)) = v;
+}
+
+template <int ROWS, int COLS>
+__device__ __forceinline__ void stage_out_f32(const float* st, float* C, long ldc, int m_base, int n_base, int M, int N,
+                                              int lane, const float* res, long ldres, float beta) {
+  constexpr int CPR = COLS / 4, RPI = 64 / CPR;
+#pragma unroll 4
+  for (int it = 0; it < ROWS / RPI; ++it) {
+    const int row = it * RPI + lane / CPR, p = lane % CPR;
+    f32x4 v = *(const f32x4*)(st + row * COLS + ((p ^ (row & (CPR - 1))) << 2));
+    const int m = m_base + row, n = n_base + p * 4;
+    if (m >= M || n >= N) continue;
+    float* c = C + (long)m * ldc + n;
+    if (n + 4 <= N) {
+      if (res) v += *(const f32x4*)(res + (long)m * ldres + n);
+      if (beta != 0.f) v += beta * *(const f32x4*)c;
+      *(f32x4*)c = v;
+    } else {
+      for (int r = 0; r < 4; ++r)
+        if (n + r < N) {
+          float o = v[r];
+          if (res) o += res[(long)m * ldres + n + r];
+          if (beta != 0.f) o += beta * c[r];
+          c[r] = o;
+        }
+    }
+  }
+}
+
+// acc fragments (+ alpha/bias when `bias_on`) -> per-wave fp32 stage -> whole-row stores
+template <int TN, int TM, int WM, int WN>
+__device__ __forceinline__ void staged_f32_epilogue(const f32x4 (&acc)[TN][TM], float* stg, float* C, long ldc, int mb,
+                                                    int nb, int M, int N, int lane, bool bias_on, float alpha,
+                                                    const f32x4 (&bb)[TN], const float* res, long ldres, float beta) {
+#pragma unroll
+  for (int j = 0; j < TM; ++j)
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      f32x4 v = acc[i][j];
+      if (bias_on) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = alpha * v[r] + bb[i][r];
+      }
+      stage_put_f32<WN>(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), v);
+    }
+  stage_out_f32<WM, WN>(stg, C, ldc, mb, nb, M, N, lane, res, ldres, beta);
+}
+
 // lm_head epilogue: logits (bf16) + per-row partial (max, sum exp) over this wave's TN*16 columns +
 // the label logit.  acc[i][j]: lane holds C[m_base + 16j + (lane&15)][n_base + 16i + 4(lane>>4) + r].
 // Epilogue operands loaded up front (all loads in flight together, ideally before the main loop
@@ -392,8 +448,14 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
 #endif
   constexpr bool STAGED = (EPI == EPI_GELU || EPI == EPI_DGELU || (DTC_STAGE_STORE && EPI == EPI_STORE)) && !OUTF32 &&
                           WN == 64;
-  f32x4 bpre[STAGED ? TN : 1];
-  if constexpr (STAGED) {
+#ifndef DTC_STAGE_F32
+#define DTC_STAGE_F32 1  // fp32 outputs and split-K slabs through an fp32 LDS stage
+#endif
+  constexpr bool FIT32 = DTC_STAGE_F32 && (WN == 64 || WN == 32) &&
+                         4 * WM * WN * 4 <= gemm_smem_elems<BM, BN, BK, AK, BKM>() * 2;  // stage fits the LDS
+  constexpr bool STAGED32 = FIT32 && OUTF32 && (EPI == EPI_STORE || EPI == EPI_RESID);
+  f32x4 bpre[(STAGED || STAGED32) ? TN : 1];
+  if constexpr (STAGED || STAGED32) {
     const int g4p = 4 * (lane >> 4);
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
@@ -518,6 +580,13 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
   const int g4 = 4 * (lane >> 4);
   if (split > 1) {
     float* s = slab + (long)z * M * N;
+    if constexpr (FIT32) {
+      if (do_cs) __syncthreads();  // colsum_store's reads of LDS are done before it is reused
+      const f32x4 nob[TN] = {};
+      staged_f32_epilogue<TN, TM, WM, WN>(acc, (float*)smem + wave * (WM * WN), s, N, m0 + wm * WM, n0 + wn * WN, M, N,
+                                          lane, false, 1.f, nob, nullptr, 0, 0.f);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -530,6 +599,14 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
           else for (int r = 0; r < 4; ++r) if (n + r < N) c[r] = acc[i][j][r];
         }
       }
+    return;
+  }
+  if constexpr (STAGED32) {
+    if (do_cs) __syncthreads();
+    staged_f32_epilogue<TN, TM, WM, WN>(acc, (float*)smem + wave * (WM * WN), (float*)e.C, e.ldc, m0 + wm * WM,
+                                        n0 + wn * WN, M, N, lane, true, e.alpha, bpre,
+                                        EPI == EPI_RESID ? (const float*)e.aux : nullptr, e.ldaux,
+                                        EPI == EPI_STORE ? e.beta : 0.f);
     return;
   }
   if (EPI == EPI_LMHEAD) {
@@ -967,6 +1044,29 @@ gemm_dma_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B
   }
 
   const int g4 = 4 * (lane >> 4);
+  constexpr bool ST32 = DTC_STAGE_F32 && 4 * WM * WN * 4 <= NSTAGE * STAGE * 2;
+  if constexpr (ST32) {
+    if (split > 1 || (OUTF32 && (EPI == EPI_STORE || EPI == EPI_RESID))) {
+      raw_barrier();  // every wave's last fragment reads are done: the ring is free for the stage
+      const bool sp = split > 1;
+      f32x4 bb[TN];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + g4;
+        bb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!sp && e.bias) {
+          if (n + 4 <= N) bb[i] = *(const f32x4*)(e.bias + n);
+          else for (int r = 0; r < 4; ++r) if (n + r < N) bb[i][r] = e.bias[n + r];
+        }
+      }
+      staged_f32_epilogue<TN, TM, WM, WN>(acc, (float*)smem + wave * (WM * WN),
+                                          sp ? slab + (long)z * M * N : (float*)e.C, sp ? N : e.ldc, m0 + wm * WM,
+                                          n0 + wn * WN, M, N, lane, !sp, e.alpha, bb,
+                                          (!sp && EPI == EPI_RESID) ? (const float*)e.aux : nullptr, e.ldaux,
+                                          (!sp && EPI == EPI_STORE) ? e.beta : 0.f);
+      return;
+    }
+  }
   if (split > 1) {
     float* sl = slab + (long)z * M * N;
 #pragma unroll
