@@ -46,7 +46,8 @@ def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, la
     P = int(L.dtc_lmhead_nparts(M, Vl, D))
     logits = torch.empty(M, Vl, dtype=torch.bfloat16, device=h.device)
     part = torch.empty(P, M, 2, dtype=torch.float32, device=h.device)  # part-major (coalesced epilogue writes)
-    lab = torch.zeros(M, dtype=torch.float32, device=h.device)
+    # a single shard (combine=False) holds every row's label: the epilogue writes all of lab
+    lab = (torch.zeros if combine else torch.empty)(M, dtype=torch.float32, device=h.device)
     from .gemm import _gemm_native
 
     _gemm_native(0, M, Vl, D, h, h.stride(0), w, w.stride(0), logits, Vl, epi=N.EPI_LMHEAD, bias=b,

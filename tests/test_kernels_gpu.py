@@ -223,6 +223,23 @@ def test_lmhead_ce(cuda, M, D, V, Vp):
     assert logits[:, V:].abs().max().item() == 0.0
 
 
+def test_lmhead_raw_partials_match_combined(cuda):
+    """combine=False (one vocab shard: raw per-tile partials, a label logit written for every row,
+    no zero-fill) gives the same logits, label logits and loss as the combined row statistics."""
+    M, D, V, Vp = 2048, 256, 50258, 50304
+    h = _r(M, D, seed=27)
+    w = _r(Vp, D, scale=0.2, seed=28)
+    b = _r(Vp, dtype=torch.float32, seed=29)
+    labels = torch.randint(0, V, (M,), dtype=torch.int32).to(cuda)
+    lg1, rs, lab1 = X.lmhead_logits_partials(h, w, b, labels, 0, V)
+    lg2, part, lab2 = X.lmhead_logits_partials(h, w, b, labels, 0, V, combine=False)
+    assert torch.equal(lg1, lg2) and torch.equal(lab1, lab2)
+    lse1, loss1 = X.ce_finalize(rs.unsqueeze(0).contiguous(), lab1, 1.0 / M)
+    lse2, loss2 = X.ce_finalize(part, lab2, 1.0 / M)
+    torch.testing.assert_close(lse1, lse2, rtol=1e-5, atol=1e-5)
+    assert abs(loss1.item() - loss2.item()) < 1e-4 * abs(loss1.item())
+
+
 def test_adamw_matches_cpu(cuda):
     n = 10_000 * 64
     p = _r(n, dtype=torch.float32, seed=25)
