@@ -51,7 +51,11 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-constexpr int LN_BWD_ROWS = 8;  // rows per block (4 waves x 2 rows, processed together): 512 blocks at M=4096
+#ifndef DTC_LN_RPW
+#define DTC_LN_RPW 2  // rows per wave in the LayerNorm backward (all loaded before the first use)
+#endif
+constexpr int LN_RPW = DTC_LN_RPW;
+constexpr int LN_BWD_ROWS = 4 * LN_RPW;  // rows per block (4 waves): 512 blocks at M=4096 with 2 rows per wave
 
 // LayerNorm backward, 2 rows per wave with all loads issued before the two row reductions (ILP),
 // fused residual-gradient add, bf16 copy of dx, and per-block column partials of
@@ -68,9 +72,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
   f32x4 ag[NV], ab[NV], ao[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) { ag[i] = f32x4{0.f, 0.f, 0.f, 0.f}; ab[i] = ag[i]; ao[i] = ag[i]; }
-  const int r0 = blockIdx.x * LN_BWD_ROWS + wave * 2;
-  f32x4 xh[2][NV], d[2][NV], rv[2][NV], gv[NV];
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, rsv[2] = {0.f, 0.f};
+  const int r0 = blockIdx.x * LN_BWD_ROWS + wave * LN_RPW;
+  f32x4 xh[LN_RPW][NV], d[LN_RPW][NV], rv[LN_RPW][NV], gv[NV];
+  float s1[LN_RPW] = {}, s2[LN_RPW] = {}, rsv[LN_RPW] = {};
   // every global load of the block (x, dy, the residual gradient, gamma) is issued before the first
   // use: the residual-gradient read used to sit after the row reductions, fully exposed
 #pragma unroll
@@ -79,7 +83,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
     gv[i] = c < D4 ? ((const f32x4*)g)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < LN_RPW; ++q) {
     const int row = r0 + q;
     const bool ok = row < M;
     const float mu = ok ? mean[row] : 0.f;
@@ -100,7 +104,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
     }
   }
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < LN_RPW; ++q)
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
@@ -114,7 +118,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
       }
     }
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < LN_RPW; ++q) {
     const int row = r0 + q;
     const float c1 = warp_sum(s1[q]) / D, c2 = warp_sum(s2[q]) / D;
     if (row >= M) continue;
