@@ -692,12 +692,20 @@ struct GemmCfg {
 // Two independent GEMMs in ONE launch (a layer's dgrad and weight gradient read the same dY):
 // blocks [0, nb1) run problem 1, the rest problem 2.  Saves a dependent kernel boundary and lets
 // the second problem's blocks fill the CUs the first one's last wave leaves idle.  nb1 % 8 == 0
-// keeps both problems' XCD-aware tile maps (blockIdx % 8) intact.
+// keeps both problems' XCD-aware tile maps (blockIdx % 8) intact.  `second_first`: problem 2's
+// blocks take the low block ids instead (dispatched first), so the long split-K weight-gradient
+// blocks start in the first round and the short whole-K dgrad tiles back-fill behind them.
 template <class C1, class C2>
-__global__ void __launch_bounds__(NT, 2) gemm_pair_kernel(GemmLaunch g1, GemmLaunch g2) {
+__global__ void __launch_bounds__(NT, 2) gemm_pair_kernel(GemmLaunch g1, GemmLaunch g2, int second_first) {
   __shared__ __attribute__((aligned(16))) bf16 smem[C1::SMEM > C2::SMEM ? C1::SMEM : C2::SMEM];
-  if ((int)blockIdx.x < g1.nblocks) C1::run(smem, blockIdx.x, g1);
-  else C2::run(smem, blockIdx.x - g1.nblocks, g2);
+  const int b = blockIdx.x;
+  if (second_first) {
+    if (b < g2.nblocks) C2::run(smem, b, g2);
+    else C1::run(smem, b - g2.nblocks, g1);
+  } else {
+    if (b < g1.nblocks) C1::run(smem, b, g1);
+    else C2::run(smem, b - g1.nblocks, g2);
+  }
 }
 
 
@@ -1302,8 +1310,13 @@ template <class C1, class C2, int BM1, int BM2>
 int launch_pair_t(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const Plan& p2, hipStream_t st) {
   const GemmLaunch g1 = make_launch<BM1, BM1, true, false>(a1, p1);
   const GemmLaunch g2 = make_launch<BM2, BM2, false, false>(a2, p2);
-  if (g1.nblocks % 8) return 1100;  // XCD maps would disagree: not pairable
-  hipLaunchKernelGGL((gemm_pair_kernel<C1, C2>), dim3(g1.nblocks + g2.nblocks), dim3(NT), 0, st, g1, g2);
+  if (g1.nblocks % 8 && g2.nblocks % 8) return 1100;  // XCD maps would disagree: not pairable
+  // DTC_PAIR_WGRAD_FIRST=1: dispatch the weight-gradient blocks first (when their count keeps the XCD
+  // maps aligned).  Measured slower (interleaved A/B, min of 4: 5.348 vs 5.284 ms/step): off
+  static const int wf = [] { const char* v = getenv("DTC_PAIR_WGRAD_FIRST"); return v ? atoi(v) : 0; }();
+  const int second_first = (wf && g2.nblocks % 8 == 0) || g1.nblocks % 8 ? 1 : 0;
+  hipLaunchKernelGGL((gemm_pair_kernel<C1, C2>), dim3(g1.nblocks + g2.nblocks), dim3(NT), 0, st, g1, g2,
+                     second_first);
   DTC_CHECK_LAUNCH();
   return 0;
 }
