@@ -19,14 +19,18 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   if (row >= M) return;
   const int D4 = D / 4;
   const f32x4* xr = (const f32x4*)(x + (long)row * D);
-  f32x4 v[NV];
+  f32x4 v[NV], gv[NV], bv[NV];
   float s = 0.f;
+  // gamma/beta are issued with the row load so their latency hides under the two row reductions
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     int c = lane + 64 * i;
     v[i] = c < D4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    gv[i] = c < D4 ? ((const f32x4*)g)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    bv[i] = c < D4 ? ((const f32x4*)b)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   const float mean = warp_sum(s) / D;
   float q = 0.f;
 #pragma unroll
@@ -43,8 +47,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   for (int i = 0; i < NV; ++i) {
     int c = lane + 64 * i;
     if (c < D4) {
-      f32x4 gg = ((const f32x4*)g)[c], bb = ((const f32x4*)b)[c];
-      f32x4 o = (v[i] - mean) * rstd * gg + bb;
+      f32x4 o = (v[i] - mean) * rstd * gv[i] + bv[i];
       if (out_f32) ((f32x4*)((float*)y + (long)row * D))[c] = o;
       else ((bf16x4*)((bf16*)y + (long)row * D))[c] = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
     }
