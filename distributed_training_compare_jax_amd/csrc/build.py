@@ -4,6 +4,8 @@
 
 Each ``csrc/*.hip`` is compiled by ``hipcc --offload-arch=gfx950`` (cross-compiles without a
 GPU) and the objects are linked into one shared library with a C ABI (``ops/_native.py``).
+The host-only runtime sources (``csrc/*.cpp``: the native data pipeline) are compiled by the host
+C++ compiler into ``_dtc_host.so`` (no GPU code, loadable on CPU-only machines).
 Rebuilds only when a source/header hash changed.
 """
 
@@ -21,6 +23,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 OUT = os.path.join(PKG, "_dtc_kernels.so")
+HOST_OUT = os.path.join(PKG, "_dtc_host.so")
 BUILD = os.path.join(HERE, "build")
 ARCH = os.environ.get("DTC_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-Wno-unused-result"]
@@ -43,7 +46,30 @@ def _digest(paths) -> str:
     return h.hexdigest()
 
 
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """csrc/*.cpp -> _dtc_host.so (host C++ only)."""
+    srcs = sorted(glob.glob(os.path.join(HERE, "*.cpp")))
+    os.makedirs(BUILD, exist_ok=True)
+    stamp = os.path.join(BUILD, "stamp_host")
+    dig = _digest(srcs)
+    if not force and os.path.exists(HOST_OUT) and os.path.exists(stamp) and open(stamp).read() == dig:
+        return HOST_OUT
+    cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++") or "/opt/rocm/llvm/bin/clang++"
+    tmp = HOST_OUT + ".tmp"
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-o", tmp, *srcs]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host build failed:\n{r.stderr[-6000:]}")
+    os.replace(tmp, HOST_OUT)
+    with open(stamp, "w") as f:
+        f.write(dig)
+    return HOST_OUT
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    build_host(force, verbose)
     srcs = sorted(glob.glob(os.path.join(HERE, "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(HERE, "*.h")))
     os.makedirs(BUILD, exist_ok=True)

@@ -42,3 +42,25 @@ def test_profile_writes_trace_and_metrics(tmp_path):
     assert {"data", "loss sync", "step 1", "step 3"} <= names
     m = json.load(open(os.path.join(tmp_path, "metrics.json")))
     assert m["trace"].endswith("rank0.json")
+
+
+def test_native_data_sampler_matches_numpy():
+    """The C++ sampler (csrc/host_data.cpp -> _dtc_host.so) yields the numpy stream bit for bit,
+    at offsets/lengths crossing row boundaries, both vocabularies and a position past 2^40."""
+    import numpy as np
+
+    from distributed_training_compare_jax_amd.csrc.build import build_host
+    from distributed_training_compare_jax_amd.data import synthetic as S
+
+    build_host()
+    S._host = None  # re-probe now that the library exists
+    for vocab, seed in ((S.BPE_VOCAB, 0), (999, 7)):
+        s = S.SyntheticTokenStream(vocab=vocab, seed=seed, native=True)
+        for start, count in ((0, 1), (0, 4104), (1, 513), (98765, 20000), (1 << 41, 3000)):
+            a, b = s.tokens(start, count), s.tokens_numpy(start, count)
+            assert a.dtype == np.int32 and np.array_equal(a, b), (vocab, seed, start, count)
+    # the iterator (what bench.py / main.py consume) is unchanged by the native path
+    it_n = S.get_batch_iterator(4, 513, seed=1, row0=1, nrows=2)
+    ref = S.SyntheticTokenStream(seed=1, native=False)
+    for step in range(3):
+        assert np.array_equal(next(it_n), ref.rows(step, 1, 2, 4, 513))
