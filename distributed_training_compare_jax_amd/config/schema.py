@@ -25,7 +25,8 @@ are optional and default to the reference behaviour:
   peer-to-peer kernels, ``parallel/p2p.py``; ``auto`` = p2p on a GPU RCCL group),
   ``defer_optimizer`` / ``defer_groups`` (run the non-embedding AdamW under the next step's
   forward in that many layer groups; exact, off by default: measured neutral at the
-  reference size because the forward kernels slow down under the AdamW's HBM traffic).
+  reference size because the forward kernels slow down under the AdamW's HBM traffic),
+  ``zero_stage`` (1 = ZeRO-1 Adam-state sharding over the DP group, ``ShardedAdamW``; pure DP only).
 """
 
 from __future__ import annotations
@@ -119,6 +120,7 @@ class TrainConfig:
     dp_bucket_mb: float = 64.0
     dp_tail_mb: float = 16.0
     dp_embed_gather: bool = True
+    zero_stage: int = 0  # 1 = ZeRO-1: Adam state sharded over the DP group (train/optimizer.py)
     warmup_steps: int = 5
     ckpt_every: int = 0
     resume: bool = False

@@ -28,7 +28,7 @@ from ..parallel.dp import GradBuckets
 from ..parallel.mesh import Mesh, build_mesh, resolve_degrees, split_layers
 from ..parallel.program import StepProgram
 from ..parallel.tp import TPComm
-from .optimizer import FusedAdamW
+from .optimizer import FusedAdamW, ShardedAdamW
 
 
 class Engine:
@@ -80,14 +80,21 @@ class Engine:
         # (103 MB fp32 for the reference vocab, issued last -> fully exposed), all-gather the
         # embedding-output grads (b_local*T*D fp32 per rank) and let every rank rebuild the
         # identical wte/wpe grads from the global batch with the deterministic sorted kernel.
-        self.embed_gather = bool(dp > 1 and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed)
+        self.zero = bool(train_cfg.zero_stage >= 1 and dp > 1)
+        if self.zero and (tp > 1 or pp > 1):
+            raise ValueError("zero_stage=1 is implemented for pure data parallelism (tp = pp = 1)")
+        self.embed_gather = bool(dp > 1 and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed
+                                 and not self.zero)
         self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb,
                                    tail_mb=train_cfg.dp_tail_mb,
                                    local_names=("wte", "wpe") if self.embed_gather else ())
-        self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,
-                              pp_global_clip=(train_cfg.pp_clip == "global"))
+        if self.zero:
+            self.opt = ShardedAdamW(self.flat, opt_cfg, self.program, m.dp_group, dp, m.dp_idx)
+        else:
+            self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,
+                                  pp_global_clip=(train_cfg.pp_clip == "global"))
         self.opt.reducer = self.stage.red
-        if pp == 1:
+        if pp == 1 and not self.zero:
             # incremental Σg²: with dp == 1 each layer's grads are final when its backward ends
             # (norm chunk per layer, reduced on the side stream); with dp > 1 only the locally
             # built embedding grads are final before the all-reduces finish
@@ -141,7 +148,7 @@ class Engine:
         # traffic) then overlaps the compute-bound forward instead of idling the MFMAs at the
         # end of the step.  Semantics are unchanged (same norm, same update, before each use);
         # :meth:`flush_optimizer` completes a pending update (checkpoint, end of run, bench).
-        self.defer_opt = bool(on_gpu and pp == 1 and train_cfg.defer_optimizer and self.stage.side.stream is not None)
+        self.defer_opt = bool(on_gpu and pp == 1 and not self.zero and train_cfg.defer_optimizer and self.stage.side.stream is not None)
         if self.defer_opt:
             # device-side "an update is pending" switch: the graph always contains the deferred
             # launch, the kernels skip when nothing is pending (first step, after a flush)
@@ -270,6 +277,8 @@ class Engine:
                     return
                 nxt = l + 1
                 bk.ready_upto(bk.layer_end_offset(nxt) if nxt in layers else bk.head_end_offset())
+        if self.zero:
+            hook = None  # grads are reduce-scattered in one call by ShardedAdamW.step
         dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=hook)
         if self.embed_gather:
             out, g = self.dh_all, self.mesh.dp_group
@@ -280,8 +289,9 @@ class Engine:
         else:
             st.embed_backward(ctx, dx, step, 0.0)
         st.side.join()
-        bk.ready_all()
-        bk.wait_all()
+        if not self.zero:
+            bk.ready_all()
+            bk.wait_all()
         self._loss_allreduce()
         self._finish_optimizer()
         return self.loss

@@ -148,3 +148,80 @@ class FusedAdamW:
 
     def grad_norm(self) -> float:
         return float(self.sumsq.item()) ** 0.5
+
+
+class ShardedAdamW:
+    """ZeRO-1 over the data-parallel group: each DP rank owns 1/dp of the Adam state.
+
+    Not in the reference (SURVEY §2.2 lists ZeRO/FSDP as absent and optional; the reference
+    replicates the optax state on every device, ``train.py:44-52``).  Step:
+
+    1. one in-place ``reduce_scatter`` of the flat grad buffer over the DP group (same bytes on
+       the xGMI ring as half an all-reduce): rank r ends with the summed grads of its slice
+       ``[r·S, (r+1)·S)``; the small remainder ``[dp·S, numel)`` is all-reduced and owned by all;
+    2. Σg² of the owned slice (+ the shared tail weighted 1/dp), one scalar all-reduce → the
+       global clip norm, exactly the replicated optimizer's;
+    3. fused clip+AdamW (the same HIP kernel) on the owned slice with shard-sized m/v;
+    4. one in-place ``all_gather`` of the updated params, then the bf16 compute mirror is rebuilt.
+
+    Adam m/v shrink from 8·numel to 8·(numel/dp) bytes per rank.  ``flat.exp_avg``/``exp_avg_sq``
+    are replaced by the shard buffers, so checkpoints hold each rank's shard (resume at the
+    same dp)."""
+
+    def __init__(self, flat: FlatParams, cfg: OptimConfig, program, dp_group, dp: int, dp_idx: int):
+        self.flat, self.cfg, self.program = flat, cfg, program
+        self.group, self.dp, self.rank = dp_group, dp, dp_idx
+        align = 64
+        self.S = (flat.numel // dp) // align * align
+        self.lo, self.hi = dp_idx * self.S, (dp_idx + 1) * self.S
+        self.n_rs = dp * self.S  # [0, n_rs) reduce-scattered, [n_rs, numel) all-reduced
+        self.n_tail = flat.numel - self.n_rs
+        dev = flat.device
+        n_own = self.S + self.n_tail
+        flat.exp_avg = torch.zeros(n_own, dtype=torch.float32, device=dev)
+        flat.exp_avg_sq = torch.zeros(n_own, dtype=torch.float32, device=dev)
+        segs = [(self.lo, self.S, 1.0)] if self.S else []
+        if self.n_tail:
+            segs.append((self.n_rs, self.n_tail, 1.0 / dp))
+        self.segments = O.make_segments(segs, dev)
+        self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.reducer = None
+        # gloo on device tensors (the 2-ranks-on-one-GPU test rig) lacks the in-place tensor
+        # collectives: emulate them with all_reduce / list all_gather (same results)
+        self._emulate = dev.type == "cuda" and dist.get_backend(dp_group) == "gloo"
+
+    def _adamw(self, lo: int, hi: int, mlo: int):
+        f, c = self.flat, self.cfg
+        if hi <= lo:
+            return
+        O.adamw_flat(f.params[lo:hi], f.grads[lo:hi], f.exp_avg[mlo:mlo + hi - lo], f.exp_avg_sq[mlo:mlo + hi - lo],
+                     None, 0, self.step_t, self.sumsq, c.lr, c.b1, c.b2, c.eps, c.weight_decay, c.grad_clip)
+
+    def step(self):
+        if self.reducer is not None:
+            self.reducer.flush_all()  # grads must be final
+        f, grp = self.flat, self.group
+        g, p = f.grads, f.params
+        lo, hi, n = self.lo, self.hi, self.n_rs
+        if n and self._emulate:
+            self.program.comm(lambda: dist.all_reduce(g[:n], group=grp))
+        elif n:
+            self.program.comm(lambda: dist.reduce_scatter_tensor(g[lo:hi], g[:n], group=grp))
+        if self.n_tail:
+            self.program.comm(lambda: dist.all_reduce(g[n:], group=grp))
+        O.sumsq_segments(g, self.segments, self.sumsq, step=self.step_t)
+        s = self.sumsq
+        self.program.comm(lambda: dist.all_reduce(s, group=grp))
+        self._adamw(lo, hi, 0)
+        self._adamw(n, f.numel, self.S)
+        if n and self._emulate:
+            S = self.S
+            self.program.comm(lambda: dist.all_gather([p[i * S:(i + 1) * S] for i in range(self.dp)],
+                                                      p[lo:hi].clone(), group=grp))
+        elif n:
+            self.program.comm(lambda: dist.all_gather_into_tensor(p[:n], p[lo:hi], group=grp))
+        f.refresh_mirror()
+
+    def grad_norm(self) -> float:
+        return float(self.sumsq.item()) ** 0.5

@@ -52,6 +52,7 @@ def single(cuda):
 @pytest.mark.parametrize("parallel,kw", [
     ("dp", {}),
     ("dp", {"dp_embed_gather": False}),
+    ("dp", {"zero_stage": 1}),
     ("tp", {}),
     ("tp", {"tp_comm": "p2p"}),
     ("pp", {"pp_microbatches": 2, "pp_clip": "global"}),

@@ -77,6 +77,8 @@ def single():
 @pytest.mark.slow
 @pytest.mark.parametrize("parallel,world,kw", [
     ("dp", 2, {}),
+    ("dp", 2, {"zero_stage": 1}),
+    ("dp", 4, {"zero_stage": 1}),
     ("tp", 2, {}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global"}),
     ("pp", 2, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
@@ -105,3 +107,11 @@ def test_pp_local_clip_is_reference_semantics(single):
     res = _run("pp", 2, pp_microbatches=2, pp_clip="local")
     assert res[0]["losses"][0] == pytest.approx(single[0]["losses"][0], rel=1e-5)
     assert res[0]["losses"] == pytest.approx(single[0]["losses"], rel=2e-2)
+
+
+@pytest.mark.slow
+def test_zero1_replicas_identical():
+    """ZeRO-1: after the all-gather every DP replica holds the same params (bit-identical)."""
+    res = _run("dp", 2, zero_stage=1)
+    for n in res[0]["params"]:
+        assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n
