@@ -35,7 +35,8 @@ def save(eng, output_dir: str, step: int):
     slots = {n: dict(offset=s.offset, shape=list(s.shape), tp=s.spec.tp, full=list(s.spec.shape))
              for n, s in f.slots.items()}
     meta = dict(step=step, dp=m.dp, tp=m.tp, pp=m.pp, rank=m.rank, dp_idx=m.dp_idx, tp_idx=m.tp_idx,
-                pp_idx=m.pp_idx, slots=slots, model=eng.mcfg.name)
+                pp_idx=m.pp_idx, slots=slots, model=eng.mcfg.name,
+                zero_stage=int(getattr(eng, "zero", False)))
     with open(os.path.join(d, f"meta_rank{m.rank}.json"), "w") as fh:
         json.dump(meta, fh)
 
@@ -45,6 +46,9 @@ def load_into(eng, output_dir: str, step: int):
     st = torch.load(os.path.join(d, f"rank{eng.mesh.rank}.pt"), map_location="cpu", weights_only=True)
     f = eng.flat
     f.params.copy_(st["params"].to(f.device))
+    if st["exp_avg"].shape != f.exp_avg.shape:
+        raise ValueError(f"checkpoint Adam state has {st['exp_avg'].numel()} elements, this rank holds "
+                         f"{f.exp_avg.numel()}: a zero_stage=1 checkpoint resumes only at the same dp and zero_stage")
     f.exp_avg.copy_(st["exp_avg"].to(f.device))
     f.exp_avg_sq.copy_(st["exp_avg_sq"].to(f.device))
     eng.opt.step_t.copy_(st["step_t"].to(f.device))

@@ -51,3 +51,30 @@ def test_consolidate_tp_checkpoint_equals_single_process(tmp_path):
             a, b = a.view(3, -1)[[0, 2]], b.view(3, -1)[[0, 2]]
         # Adam's first steps turn near-zero gradients into +-lr updates, so compare in norm
         assert ((a - b).norm() / b.norm()).item() < 2e-3, n
+
+
+def _zero_worker(out, steps, ckpt_every, resume, res_dir):
+    from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
+
+    torch.set_num_threads(1)
+    d = init_distributed("cpu")
+    r = train(TrainConfig(seed=0, parallel="dp", batch=4, steps=steps, log_every=1000, output_dir=out, device="cpu",
+                          warmup_steps=0, ckpt_every=ckpt_every, resume=resume, zero_stage=1), MC, OC, d, quiet=True)
+    eng = r["engine"]
+    # ZeRO-1: each rank holds its shard of the Adam state, not the whole buffer
+    assert eng.flat.exp_avg.numel() < eng.flat.numel
+    if d.rank == 0:
+        torch.save(r["history"], os.path.join(res_dir, "hist.pt"))
+    destroy()
+
+
+@pytest.mark.slow
+def test_zero1_resume_reproduces_uninterrupted_run(tmp_path):
+    def run(out, steps, ckpt_every=0, resume=False):
+        spawn(_zero_worker, 2, args=(str(tmp_path / out), steps, ckpt_every, resume, str(tmp_path)))
+        return torch.load(str(tmp_path / "hist.pt"))
+
+    full = run("a", 6)
+    part1 = run("b", 3, ckpt_every=3)
+    part2 = run("b", 3, resume=True)
+    assert part1 + part2 == pytest.approx(full, rel=1e-6, abs=1e-6)
