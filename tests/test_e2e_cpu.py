@@ -45,6 +45,15 @@ def test_main_cli(tmp_path, yaml, strategy, nproc):
     assert df.loss.between(5, 12).all()
 
 
+@pytest.mark.slow
+def test_main_cli_zero1(tmp_path):
+    """configs/train_config_dp_zero1.yaml: DP with ZeRO-1 optimizer-state sharding over 2 ranks."""
+    out = _run(tmp_path, "train_config_dp_zero1.yaml", nproc=2)
+    assert "Running `dp` on 2 devices." in out
+    df = pd.read_csv(tmp_path / "outputs" / "dp_zero1" / "log.csv")
+    assert df.step.tolist() == [0, 1, 2, 3] and df.loss.between(5, 12).all()
+
+
 def test_unknown_strategy_rejected(tmp_path):
     shutil.copytree(os.path.join(ROOT, "configs"), tmp_path / "configs")
     (tmp_path / "configs" / "bad.yaml").write_text(
