@@ -11,6 +11,7 @@ segments after the first eager warmup step.
 from __future__ import annotations
 
 import os
+import warnings
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -80,9 +81,16 @@ class Engine:
         # (103 MB fp32 for the reference vocab, issued last -> fully exposed), all-gather the
         # embedding-output grads (b_local*T*D fp32 per rank) and let every rank rebuild the
         # identical wte/wpe grads from the global batch with the deterministic sorted kernel.
-        self.zero = bool(train_cfg.zero_stage >= 1 and dp > 1)
+        if train_cfg.zero_stage not in (0, 1):
+            raise ValueError(f"zero_stage={train_cfg.zero_stage}: only 0 (replicated Adam state) and 1 (ZeRO-1) "
+                             "are implemented")
+        self.zero = bool(train_cfg.zero_stage == 1 and dp > 1)
         if self.zero and (tp > 1 or pp > 1):
             raise ValueError("zero_stage=1 is implemented for pure data parallelism (tp = pp = 1)")
+        if train_cfg.zero_stage == 1 and dp == 1 and dinfo.rank == 0:
+            warnings.warn("zero_stage=1 ignored: dp == 1 (nothing to shard); running the replicated AdamW")
+        if self.zero and train_cfg.defer_optimizer and dinfo.rank == 0:
+            warnings.warn("defer_optimizer ignored under zero_stage=1 (the sharded update ends the step)")
         self.embed_gather = bool(dp > 1 and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed
                                  and not self.zero)
         self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb,

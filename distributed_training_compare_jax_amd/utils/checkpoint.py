@@ -41,14 +41,62 @@ def save(eng, output_dir: str, step: int):
         json.dump(meta, fh)
 
 
+def _read_metas(d: str) -> Dict[int, dict]:
+    if not os.path.isdir(d):
+        raise FileNotFoundError(f"no checkpoint directory {d}")
+    metas = {}
+    for x in sorted(os.listdir(d)):
+        if x.startswith("meta_rank") and x.endswith(".json"):
+            with open(os.path.join(d, x)) as fh:
+                m = json.load(fh)
+            metas[int(m["rank"])] = m
+    if not metas:
+        raise FileNotFoundError(f"checkpoint {d} has no meta_rank*.json")
+    return metas
+
+
+def source_rank(eng, metas: Dict[int, dict]) -> int:
+    """The checkpoint rank file this rank resumes from, after checking the layouts are compatible.
+
+    Every check runs on the metadata alone, before any buffer is touched.  TP/PP degrees and
+    ``zero_stage`` must match (flat buffers are laid out per TP/PP shard; ZeRO-1 Adam state per DP
+    rank).  Without ZeRO the DP replicas hold identical state, so the DP degree may change: a rank
+    whose own (dp, tp, pp) index has no file reads the dp_idx 0 replica of its shard."""
+    mesh = eng.mesh
+    m0 = metas[min(metas)]
+    zero_now = int(bool(getattr(eng, "zero", False)))
+    zero_ck = int(m0.get("zero_stage", 0))
+    if m0.get("model") not in (None, eng.mcfg.name):
+        raise ValueError(f"checkpoint is of model {m0.get('model')!r}, this run trains {eng.mcfg.name!r}")
+    if (m0["tp"], m0["pp"]) != (mesh.tp, mesh.pp):
+        raise ValueError(f"checkpoint layout tp={m0['tp']} pp={m0['pp']} differs from this run's tp={mesh.tp} "
+                         f"pp={mesh.pp}: resume needs the same TP/PP split (use consolidate() to re-shard)")
+    if zero_ck != zero_now:
+        raise ValueError(f"checkpoint zero_stage={zero_ck} (dp={m0['dp']}) but this run has zero_stage={zero_now} "
+                         f"(dp={mesh.dp}): Adam state is stored per layout")
+    if zero_now and m0["dp"] != mesh.dp:
+        raise ValueError(f"zero_stage=1 checkpoint was written at dp={m0['dp']}, this run has dp={mesh.dp}: "
+                         "each rank's Adam shard resumes only at the same dp")
+    want = (mesh.dp_idx, mesh.tp_idx, mesh.pp_idx)
+    for r, m in metas.items():
+        if (m["dp_idx"], m["tp_idx"], m["pp_idx"]) == want:
+            return r
+    if not zero_now:
+        for r, m in metas.items():
+            if (m["dp_idx"], m["tp_idx"], m["pp_idx"]) == (0, mesh.tp_idx, mesh.pp_idx):
+                return r
+    raise ValueError(f"checkpoint (world {len(metas)}) has no rank file for dp/tp/pp index {want}")
+
+
 def load_into(eng, output_dir: str, step: int):
     d = _dir(output_dir, step)
-    st = torch.load(os.path.join(d, f"rank{eng.mesh.rank}.pt"), map_location="cpu", weights_only=True)
+    src = source_rank(eng, _read_metas(d))
+    st = torch.load(os.path.join(d, f"rank{src}.pt"), map_location="cpu", weights_only=True)
     f = eng.flat
+    for k, have in (("params", f.params), ("exp_avg", f.exp_avg), ("exp_avg_sq", f.exp_avg_sq)):
+        if st[k].shape != have.shape:
+            raise ValueError(f"checkpoint {k} has {st[k].numel()} elements, this rank holds {have.numel()}")
     f.params.copy_(st["params"].to(f.device))
-    if st["exp_avg"].shape != f.exp_avg.shape:
-        raise ValueError(f"checkpoint Adam state has {st['exp_avg'].numel()} elements, this rank holds "
-                         f"{f.exp_avg.numel()}: a zero_stage=1 checkpoint resumes only at the same dp and zero_stage")
     f.exp_avg.copy_(st["exp_avg"].to(f.device))
     f.exp_avg_sq.copy_(st["exp_avg_sq"].to(f.device))
     eng.opt.step_t.copy_(st["step_t"].to(f.device))

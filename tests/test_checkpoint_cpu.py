@@ -78,3 +78,66 @@ def test_zero1_resume_reproduces_uninterrupted_run(tmp_path):
     part1 = run("b", 3, ckpt_every=3)
     part2 = run("b", 3, resume=True)
     assert part1 + part2 == pytest.approx(full, rel=1e-6, abs=1e-6)
+
+
+def _edit_meta(out, step, **kw):
+    import json
+
+    d = os.path.join(out, "ckpt", f"step_{step}")
+    for x in os.listdir(d):
+        if x.startswith("meta_rank"):
+            p = os.path.join(d, x)
+            m = json.load(open(p))
+            m.update(kw)
+            json.dump(m, open(p, "w"))
+
+
+@pytest.mark.parametrize("edit,msg", [(dict(zero_stage=1, dp=2), "zero_stage"), (dict(tp=2), "tp=2"),
+                                      (dict(model="gpt2-medium"), "model")])
+def test_resume_layout_mismatch_fails_before_touching_buffers(tmp_path, edit, msg):
+    out = str(tmp_path / "c")
+    train(_tc(out, 2, ckpt_every=2), MC, OC, CPU, quiet=True)
+    _edit_meta(out, 2, **edit)
+    eng = train(_tc(str(tmp_path / "fresh"), 0), MC, OC, CPU, quiet=True)["engine"]
+    before = eng.flat.params.clone()
+    with pytest.raises(ValueError, match=msg):
+        C.load_into(eng, out, 2)
+    assert torch.equal(eng.flat.params, before)
+
+
+def test_resume_missing_checkpoint_is_a_clear_error(tmp_path):
+    eng = train(_tc(str(tmp_path / "fresh"), 0), MC, OC, CPU, quiet=True)["engine"]
+    with pytest.raises(FileNotFoundError, match="no checkpoint"):
+        C.load_into(eng, str(tmp_path / "nothing"), 5)
+
+
+def test_zero_stage_validation():
+    from distributed_training_compare_jax_amd.train.engine import Engine
+
+    with pytest.raises(ValueError, match="zero_stage=2"):
+        Engine(MC, _tc("/tmp/unused", 1, zero_stage=2), OC, CPU)
+    with pytest.warns(UserWarning, match="dp == 1"):
+        Engine(MC, _tc("/tmp/unused", 1, zero_stage=1), OC, CPU)
+
+
+def _dp_resume_worker(out, res_dir):
+    from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
+
+    torch.set_num_threads(1)
+    d = init_distributed("cpu")
+    r = train(TrainConfig(seed=0, parallel="dp", batch=4, steps=3, log_every=1000, output_dir=out, device="cpu",
+                          warmup_steps=0, resume=True), MC, OC, d, quiet=True)
+    if d.rank == 0:
+        torch.save(r["history"], os.path.join(res_dir, "hist_dp2.pt"))
+    destroy()
+
+
+@pytest.mark.slow
+def test_replicated_checkpoint_resumes_at_larger_dp(tmp_path):
+    """dp1 checkpoint -> dp2 resume: rank 1 has no file of its own and reads the dp_idx 0 replica."""
+    full = train(_tc(str(tmp_path / "a"), 6), MC, OC, CPU, quiet=True)["history"]
+    out = str(tmp_path / "b")
+    train(_tc(out, 3, ckpt_every=3), MC, OC, CPU, quiet=True)
+    spawn(_dp_resume_worker, 2, args=(out, str(tmp_path)))
+    part2 = torch.load(str(tmp_path / "hist_dp2.pt"))
+    assert part2 == pytest.approx(full[3:], rel=1e-4, abs=1e-4)
