@@ -778,6 +778,238 @@ __global__ void __launch_bounds__(RES_THREADS) attn_bwd_dq_res_kernel(
   attn_bwd_dq_res_body<HD>(lds, blockIdx.x, qkv, o, dout, lse, dqkv, B, T, H, scale);
 }
 
+// ============================================================================ fused single-round backward
+// The merged backward above runs 2*B*H dK/dV blocks and 2*B*H dQ blocks of 16 waves at one block
+// per CU: two rounds, each paying its own panel staging and its own causal tail (the wave with the
+// most tiles sets the round time).  Here ONE block per (b, h) half holds all four panels (Q, dO,
+// K, V) and wave w computes BOTH the dK/dV of key group g = 2w + half (queries >= its keys:
+// ~(T - 16g)/64 tiles) and the dQ of query group g (keys <= its queries: ~(16g + 16)/64 tiles), so
+// every wave carries the same ~T/64 + 1 tiles and the backward is a single round with one staging.
+//
+// LDS: unpadded [rows][32] bf16 panels (64-B rows) with the 16-B chunk c of row r stored at
+// c ^ fb_swz(r), fb_swz = {0, 2, 3, 1}[(r >> 2) & 3]: the row-fragment ds_read_b128 (16 rows x 4
+// chunks) and the transposed ds_read_b64_tr_b16 (8 rows x 32 B per 32-lane half) are both
+// bank-conflict-free (tests/test_attn_swizzle_cpu.py simulates the banks).  Q and dO get 64 slack
+// rows (dK/dV query tiles start at 16-row offsets) and every row >= T is zero: there p = 2^0 = 1
+// but dO = 0 and delta = 0, so dV and dK receive exactly 0 from them — no bounds masks in the loops.
+// The causal mask is needed only on the diagonal tile, which is peeled (DIAG template).
+constexpr int FB_THREADS = 1024;
+constexpr int FB_MAXT_Q = RES_MAXT + 64;  // Q/dO panel rows at T = RES_MAXT
+
+__device__ __forceinline__ int fb_swz(int r) { return (0x1320 >> (((r >> 2) & 3) * 4)) & 3; }
+
+// A/B operand fragment: rows r0 + (lane & 15), hd chunk lane >> 4 (r0 % 16 == 0)
+__device__ __forceinline__ bf16x8 fb_row(const bf16* p, int r0, int lane) {
+  const int r = r0 + (lane & 15), c = lane >> 4;
+  return *(const bf16x8*)(p + r * 32 + ((c ^ fb_swz(r)) << 3));
+}
+// transposed fragment over the 32 k-rows r0..r0+31 (r0 % 16 == 0), hd columns 16t..16t+15, in the
+// permuted k order of tr_frag above
+__device__ __forceinline__ bf16x8 fb_tr(const bf16* p, int r0, int t, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int r = r0 + 4 * g + q;
+  const int c = 2 * t + (pp >> 1);
+  const bf16* p0 = p + r * 32 + ((c ^ fb_swz(r)) << 3) + (pp & 1) * 4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0 + 16 * 32));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// dK/dV of one 64-query tile (queries q0..q0+63) for this wave's 16 keys
+template <bool DIAG>
+__device__ __forceinline__ void fb_dkdv_tile(const bf16* sQ, const bf16* sD, const float* sLse, const float* sDel,
+                                             int q0, int key, const bf16x8& kf, const bf16x8& vf, float c,
+                                             f32x4 (&dk)[2], f32x4 (&dv)[2], int lane) {
+  const int g = lane >> 4;
+  f32x4 p[4], ds[4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 sc = mfma(fb_row(sQ, q0 + qt * 16, lane), kf, z);  // S[q][key]
+    const f32x4 dp = mfma(fb_row(sD, q0 + qt * 16, lane), vf, z);  // dP[q][key]
+    const int qr = q0 + qt * 16 + 4 * g;
+    const f32x4 l4 = *(const f32x4*)(sLse + qr), d4 = *(const f32x4*)(sDel + qr);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = fast_exp2(sc[r] * c - l4[r]);  // sLse holds lse * log2(e)
+      if (DIAG) pv = key <= qr + r ? pv : 0.f;
+      p[qt][r] = pv;
+      ds[qt][r] = pv * (dp[r] - d4[r]);
+    }
+  }
+#pragma unroll
+  for (int hq = 0; hq < 2; ++hq) {
+    const bf16x8 pb = pack_p(p[2 * hq], p[2 * hq + 1]), dsb = pack_p(ds[2 * hq], ds[2 * hq + 1]);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      dv[t] = mfma(fb_tr(sD, q0 + 32 * hq, t, lane), pb, dv[t]);   // dV^T[hd][key] += dO^T P
+      dk[t] = mfma(fb_tr(sQ, q0 + 32 * hq, t, lane), dsb, dk[t]);  // dK^T[hd][key] += Q^T dS
+    }
+  }
+}
+
+// dQ of one 64-key tile (keys k0..k0+63) for this wave's 16 queries
+template <bool DIAG>
+__device__ __forceinline__ void fb_dq_tile(const bf16* sK, const bf16* sV, int k0, int q, float lq, float dlt,
+                                           const bf16x8& qf, const bf16x8& df, float c, f32x4 (&acc)[2], int lane) {
+  const int g = lane >> 4;
+  f32x4 ds[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 sc = mfma(fb_row(sK, k0 + st * 16, lane), qf, z);
+    const f32x4 dp = mfma(fb_row(sV, k0 + st * 16, lane), df, z);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pv = fast_exp2(sc[r] * c - lq);
+      if (DIAG) pv = k0 + st * 16 + 4 * g + r <= q ? pv : 0.f;
+      ds[st][r] = pv * (dp[r] - dlt);
+    }
+  }
+#pragma unroll
+  for (int hk = 0; hk < 2; ++hk) {
+    const bf16x8 dsb = pack_p(ds[2 * hk], ds[2 * hk + 1]);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc[t] = mfma(fb_tr(sK, k0 + 32 * hk, t, lane), dsb, acc[t]);
+  }
+}
+
+// rows of the Q/dO panels (and lse/delta) the fused backward stages: the dK/dV query tiles of the
+// last key group reach row 16*(ngroups-1) + 63
+__host__ __device__ inline int fb_rows_q(int T) { return (T + 15) / 16 * 16 + 64; }
+__host__ __device__ inline int fb_rows_k(int T) { return (T + 63) / 64 * 64; }
+
+template <int HD>
+__global__ void __launch_bounds__(FB_THREADS) attn_bwd_fused_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  static_assert(HD == 32, "fused backward: head_dim 32 (one MFMA K, 64-B panel rows)");
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, g4 = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int half, bh;
+  res_block_map(blockIdx.x, B * H, half, bh);
+  const int b = bh / H, h = bh % H;
+  const int Rq = fb_rows_q(T), Rk = fb_rows_k(T);
+  bf16* sQ = lds;
+  bf16* sD = sQ + Rq * 32;
+  bf16* sK = sD + Rq * 32;
+  bf16* sV = sK + Rk * 32;
+  float* sLse = (float*)(sV + Rk * 32);
+  float* sDel = sLse + Rq;
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const bf16* Ob = o + (long)b * T * dts + h * HD;
+  const float* lseb = lse + ((long)b * H + h) * T;
+
+  // ---- staging: every global load of the thread in flight before the first LDS store
+  {
+    constexpr int PQ = (FB_MAXT_Q * 4 + FB_THREADS - 1) / FB_THREADS;  // 16-B chunks per thread (Q/dO/O)
+    constexpr int PK = (RES_MAXT * 4 + FB_THREADS - 1) / FB_THREADS;   // (K/V)
+    u32x4 vq[PQ], vd[PQ], vo[PQ], vk[PK], vv[PK];
+#pragma unroll
+    for (int i = 0; i < PQ; ++i) {
+      const int c = tid + i * FB_THREADS, r = c >> 2, col = (c & 3) * 8;
+      const bool ok = r < T;
+      vq[i] = ok ? *(const u32x4*)(Qb + (long)r * ts + col) : u32x4{0, 0, 0, 0};
+      vd[i] = ok ? *(const u32x4*)(dOb + (long)r * dts + col) : u32x4{0, 0, 0, 0};
+      vo[i] = ok ? *(const u32x4*)(Ob + (long)r * dts + col) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < PK; ++i) {
+      const int c = tid + i * FB_THREADS, r = c >> 2, col = (c & 3) * 8;
+      const bool ok = r < T;
+      vk[i] = ok ? *(const u32x4*)(Kb + (long)r * ts + col) : u32x4{0, 0, 0, 0};
+      vv[i] = ok ? *(const u32x4*)(Vb + (long)r * ts + col) : u32x4{0, 0, 0, 0};
+    }
+    float lv[PQ / 4 + 1];
+#pragma unroll
+    for (int i = 0; i * FB_THREADS < FB_MAXT_Q; ++i) {
+      const int r = tid + i * FB_THREADS;
+      lv[i] = r < T ? lseb[r] * LOG2E : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < PQ; ++i) {
+      const int c = tid + i * FB_THREADS, r = c >> 2, ch = c & 3;
+      // delta[r] = rowsum(dO * O): the row's 4 chunks sit in 4 adjacent lanes
+      float d = dot8(__builtin_bit_cast(bf16x8, vd[i]), __builtin_bit_cast(bf16x8, vo[i]));
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 1, 64);
+      if (r < Rq) {
+        const int off = r * 32 + ((ch ^ fb_swz(r)) << 3);
+        *(u32x4*)(sQ + off) = vq[i];
+        *(u32x4*)(sD + off) = vd[i];
+        if (ch == 0) sDel[r] = d;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PK; ++i) {
+      const int c = tid + i * FB_THREADS, r = c >> 2, ch = c & 3;
+      if (r < Rk) {
+        const int off = r * 32 + ((ch ^ fb_swz(r)) << 3);
+        *(u32x4*)(sK + off) = vk[i];
+        *(u32x4*)(sV + off) = vv[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i * FB_THREADS < FB_MAXT_Q; ++i) {
+      const int r = tid + i * FB_THREADS;
+      if (r < Rq) sLse[r] = lv[i];
+    }
+  }
+  __syncthreads();
+  const int grp = 2 * w + half;
+  if (grp * 16 >= T) return;  // no barrier below
+  const float c = scale * LOG2E;
+
+  // ---- dK / dV of keys 16*grp .. +15 (queries q0 >= the keys; the first tile is the diagonal)
+  {
+    const int key = grp * 16 + j;
+    const bf16x8 kf = fb_row(sK, grp * 16, lane), vf = fb_row(sV, grp * 16, lane);
+    f32x4 dk[2], dv[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) { dk[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
+    fb_dkdv_tile<true>(sQ, sD, sLse, sDel, grp * 16, key, kf, vf, c, dk, dv, lane);
+    for (int q0 = grp * 16 + 64; q0 < T; q0 += 64)
+      fb_dkdv_tile<false>(sQ, sD, sLse, sDel, q0, key, kf, vf, c, dk, dv, lane);
+    if (key < T) {
+      bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
+      bf16* pv = dqkv + ((long)b * T + key) * ts + (2 * H + h) * HD;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        *(bf16x4*)(pk + t * 16 + 4 * g4) = bf16x4{f2bf(dk[t][0] * scale), f2bf(dk[t][1] * scale),
+                                                  f2bf(dk[t][2] * scale), f2bf(dk[t][3] * scale)};
+        *(bf16x4*)(pv + t * 16 + 4 * g4) = bf16x4{f2bf(dv[t][0]), f2bf(dv[t][1]), f2bf(dv[t][2]), f2bf(dv[t][3])};
+      }
+    }
+  }
+  // ---- dQ of queries 16*grp .. +15 (keys <= the queries; the last tile is the diagonal)
+  {
+    const int q = grp * 16 + j;
+    const bf16x8 qf = fb_row(sQ, grp * 16, lane), df = fb_row(sD, grp * 16, lane);
+    const float lq = sLse[q], dlt = sDel[q];
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int ntile = (grp * 16 + 16 + 63) / 64;
+    for (int kt = 0; kt < ntile - 1; ++kt) fb_dq_tile<false>(sK, sV, kt * 64, q, lq, dlt, qf, df, c, acc, lane);
+    fb_dq_tile<true>(sK, sV, (ntile - 1) * 64, q, lq, dlt, qf, df, c, acc, lane);
+    if (q < T) {
+      bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        *(bf16x4*)(pq + t * 16 + 4 * g4) = bf16x4{f2bf(acc[t][0] * scale), f2bf(acc[t][1] * scale),
+                                                  f2bf(acc[t][2] * scale), f2bf(acc[t][3] * scale)};
+    }
+  }
+}
+
+
+inline long fb_lds_bytes(int T) {
+  return (long)(2 * fb_rows_q(T) + 2 * fb_rows_k(T)) * 32 * 2 + (long)2 * fb_rows_q(T) * 4;
+}
+
 // LDS bytes of the resident kernels; 0 if the sequence does not fit (then the tiled kernels run)
 inline long res_lds_fwd(int T, int HD) { const long Tp = (T + 63) / 64 * 64; return Tp * (AttnLds<32>::KLD + HD + 16) * 2; }
 inline long res_lds_dkdv(int T, int HD) { const long Tp = (T + 63) / 64 * 64 + 64; return 2 * Tp * (HD + 16) * 2 + Tp * 8; }
@@ -837,7 +1069,14 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
   int nb = (T + 63) / 64;
   dim3 grid(B * H * nb);
   static const int merged = [] { const char* v = getenv("DTC_ATTN_MERGED"); return v ? atoi(v) : 1; }();
-  if (use_resident(T, HD) && !merged) {
+  // DTC_ATTN_FUSED=0: the two-round merged/split resident kernels instead of the fused single round
+  static const int fused = [] { const char* v = getenv("DTC_ATTN_FUSED"); return v ? atoi(v) : 1; }();
+  // flags bit 0: force the two-round kernels (in-process A/B, benchmarks/attn_ab.py)
+  if (use_resident(T, HD) && fused && !(flags & 1) && fb_lds_bytes(T) <= LDS_MAX) {
+    allow_lds(attn_bwd_fused_kernel<32>, fb_lds_bytes(T));
+    hipLaunchKernelGGL(attn_bwd_fused_kernel<32>, dim3(B * H * 2), dim3(FB_THREADS), fb_lds_bytes(T), st, qkv, o, dout,
+                       lse, dqkv, B, T, H, scale);
+  } else if (use_resident(T, HD) && !merged) {
     allow_lds(attn_bwd_dkdv_res_kernel<32>, res_lds_dkdv(T, HD));
     allow_lds(attn_bwd_dq_res_kernel<32>, res_lds_dq(T, HD));
     hipLaunchKernelGGL(attn_bwd_dkdv_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_dkdv(T, HD), st, qkv,

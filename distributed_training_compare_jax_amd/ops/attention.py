@@ -46,8 +46,9 @@ def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None):
 
 
 def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Tensor, n_heads: int,
-             scale: float | None = None) -> torch.Tensor:
-    """Returns dqkv [B,T,3*H*hd] (same dtype as qkv)."""
+             scale: float | None = None, flags: int = 0) -> torch.Tensor:
+    """Returns dqkv [B,T,3*H*hd] (same dtype as qkv).  ``flags`` bit 0 forces the two-round resident
+    kernels instead of the fused single-round one (A/B and tests)."""
     B, T, C3 = qkv.shape
     hd = C3 // (3 * n_heads)
     scale = scale if scale is not None else hd ** -0.5
@@ -69,7 +70,7 @@ def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Te
     dqkv = torch.empty_like(qkv)
     L = N.lib()
     ws = _workspace(qkv.device, int(L.dtc_attn_bwd_workspace_bytes(B, T, n_heads, hd)))
-    N.check(L.dtc_attn_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), 0,
+    N.check(L.dtc_attn_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), int(flags),
                            B, T, n_heads, hd, 0, scale, ws.data_ptr(), ws.numel(), N.stream_ptr(qkv.device)),
             "dtc_attn_bwd")
     return dqkv

@@ -194,6 +194,22 @@ def test_attention(cuda, B, T, H, hd):
         _close(d3[:, :, i], r3[:, :, i], 3e-2, f"attn_d{n}")
 
 
+@pytest.mark.parametrize("B,T,H", [(2, 512, 4), (1, 200, 3), (2, 64, 2)])
+def test_attention_bwd_fused_matches_two_round(cuda, B, T, H):
+    """The fused single-round backward and the two-round resident kernels compute the same
+    gradients (different summation orders only) and both match the fp32 reference."""
+    qkv = _r(B, T, 3 * H * 32, seed=30)
+    do = _r(B, T, H * 32, seed=31)
+    o, lse = A.attn_fwd(qkv, H)
+    d_fused = A.attn_bwd(qkv, o, lse, do, H)
+    d_two = A.attn_bwd(qkv, o, lse, do, H, flags=1)
+    dref = A.attn_bwd(qkv.cpu().float(), o.cpu().float(), lse.cpu(), do.cpu().float(), H)
+    _close(d_fused.cpu().float(), dref, 3e-2, "attn_bwd_fused")
+    _close(d_fused.cpu().float(), d_two.cpu().float(), 2e-2, "fused_vs_two_round")
+    # deterministic: a second launch is bitwise identical
+    assert torch.equal(d_fused, A.attn_bwd(qkv, o, lse, do, H))
+
+
 @pytest.mark.parametrize("M,D,V,Vp", [(512, 128, 1000, 1024), (2048, 256, 50258, 50304)])
 def test_lmhead_ce(cuda, M, D, V, Vp):
     """Second case runs the 256x256 DMA-staged kernel (>= 512 tiles), incl. its ragged last N tile."""
