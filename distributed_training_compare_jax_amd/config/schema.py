@@ -24,8 +24,9 @@ are optional and default to the reference behaviour:
   ``tp_comm`` (``auto`` | ``p2p`` | ``rccl``: TP activation all-reduces as in-graph xGMI
   peer-to-peer kernels, ``parallel/p2p.py``; ``auto`` = p2p on a GPU RCCL group),
   ``defer_optimizer`` / ``defer_groups`` (run the non-embedding AdamW under the next step's
-  forward in that many layer groups; exact, off by default: measured neutral at the
-  reference size because the forward kernels slow down under the AdamW's HBM traffic),
+  forward in that many layer groups, on its own stream with a capped grid, ``DTC_DEFER_BLOCKS``;
+  exact, off by default: measured slower at the reference size because the forward GEMMs run
+  ~2x slower while the AdamW blocks share their CUs, ``profiles/r2_ab_defer_optimizer.log``),
   ``zero_stage`` (1 = ZeRO-1 Adam-state sharding over the DP group, ``ShardedAdamW``; pure DP only).
 """
 

@@ -106,7 +106,7 @@ def _declare(lib):
         "dtc_sumsq_workspace_bytes": ([], l),
         "dtc_sumsq_partial": ([vp, vp, i, vp, i, vp], i),
         "dtc_sum_finish": ([vp, i, vp, vp, vp], i),
-        "dtc_adamw": ([vp, vp, vp, vp, vp, l, l, vp, vp, f, f, f, f, f, f, vp, vp], i),
+        "dtc_adamw": ([vp, vp, vp, vp, vp, l, l, vp, vp, f, f, f, f, f, f, vp, i, vp], i),
         "dtc_cast_f32_bf16": ([vp, vp, l, vp], i),
         "dtc_fill_f32": ([vp, f, l, vp], i),
     }

@@ -82,12 +82,13 @@ def sum_finish(part: torch.Tensor, out: torch.Tensor, step: Optional[torch.Tenso
 def adamw_flat(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                mirror: Optional[torch.Tensor], n_mirror: int, step: torch.Tensor, sumsq: torch.Tensor,
                lr: float, b1: float, b2: float, eps: float, wd: float, max_norm: float,
-               enable: Optional[torch.Tensor] = None):
+               enable: Optional[torch.Tensor] = None, max_blocks: int = 0):
     """In-place AdamW on flat fp32 buffers; ``mirror[:n_mirror] = bf16(p[:n_mirror])``.
 
     ``step`` (int64 [1], already incremented) gives t for the bias correction; ``sumsq``
     (fp32 [1]) is the global Σg² for the clip.  ``enable`` (fp32 [1], optional): the update is
-    skipped when ``enable[0] == 0`` (device-side switch for the deferred optimizer)."""
+    skipped when ``enable[0] == 0`` (device-side switch for the deferred optimizer).  ``max_blocks``
+    (GPU, > 0): cap the grid (grid-stride loop) so the pass shares the CUs with concurrent kernels."""
     n = p.numel()
     if not p.is_cuda:
         if enable is not None and float(enable.item()) == 0.0:
@@ -106,7 +107,7 @@ def adamw_flat(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tenso
         return
     N.check(N.lib().dtc_adamw(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), N.ptr(mirror), n, n_mirror,
                               step.data_ptr(), sumsq.data_ptr(), lr, b1, b2, eps, wd, max_norm, N.ptr(enable),
-                              N.stream_ptr(p.device)), "dtc_adamw")
+                              int(max_blocks), N.stream_ptr(p.device)), "dtc_adamw")
 
 
 def cast_to_bf16(src: torch.Tensor, dst: torch.Tensor):

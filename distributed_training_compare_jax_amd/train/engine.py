@@ -156,8 +156,13 @@ class Engine:
         # traffic) then overlaps the compute-bound forward instead of idling the MFMAs at the
         # end of the step.  Semantics are unchanged (same norm, same update, before each use);
         # :meth:`flush_optimizer` completes a pending update (checkpoint, end of run, bench).
-        self.defer_opt = bool(on_gpu and pp == 1 and not self.zero and train_cfg.defer_optimizer and self.stage.side.stream is not None)
+        self.defer_opt = bool(on_gpu and pp == 1 and not self.zero and train_cfg.defer_optimizer)
         if self.defer_opt:
+            # its own stream (the backward side stream when that is on): the capped-grid AdamW passes
+            # share the CUs with the forward GEMMs instead of queueing ahead of them
+            self.opt_stream = self.stage.side.stream or torch.cuda.Stream(self.device)
+            self._defer_blocks = int(os.environ.get("DTC_DEFER_BLOCKS", "256"))
+            self.program.before_comm.append(self._join_opt)
             # device-side "an update is pending" switch: the graph always contains the deferred
             # launch, the kernels skip when nothing is pending (first step, after a flush)
             self._pending_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -220,18 +225,23 @@ class Engine:
 
     # ------------------------------------------------------------------ step bodies
     def _launch_deferred_update(self):
-        """Queue the pending AdamW (all but the embedding tables) on the side stream, group by group."""
+        """Queue the pending AdamW (all but the embedding tables) on the optimizer stream, group by
+        group in forward order; each group's event gates the first forward use of its params."""
         if not self.defer_opt:
             return
-        st, flag = self.stage, self._pending_dev
+        st, flag, s = self.stage, self._pending_dev, self.opt_stream
+        s.wait_stream(torch.cuda.current_stream())
         for key, ranges in self._opt_groups:
-            def upd(ranges=ranges):
+            with torch.cuda.stream(s):
                 for lo, hi in ranges:
-                    self.opt.update_range(lo, hi, enable=flag)
-            st.side.run(upd)
-            ev = torch.cuda.Event()
-            ev.record(st.side.stream)
+                    self.opt.update_range(lo, hi, enable=flag, max_blocks=self._defer_blocks)
+                ev = torch.cuda.Event()
+                ev.record(s)
             st.param_ready[key] = ev
+
+    def _join_opt(self):
+        if self.defer_opt:
+            torch.cuda.current_stream().wait_stream(self.opt_stream)
 
     def _finish_optimizer(self):
         if self.defer_opt:

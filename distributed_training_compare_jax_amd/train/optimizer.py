@@ -131,16 +131,16 @@ class FusedAdamW:
             s = self.sumsq
             self.program.comm(lambda: dist.all_reduce(s, group=g))
 
-    def update_range(self, lo: int, hi: int, enable=None):
+    def update_range(self, lo: int, hi: int, enable=None, max_blocks: int = 0):
         """Clip + AdamW over flat[lo:hi] (4-aligned) with the norm/step of the last :meth:`norm`
-        (skipped on device when ``enable[0] == 0``)."""
+        (skipped on device when ``enable[0] == 0``; ``max_blocks`` caps the kernel's grid)."""
         f, c = self.flat, self.cfg
         if hi <= lo:
             return
         nm = (min(max(f.n_mirror - lo, 0), hi - lo) if f.use_mirror else 0)
         O.adamw_flat(f.params[lo:hi], f.grads[lo:hi], f.exp_avg[lo:hi], f.exp_avg_sq[lo:hi],
                      f.mirror[lo:lo + max(nm, 4)] if nm > 0 else None, nm, self.step_t, self.sumsq, c.lr, c.b1, c.b2,
-                     c.eps, c.weight_decay, c.grad_clip, enable=enable)
+                     c.eps, c.weight_decay, c.grad_clip, enable=enable, max_blocks=max_blocks)
 
     def step(self):
         self.norm()

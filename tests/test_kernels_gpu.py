@@ -277,6 +277,11 @@ def test_adamw_matches_cpu(cuda):
     _close(p.cpu(), pc, 1e-6, "adamw_p")
     _close(mirror.cpu(), pc, 1e-2, "adamw_mirror")
     _close(v.cpu(), vc, 1e-5, "adamw_v")
+    # capped grid (grid-stride loop, the deferred optimizer's form) is bitwise the same update
+    p2, m2, v2, mir2 = p.clone(), m.clone(), v.clone(), mirror.clone()
+    O.adamw_flat(p, g, m, v, mirror, n, step, ss, 3e-4, 0.9, 0.999, 1e-8, 0.1, 1.0)
+    O.adamw_flat(p2, g, m2, v2, mir2, n, step, ss, 3e-4, 0.9, 0.999, 1e-8, 0.1, 1.0, max_blocks=7)
+    assert torch.equal(p, p2) and torch.equal(m, m2) and torch.equal(v, v2) and torch.equal(mirror, mir2)
 
 
 def test_batched_reducer_matches_per_op(cuda):
