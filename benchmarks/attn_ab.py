@@ -53,9 +53,14 @@ def main():
     diff = (d_new.float() - d_old.float()).abs().max().item()
     ref = d_old.float().abs().max().item()
     print(f"max |fused - two-round| = {diff:.3e} (max |d| {ref:.3e})", flush=True)
-    res = {"fwd": [], "bwd fused": [], "bwd two-round": []}
+    o1, l1 = A.attn_fwd(qkv, H, flags=1)
+    torch.cuda.synchronize()
+    print(f"fwd zig vs plain order: max |do| {(o.float() - o1.float()).abs().max().item():.3e}, "
+          f"max |dlse| {(lse - l1).abs().max().item():.3e}", flush=True)
+    res = {"fwd": [], "fwd plain order": [], "bwd fused": [], "bwd two-round": []}
     for _ in range(a.rounds):
         res["fwd"].append(timeit(lambda: A.attn_fwd(qkv, H), a.reps))
+        res["fwd plain order"].append(timeit(lambda: A.attn_fwd(qkv, H, flags=1), a.reps))
         res["bwd fused"].append(timeit(lambda: A.attn_bwd(qkv, o, lse, do, H), a.reps))
         res["bwd two-round"].append(timeit(lambda: A.attn_bwd(qkv, o, lse, do, H, flags=1), a.reps))
     for k, v in res.items():

@@ -445,7 +445,7 @@ __device__ __forceinline__ void stage_rows(bf16* lds, const bf16* __restrict__ b
 template <int HD>
 __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
                                                                   float* __restrict__ lse, int B, int T, int H,
-                                                                  float scale) {
+                                                                  float scale, int zig) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
@@ -464,7 +464,10 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
   stage_rows<L::KLD, HD, RES_MAXT>(sK, Kb, ts, T, Tp, tid);  // rows >= T are zero-filled
   stage_rows<L::VLD, HD, RES_MAXT>(sV, Vb, ts, T, Tp, tid);
   __syncthreads();
-  const int qg = 2 * w + half;
+  // zig: waves w..w+3 of every other row of four take their query groups in reverse, so the four
+  // waves sharing a SIMD (w, w+4, w+8, w+12) carry 18 causal tiles each instead of 16 / 20
+  const int wk = (zig && (w & 4)) ? (w | 3) - (w & 3) : w;
+  const int qg = 2 * wk + half;
   if (qg * 16 >= T) return;  // no barrier below
   const int q = qg * 16 + j;
   bf16x8 qf[KC];
@@ -1046,8 +1049,9 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
                  hipStream_t st) {
   if (use_resident(T, HD)) {
     allow_lds(attn_fwd_res_kernel<32>, res_lds_fwd(T, HD));
+    // flags bit 0: plain wave -> query-group order (A/B of the SIMD-balanced order)
     hipLaunchKernelGGL(attn_fwd_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_fwd(T, HD), st, qkv, o,
-                       lse, B, T, H, scale);
+                       lse, B, T, H, scale, (int)!(flags & 1));
     DTC_CHECK_LAUNCH();
     return 0;
   }

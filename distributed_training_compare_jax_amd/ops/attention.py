@@ -21,8 +21,9 @@ from . import _native as N
 from .gemm import _workspace
 
 
-def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None):
-    """qkv [B,T,3*H*hd] → (o [B,T,H*hd], lse [B,H,T] fp32, natural-log units)."""
+def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None, flags: int = 0):
+    """qkv [B,T,3*H*hd] → (o [B,T,H*hd], lse [B,H,T] fp32, natural-log units).  ``flags`` bit 0:
+    the resident kernel's plain wave → query-group order (A/B)."""
     B, T, C3 = qkv.shape
     hd = C3 // (3 * n_heads)
     scale = scale if scale is not None else hd ** -0.5
@@ -40,7 +41,7 @@ def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None):
         raise NotImplementedError(f"attention kernel supports head_dim 32/64, got {hd}")
     o = torch.empty(B, T, n_heads * hd, dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty(B, n_heads, T, dtype=torch.float32, device=qkv.device)
-    N.check(N.lib().dtc_attn_fwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, T, n_heads, hd, 0, scale,
+    N.check(N.lib().dtc_attn_fwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, T, n_heads, hd, int(flags), scale,
                                  N.stream_ptr(qkv.device)), "dtc_attn_fwd")
     return o, lse
 
@@ -71,7 +72,7 @@ def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Te
     L = N.lib()
     ws = _workspace(qkv.device, int(L.dtc_attn_bwd_workspace_bytes(B, T, n_heads, hd)))
     N.check(L.dtc_attn_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), int(flags),
-                           B, T, n_heads, hd, 0, scale, ws.data_ptr(), ws.numel(), N.stream_ptr(qkv.device)),
+                           B, T, n_heads, hd, int(flags), scale, ws.data_ptr(), ws.numel(), N.stream_ptr(qkv.device)),
             "dtc_attn_bwd")
     return dqkv
 
