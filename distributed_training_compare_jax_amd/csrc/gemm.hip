@@ -931,15 +931,16 @@ __device__ __forceinline__ int dimg_mn_swz(int r) {
   return 2 * ((r & 3) | ((r >> 1) & 4));                      // >= 256-B rows: 8 windows
 }
 
-template <int R, bool KMAJ>
+template <int R, bool KMAJ, int NW = 4>
 struct DImg {
   static constexpr int ELEMS = R * 64;
-  static constexpr int NI = ELEMS * 2 / 1024 / 4;  // 1-KB DMA instructions per wave (4 waves)
+  static constexpr int NI = ELEMS * 2 / 1024 / NW;  // 1-KB DMA instructions per wave (NW waves)
+  static_assert(NI >= 1, "operand image smaller than one DMA instruction per wave");
   __device__ __forceinline__ static void dma(const bf16* __restrict__ X, long ldx, int r0, int rmax, int k0, bf16* img,
                                              int wave, int lane) {
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
-      const int blk = q * 4 + wave;
+      const int blk = q * NW + wave;
       const bf16* src;
       if (KMAJ) {
         const int row = blk * 8 + (lane >> 3);
@@ -1103,6 +1104,172 @@ gemm_dma_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B
     for (int j = 0; j < TM; ++j) {
       const int m = m0 + wm * WM + j * 16 + (lane & 15);
       const int n = n0 + wn * WN + i * 16 + g4;
+      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+    }
+}
+
+// ============================================================================================
+// 8-wave DMA-ring layer GEMM (512 threads, WGM x WGN waves, one block per CU).  The 4-wave kernels
+// above run at 2 blocks/CU (register-staged) or 1 block/CU with one wave per SIMD (DMA): their main
+// loops fill LDS at ~45 GB/s per CU, which bounds every layer GEMM of the reference step at its 1-2
+// tiles per CU.  Two waves per SIMD over an NSTAGE global_load_lds ring keep more bytes in flight
+// and give each SIMD a second wave to issue under the first one's LDS reads: at the reference shapes
+// the main loops run 20-40 % faster (benchmarks/gemm_dma8_micro.hip).  Same operand images,
+// swizzles, counted-vmcnt/raw-barrier ring and epilogues as gemm_dma_kernel; the bf16 epilogues go
+// through a per-wave LDS stage when the wave tile is 64 columns wide (full 128-B output rows).
+template <int BM, int BN, int NSTAGE, int WGM, int WGN, bool AK, bool BKM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(64 * WGM * WGN, 1)
+gemm_dmaw_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+                 int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+  constexpr int NW = WGM * WGN;
+  using IA = DImg<BM, AK, NW>;
+  using IB = DImg<BN, BKM, NW>;
+  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
+  constexpr int G = IA::NI + IB::NI;  // DMA instructions per thread per K-tile
+  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  constexpr int LDS_BYTES = NSTAGE * STAGE * 2;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int ntiles = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, ntiles * split);
+  const int tile = lid % ntiles, z = lid / ntiles;
+  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+  const int gm_eff = min(gm, tiles_m - grp * gm);
+  const int m0 = (grp * gm + in_g % gm_eff) * BM, n0 = (in_g / gm_eff) * BN;
+  const int kbeg = z * k_per_split;
+  const int nk = min(k_per_split, K - kbeg) / 64;
+  const int g4 = 4 * (lane >> 4);
+  const int mb = m0 + wm * WM, nb = n0 + wn * WN;
+
+  // epilogue operands issued ahead of the main loop (their latency hides under it)
+  constexpr bool STAGED16 = !OUTF32 && WN == 64 && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU) &&
+                            NW * WM * 64 * 2 <= LDS_BYTES;
+  constexpr bool ST32 = DTC_STAGE_F32 && (WN == 64 || WN == 32) && BM * BN * 4 <= LDS_BYTES;
+  f32x4 bpre[TN];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = nb + i * 16 + g4;
+    bpre[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (split == 1 && e.bias) {
+      if (n + 4 <= N) bpre[i] = *(const f32x4*)(e.bias + n);
+      else for (int r = 0; r < 4; ++r) if (n + r < N) bpre[i][r] = e.bias[n + r];
+    }
+  }
+  constexpr bool PRE_U = EPI == EPI_DGELU;
+  bf16x4 upre[PRE_U ? TN : 1][PRE_U ? TM : 1];
+  if constexpr (PRE_U) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = mb + j * 16 + (lane & 15), n = nb + i * 16 + g4;
+        upre[i][j] = (m < M && n + 4 <= N) ? *(const bf16x4*)((const bf16*)e.aux + (long)m * e.ldaux + n) : bf16x4{};
+      }
+  }
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < NSTAGE - 1; ++st)
+    if (st < nk) {
+      IA::dma(A, lda, m0, M, kbeg + st * 64, smem + st * STAGE, wave, lane);
+      IB::dma(B, ldb, n0, N, kbeg + st * 64, smem + st * STAGE + IA::ELEMS, wave, lane);
+    }
+  // the epilogue operand loads above sit in the VM queue AHEAD of the ring's DMAs: the first counted
+  // wait covers them too (they have landed long before the first K-tile is needed)
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_tiles<G, NSTAGE - 2>(min(NSTAGE - 2, nk - 1 - kt));  // tile kt landed (this wave)
+    raw_barrier();                                            // ... for every wave; slot kt-1 free
+    const int nt = kt + NSTAGE - 1;
+    if (nt < nk) {
+      bf16* sl = smem + (nt % NSTAGE) * STAGE;
+      IA::dma(A, lda, m0, M, kbeg + nt * 64, sl, wave, lane);
+      IB::dma(B, ldb, n0, N, kbeg + nt * 64, sl + IA::ELEMS, wave, lane);
+    }
+    const bf16* sA = smem + (kt % NSTAGE) * STAGE;
+    const bf16* sB = sA + IA::ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = IA::frag(sA, wm * TM + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = IB::frag(sB, wn * TN + i, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  if constexpr (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  if (nk > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  raw_barrier();  // every wave's last fragment reads are done: the ring is free for the stages
+  if constexpr (ST32) {
+    if (split > 1 || (OUTF32 && (EPI == EPI_STORE || EPI == EPI_RESID))) {
+      const bool sp = split > 1;
+      staged_f32_epilogue<TN, TM, WM, WN>(acc, (float*)smem + wave * (WM * WN), sp ? slab + (long)z * M * N : (float*)e.C,
+                                          sp ? N : e.ldc, mb, nb, M, N, lane, !sp, e.alpha, bpre,
+                                          (!sp && EPI == EPI_RESID) ? (const float*)e.aux : nullptr, e.ldaux,
+                                          (!sp && EPI == EPI_STORE) ? e.beta : 0.f);
+      return;
+    }
+  }
+  if (split > 1) {  // slab without the LDS stage
+    float* sl = slab + (long)z * M * N;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = mb + j * 16 + (lane & 15), n = nb + i * 16 + g4;
+        if (m < M) {
+          float* c = sl + (long)m * N + n;
+          if (n + 4 <= N) *(f32x4*)c = acc[i][j];
+          else for (int r = 0; r < 4; ++r) if (n + r < N) c[r] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if constexpr (STAGED16) {
+    bf16* stg = smem + wave * (WM * 64);
+#pragma unroll
+    for (int pass = 0; pass < (EPI == EPI_GELU ? 2 : 1); ++pass) {
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int i = 0; i < TN; ++i) {
+          bf16x4 ob;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = e.alpha * acc[i][j][r] + bpre[i][r];
+            if constexpr (EPI == EPI_GELU) {  // pass 0: C = gelu'(u), pass 1: aux_out = gelu(u)
+              float gv, dgv;
+              gelu_tanh_and_grad_f(v, gv, dgv);
+              v = pass == 1 ? gv : dgv;
+            }
+            if constexpr (EPI == EPI_DGELU) v *= (float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r];
+            ob[r] = f2bf(v);
+          }
+          stage_put(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
+        }
+      stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = mb + j * 16 + (lane & 15), n = nb + i * 16 + g4;
       if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
     }
 }
@@ -1335,6 +1502,102 @@ int launch_pair_w(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const 
                       : launch_pair_t<D, W64, 64, 64>(a1, p1, a2, p2, st);
 }
 
+// ---- 8-wave DMA plans (gemm_dmaw_kernel) for the layer-GEMM shapes ------------------------------
+// Main loop only, L2-hot and back to back (benchmarks/gemm_dma8_micro.hip) the 8-wave configs beat the
+// 4-wave kernels on every layer shape (e.g. fc1 fwd 10.9 -> 8.8 us, fc1 dgrad 26 -> 18 us), but in the
+// step (rocprofv3, profiles/r2_gemm_w8_instep.md) only two keep a gain once their epilogues and
+// in-step operand traffic are counted: the fp32 residual forwards (out_proj, fc2: 128x64 tiles, 16.1
+// -> 14.4 us per call) and the bias-free small weight gradient (out_proj: 64x128, split 8, 11.4 ->
+// 10.8 us).  The 256x128 bf16 forwards tie (14.4 vs 14.7, 22.9 vs 22.6 us: the all-CU epilogue
+// dominates), the dgrads lose (fc1 dgrad 26.5 -> 34-36 us) and unpairing the fc2 / qkv
+// dgrad+weight-gradient launches loses (37.9 -> 49.6, 36.1 -> 43.4 us).  Those configs stay
+// selectable for experiments (DTC_GEMM_W8=2) but are off in the default plan.
+enum { W_NONE = -1, W_256x128 = 0, W_128x64 = 1, W_64x128 = 2, W_128x128 = 3 };
+
+inline int gemm_w8_mode() {  // DTC_GEMM_W8: 0 = off (A/B), 1 = measured winners (default), 2 = all configs
+  static const int v = [] { const char* s = getenv("DTC_GEMM_W8"); return s ? atoi(s) : 1; }();
+  return v;
+}
+
+struct WPlan {
+  int cfg, split;
+};
+
+// The 8-wave config (and split-K) of a problem, or W_NONE.  Layer-sized problems only (the lm_head
+// GEMMs keep the 256^2 kernel); weight gradients that fuse their bias column sums (has_colsum) stay
+// on the register-staged kernel, which reads dY through registers.
+WPlan dmaw_plan(int layout, int M, int N, int K, int epi, bool f32, bool has_colsum) {
+  WPlan w{W_NONE, 1};
+  const int mode = gemm_w8_mode();
+  if (!mode || K % 64 || M % 8 || N % 8) return w;
+  const bool all = mode >= 2;
+  auto tiles = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (layout == 0) {
+    if (all && !f32 && (epi == EPI_STORE || epi == EPI_GELU) && K <= 1024 && tiles(256, 128) >= 128 &&
+        tiles(256, 128) <= 512)
+      w.cfg = W_256x128;
+    else if (f32 && (epi == EPI_RESID || epi == EPI_STORE) && K <= 4096 && tiles(128, 64) >= 192 && tiles(128, 64) <= 512)
+      w.cfg = W_128x64;
+  } else if (layout == 1) {
+    if (all && !f32 && epi == EPI_DGELU && K <= 1024 && tiles(256, 128) >= 128 && tiles(256, 128) <= 512)
+      w.cfg = W_256x128;
+    else if (all && epi == EPI_STORE && K <= 4096 && tiles(64, 128) >= 192 && tiles(64, 128) <= 512)
+      w.cfg = W_64x128;
+  } else if (layout == 2 && epi == EPI_STORE && f32 && !has_colsum && tiles(128, 128) <= 256 &&
+             (all || tiles(128, 128) < 32)) {
+    // weight gradient (K = tokens): split-K towards 256 blocks of >= 8 k-steps
+    const int nk = K / 64;
+    const int cfg = tiles(128, 128) >= 32 ? W_128x128 : W_64x128;
+    const long t = cfg == W_128x128 ? tiles(128, 128) : tiles(64, 128);
+    int split = 1;
+    while (t * split * 2 <= 256 && nk / (split * 2) >= 8) split *= 2;
+    w.cfg = cfg;
+    w.split = split;
+  }
+  return w;
+}
+
+template <int BM, int BN, int NS, int WGM, int WGN, bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_w(const GemmArgs& a, int split, hipStream_t st) {
+  Epi e;
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
+  e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out; e.colsum = nullptr;
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  e.nparts = tiles_n * WGN;
+  const int ntiles = tiles_m * tiles_n;
+  int gm = tiles_m;
+  if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
+  const int nk = a.K / 64;
+  const int kps = ((nk + split - 1) / split) * 64;
+  if (split > 1 && a.ws_bytes < (long)split * a.M * a.N * 4) return 1005;
+  hipLaunchKernelGGL((gemm_dmaw_kernel<BM, BN, NS, WGM, WGN, AK, BKM, EPI, OUTF32>), dim3(ntiles * split),
+                     dim3(64 * WGM * WGN), 0, st, (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m,
+                     tiles_n, gm, split, kps, (float*)a.workspace, e);
+  DTC_CHECK_LAUNCH();
+  if (split > 1 && !a.defer_reduce) {
+    long MN = (long)a.M * a.N;
+    hipLaunchKernelGGL(splitk_reduce, dim3((int)((MN / 4 + 255) / 256)), dim3(256), 0, st, (const float*)a.workspace, split,
+                       MN, (float*)a.C, a.ldc, a.N, a.beta);
+    DTC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// only the (config, layout, epilogue) combinations dmaw_plan can return are instantiated
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_wcfg(const GemmArgs& a, const WPlan& w, hipStream_t st) {
+  if constexpr (!OUTF32 && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU) && (AK && (BKM || EPI == EPI_DGELU)))
+    if (w.cfg == W_256x128) return launch_w<256, 128, 2, 4, 2, AK, BKM, EPI, OUTF32>(a, w.split, st);
+  if constexpr (AK && BKM && OUTF32 && (EPI == EPI_RESID || EPI == EPI_STORE))
+    if (w.cfg == W_128x64) return launch_w<128, 64, 4, 4, 2, AK, BKM, EPI, OUTF32>(a, w.split, st);
+  if constexpr (EPI == EPI_STORE && ((AK && !BKM) || (!AK && !BKM && OUTF32)))
+    if (w.cfg == W_64x128) return launch_w<64, 128, 4, 2, 4, AK, BKM, EPI, OUTF32>(a, w.split, st);
+  if constexpr (!AK && !BKM && OUTF32 && EPI == EPI_STORE)
+    if (w.cfg == W_128x128) return launch_w<128, 128, 4, 4, 2, AK, BKM, EPI, OUTF32>(a, w.split, st);
+  return 1101;  // not instantiated (dmaw_plan and this table disagree)
+}
+
 }  // namespace
 
 extern "C" {
@@ -1349,6 +1612,9 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   if (a1->M <= 0 || a1->N <= 0 || a2->M <= 0 || a2->N <= 0) return 1100;
   if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
   if (big_split(1, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
+  if (dmaw_plan(1, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
+      dmaw_plan(2, a2->M, a2->N, a2->K, a2->epi, a2->c_f32 != 0, a2->colsum != nullptr).cfg != W_NONE)
+    return 1100;  // the 8-wave kernels run these as two launches
   const Plan p1 = make_plan(a1->M, a1->N, a1->K, (a1->epi == EPI_STORE && a1->c_f32) ? 2 : 0);
   const Plan p2 = make_plan(a2->M, a2->N, a2->K, 1);
   if (p1.split != 1 || p1.bk != 64 || p2.bk != 64) return 1100;
@@ -1363,9 +1629,14 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
 
 int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }
 
-// split-K factor dtc_gemm will use for a weight-gradient (layout 2) problem (1 = none)
-int dtc_gemm_wgrad_split(int M, int N, int K) {
+// split-K factor dtc_gemm will use for a weight-gradient (layout 2) problem (1 = none); has_db: the
+// caller wants the bias gradient fused (GemmArgs.colsum), which pins the register-staged kernel
+int dtc_gemm_wgrad_split(int M, int N, int K, int has_db) {
   if (big_split(2, M, N, K)) return 1;
+  if (!has_db) {
+    const WPlan w = dmaw_plan(2, M, N, K, EPI_STORE, true, false);
+    if (w.cfg != W_NONE) return w.split;
+  }
   return make_plan(M, N, K, 1).split;
 }
 
@@ -1381,7 +1652,8 @@ int dtc_gemm_wgrad_fuses_colsum(int M, int N, int K) {
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   Plan p = make_plan(M, N, K, layout == 2 ? 1 : (layout == 1 ? 2 : 0));
   const int bs = big_split(layout, M, N, K);
-  const int split = bs ? bs : p.split;
+  int split = bs ? bs : p.split;
+  if (layout == 2 && !bs) split = std::max(split, dmaw_plan(2, M, N, K, EPI_STORE, true, false).split);
   return split > 1 ? (long)split * M * N * 4 : 0;
 }
 
@@ -1391,6 +1663,23 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
+  if (a->layout <= 2 && !(a->layout == 2 && a->bias)) {
+    const WPlan w = dmaw_plan(a->layout, a->M, a->N, a->K, epi, f32, a->colsum != nullptr);
+    if (w.cfg != W_NONE) {
+      if (a->layout == 0) {
+        if (epi == EPI_STORE) return f32 ? launch_wcfg<true, true, EPI_STORE, true>(*a, w, st)
+                                         : launch_wcfg<true, true, EPI_STORE, false>(*a, w, st);
+        if (epi == EPI_GELU && !f32) return launch_wcfg<true, true, EPI_GELU, false>(*a, w, st);
+        if (epi == EPI_RESID && f32) return launch_wcfg<true, true, EPI_RESID, true>(*a, w, st);
+      } else if (a->layout == 1) {
+        if (epi == EPI_DGELU && !f32) return launch_wcfg<true, false, EPI_DGELU, false>(*a, w, st);
+        if (epi == EPI_STORE) return f32 ? launch_wcfg<true, false, EPI_STORE, true>(*a, w, st)
+                                         : launch_wcfg<true, false, EPI_STORE, false>(*a, w, st);
+      } else if (epi == EPI_STORE && f32) {
+        return launch_wcfg<false, false, EPI_STORE, true>(*a, w, st);
+      }
+    }
+  }
   if (a->layout == 0) {
     Plan p = make_plan(a->M, a->N, a->K, 0);
     if (big_split(0, a->M, a->N, a->K)) {

@@ -76,7 +76,7 @@ def _declare(lib):
         "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, i, vp], i),
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, i, vp], i),
-        "dtc_gemm_wgrad_split": ([i, i, i], i),
+        "dtc_gemm_wgrad_split": ([i, i, i, i], i),
         "dtc_gemm_pair": ([ctypes.POINTER(GemmArgs), ctypes.POINTER(GemmArgs), vp], i),
         "dtc_gemm_wgrad_fuses_colsum": ([i, i, i], i),
         "dtc_reduce_tasks": ([vp, vp], i),

@@ -235,7 +235,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
     assert dw.dtype == torch.float32 and dw.is_contiguous()
     if red is not None:
         L = N.lib()
-        split = int(L.dtc_gemm_wgrad_split(Nn, K, M))
+        split = int(L.dtc_gemm_wgrad_split(Nn, K, M, 1 if db is not None else 0))
         cs = None
         if db is not None and L.dtc_gemm_wgrad_fuses_colsum(Nn, K, M):
             cs = red.alloc(split * Nn)
@@ -287,7 +287,7 @@ def linear_backward(dy: torch.Tensor, w: torch.Tensor, x: torch.Tensor, dw: torc
     else:
         dx = torch.empty(M, K, dtype=out_dtype, device=dy.device)
         a1 = _gemm_args(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), dx, K)
-    split = int(L.dtc_gemm_wgrad_split(Nn, Kx, M))
+    split = int(L.dtc_gemm_wgrad_split(Nn, Kx, M, 1 if db is not None else 0))
     fuse_cs = db is not None and bool(L.dtc_gemm_wgrad_fuses_colsum(Nn, Kx, M))
     mark = red.off
     cs = red.alloc(split * Nn) if fuse_cs else None

@@ -61,6 +61,27 @@ def test_gemm_resid_gelu(cuda):
     _close(g, G.gelu_tanh(uref), 1e-2, "gelu_g")
 
 
+@pytest.mark.parametrize("N,K", [(512, 512), (512, 2048), (2048, 512), (1536, 512)])
+def test_gemm_reference_shape_epilogues(cuda, N, K):
+    """Every forward / dgrad epilogue at the reference model's Dense shapes (4096 tokens): these are
+    the shapes the 8-wave DMA kernels (csrc/gemm.hip gemm_dmaw_kernel) are planned for."""
+    M = 4096
+    x, w = _r(M, K, seed=41), _r(N, K, scale=0.05, seed=42)
+    b = _r(N, dtype=torch.float32, seed=43)
+    res = _r(M, N, dtype=torch.float32, seed=44)
+    ref = x.float() @ w.float().t() + b
+    _close(G.linear(x, w, b), ref, 1e-2, "store_bf16")
+    _close(G.linear_resid(x, w, b, res), res + ref, 2e-3, "resid")
+    u, g = G.linear_gelu(x, w, b)
+    _close(u, G.gelu_tanh_grad(ref), 1e-2, "gelu_grad")
+    _close(g, G.gelu_tanh(ref), 1e-2, "gelu")
+    dy = _r(M, N, seed=45)  # dgrad through the same weight: [M, N] . [N, K]
+    _close(G.matmul_nn(dy, w), dy.float() @ w.float(), 2e-3, "nn_f32")
+    _close(G.matmul_nn(dy, w, out_dtype=torch.bfloat16), dy.float() @ w.float(), 1e-2, "nn_bf16")
+    uu = _r(M, K, seed=46)
+    _close(G.matmul_nn_dgelu(dy, w, uu), (dy.float() @ w.float()) * uu.float(), 1e-2, "dgelu")
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 512, 1536), (4096, 2048, 512), (4096, 512, 50304), (256, 128, 64), (256, 64, 96),
                                    (256, 32, 64), (2000, 384, 40000)])
 def test_gemm_nn(cuda, M, N, K):
