@@ -1514,7 +1514,7 @@ int launch_pair_w(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const 
 // selectable for experiments (DTC_GEMM_W8=2) but are off in the default plan.
 enum { W_NONE = -1, W_256x128 = 0, W_128x64 = 1, W_64x128 = 2, W_128x128 = 3 };
 
-inline int gemm_w8_mode() {  // DTC_GEMM_W8: 0 = off (A/B), 1 = measured winners (default), 2 = all configs
+inline int gemm_w8_mode() {  // DTC_GEMM_W8 bits: 1 = measured winners (default), 2 = every config, 4 = 128x64 fp32 dgrads
   static const int v = [] { const char* s = getenv("DTC_GEMM_W8"); return s ? atoi(s) : 1; }();
   return v;
 }
@@ -1529,8 +1529,8 @@ struct WPlan {
 WPlan dmaw_plan(int layout, int M, int N, int K, int epi, bool f32, bool has_colsum) {
   WPlan w{W_NONE, 1};
   const int mode = gemm_w8_mode();
-  if (!mode || K % 64 || M % 8 || N % 8) return w;
-  const bool all = mode >= 2;
+  if (!(mode & 7) || K % 64 || M % 8 || N % 8) return w;
+  const bool all = (mode & 2) != 0;
   auto tiles = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   if (layout == 0) {
     if (all && !f32 && (epi == EPI_STORE || epi == EPI_GELU) && K <= 1024 && tiles(256, 128) >= 128 &&
@@ -1543,6 +1543,8 @@ WPlan dmaw_plan(int layout, int M, int N, int K, int epi, bool f32, bool has_col
       w.cfg = W_256x128;
     else if (all && epi == EPI_STORE && K <= 4096 && tiles(64, 128) >= 192 && tiles(64, 128) <= 512)
       w.cfg = W_64x128;
+    else if ((mode & 4) && epi == EPI_STORE && f32 && K <= 4096 && tiles(128, 64) >= 192 && tiles(128, 64) <= 512)
+      w.cfg = W_128x64;
   } else if (layout == 2 && epi == EPI_STORE && f32 && !has_colsum && tiles(128, 128) <= 256 &&
              (all || tiles(128, 128) < 32)) {
     // weight gradient (K = tokens): split-K towards 256 blocks of >= 8 k-steps
@@ -1589,7 +1591,7 @@ template <bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_wcfg(const GemmArgs& a, const WPlan& w, hipStream_t st) {
   if constexpr (!OUTF32 && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU) && (AK && (BKM || EPI == EPI_DGELU)))
     if (w.cfg == W_256x128) return launch_w<256, 128, 2, 4, 2, AK, BKM, EPI, OUTF32>(a, w.split, st);
-  if constexpr (AK && BKM && OUTF32 && (EPI == EPI_RESID || EPI == EPI_STORE))
+  if constexpr (AK && OUTF32 && (EPI == EPI_STORE || (BKM && EPI == EPI_RESID)))
     if (w.cfg == W_128x64) return launch_w<128, 64, 4, 4, 2, AK, BKM, EPI, OUTF32>(a, w.split, st);
   if constexpr (EPI == EPI_STORE && ((AK && !BKM) || (!AK && !BKM && OUTF32)))
     if (w.cfg == W_64x128) return launch_w<64, 128, 4, 2, 4, AK, BKM, EPI, OUTF32>(a, w.split, st);
