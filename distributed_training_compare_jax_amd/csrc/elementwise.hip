@@ -415,6 +415,49 @@ __global__ void fill_kernel(float* __restrict__ x, float v, long n) {
 
 inline int blocks_for(long n, int per_block) { return (int)((n + per_block - 1) / per_block); }
 
+// Batched bf16 transpose of weight matrices (the transposed compute mirror: the fc1 / qkv dgrads
+// run as NT GEMMs on W^T, both operands K-major).  64x64 tiles through LDS: rows of the source and
+// of the destination are read / written as 16-byte vectors.  Task t: src [rows][cols] -> dst
+// [cols][rows], blocks [blk0, blk0 + ceil(rows/64) * ceil(cols/64)).
+constexpr int TR_MAX_TASKS = 32;
+struct TrTask {
+  const bf16* src;
+  bf16* dst;
+  int rows, cols, blk0, pad;
+};
+struct TrBatch {
+  int ntasks, nblocks;
+  TrTask t[TR_MAX_TASKS];
+};
+
+__global__ void __launch_bounds__(256) transpose_batch_kernel(TrBatch batch) {
+  int t = 0;
+  while (t + 1 < batch.ntasks && (int)blockIdx.x >= batch.t[t + 1].blk0) ++t;
+  const TrTask& T = batch.t[t];
+  const int b = blockIdx.x - T.blk0;
+  const int tcols = (T.cols + 63) / 64;
+  const int r0 = (b / tcols) * 64, c0 = (b % tcols) * 64;
+  __shared__ bf16 tile[64][64 + 8];  // +8: a column read walks rows 16 B apart in bank space
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // 64 rows x 8 chunks of 8
+    const int c = tid + i * 256, r = c >> 3, ch = (c & 7) * 8;
+    bf16x8 v{};
+    if (r0 + r < T.rows && c0 + ch + 8 <= T.cols) v = *(const bf16x8*)(T.src + (long)(r0 + r) * T.cols + c0 + ch);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[r][ch + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // destination rows = source columns
+    const int c = tid + i * 256, dr = c >> 3, ch = (c & 7) * 8;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[ch + e][dr];
+    if (c0 + dr < T.cols && r0 + ch + 8 <= T.rows) *(bf16x8*)(T.dst + (long)(c0 + dr) * T.rows + r0 + ch) = v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -549,6 +592,20 @@ int dtc_adamw(float* p, const float* g, float* m, float* v, bf16* mirror, long n
   else  // one 4-element group per thread (the fastest standalone pass)
     hipLaunchKernelGGL(adamw_kernel<false>, dim3(blocks), dim3(256), 0, st, p, g, m, v, mirror, n, n_mirror,
                        step, sumsq, lr, b1, b2, eps, wd, max_norm, enable);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_tr_max_tasks() { return TR_MAX_TASKS; }
+int dtc_tr_task_bytes() { return (int)sizeof(TrTask); }
+
+// rows and cols must be multiples of 8 (16-byte vectors)
+int dtc_transpose_batch(const TrBatch* b, hipStream_t st) {
+  if (b->ntasks <= 0) return 0;
+  if (b->ntasks > TR_MAX_TASKS) return 3010;
+  for (int i = 0; i < b->ntasks; ++i)
+    if (b->t[i].rows % 8 || b->t[i].cols % 8) return 3011;
+  hipLaunchKernelGGL(transpose_batch_kernel, dim3(b->nblocks), dim3(256), 0, st, *b);
   DTC_CHECK_LAUNCH();
   return 0;
 }

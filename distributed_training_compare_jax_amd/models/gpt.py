@@ -232,16 +232,14 @@ class GPTStage:
                 G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
             # paired launches measured per Dense (in-step, us): fc2 44.1 vs 46.8 and qkv 35.6 vs 38.1
             # separate; fc1 48.7 vs 48.1 and out_proj 22.4 vs 21.7 -> those two stay separate
-            dy2 = G.linear_backward(du, f.w(p + "fc1.w"), y2, f.g(p + "fc1.w"), beta, red=red, db=f.g(p + "fc1.b"),
-                                    pair=False)
+            dy2 = self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False)
             tp.all_reduce_(dy2)
             dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
             do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
                                    out_dtype=self.act_dtype, pair=False)
             dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                               self.heads_local).view(batch * T, -1)
-            dy1 = G.linear_backward(dqkv, f.w(p + "qkv.w"), y1, f.g(p + "qkv.w"), beta, red=red,
-                                    db=f.g(p + "qkv.b"))
+            dy1 = self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True)
             tp.all_reduce_(dy1)
             return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
         # MLP (dgrad chain on the main stream, weight grads on the side stream)
@@ -270,6 +268,19 @@ class GPTStage:
         side.flush_one()
         tp.all_reduce_(dy1)
         return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
+
+    def _dgrad_wgrad(self, dy, dense: str, x, beta, red, pair: bool):
+        """dX = dY·W (fp32) and dW/db of a Dense with a bias.  With the transposed weight mirror
+        (``flat.wt``) the dgrad is an NT GEMM on W^T followed by the weight gradient; otherwise the
+        NN dgrad (paired with the weight gradient in one launch when ``pair``)."""
+        f = self.flat
+        wt = f.wt(dense + ".w")
+        if wt is None:
+            return G.linear_backward(dy, f.w(dense + ".w"), x, f.g(dense + ".w"), beta, red=red, db=f.g(dense + ".b"),
+                                     pair=pair)
+        dx = G.linear_resid(dy, wt, None, None)
+        G.wgrad(dy, x, f.g(dense + ".w"), beta, red=red, db=f.g(dense + ".b"))
+        return dx
 
     def _prev_fc2b(self, l: int):
         """fc2.b of the block feeding layer l's input, if this stage owns it (its grad = Σ_rows dx)."""

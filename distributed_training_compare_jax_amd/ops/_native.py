@@ -108,6 +108,9 @@ def _declare(lib):
         "dtc_sum_finish": ([vp, i, vp, vp, vp], i),
         "dtc_adamw": ([vp, vp, vp, vp, vp, l, l, vp, vp, f, f, f, f, f, f, vp, i, vp], i),
         "dtc_cast_f32_bf16": ([vp, vp, l, vp], i),
+        "dtc_transpose_batch": ([vp, vp], i),
+        "dtc_tr_max_tasks": ([], i),
+        "dtc_tr_task_bytes": ([], i),
         "dtc_fill_f32": ([vp, f, l, vp], i),
     }
     for name, (args, res) in sigs.items():

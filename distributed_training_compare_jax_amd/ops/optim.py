@@ -18,6 +18,8 @@ weights — no per-parameter launches, no host sync (graph-capturable).
 
 from __future__ import annotations
 
+import ctypes
+
 from typing import Optional
 
 import torch
@@ -116,6 +118,45 @@ def cast_to_bf16(src: torch.Tensor, dst: torch.Tensor):
         return
     N.check(N.lib().dtc_cast_f32_bf16(src.data_ptr(), dst.data_ptr(), src.numel(), N.stream_ptr(src.device)),
             "dtc_cast_f32_bf16")
+
+
+class _TrTask(ctypes.Structure):
+    """Mirror of ``struct TrTask`` (csrc/elementwise.hip)."""
+
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int), ("cols", ctypes.c_int),
+                ("blk0", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+_TR_MAX = 32
+
+
+class _TrBatch(ctypes.Structure):
+    _fields_ = [("ntasks", ctypes.c_int), ("nblocks", ctypes.c_int), ("t", _TrTask * _TR_MAX)]
+
+
+def transpose_batch(pairs):
+    """dst = src.T for each (src [rows, cols], dst [cols, rows]) bf16 pair: one launch per 32 matrices
+    on GPU (the transposed weight mirror), torch on CPU."""
+    if not pairs:
+        return
+    if not pairs[0][0].is_cuda:
+        for src, dst in pairs:
+            dst.copy_(src.t())
+        return
+    L = N.lib()
+    assert L.dtc_tr_task_bytes() == ctypes.sizeof(_TrTask) and L.dtc_tr_max_tasks() == _TR_MAX
+    for i in range(0, len(pairs), _TR_MAX):
+        chunk = pairs[i:i + _TR_MAX]
+        b = _TrBatch()
+        b.ntasks = len(chunk)
+        blk = 0
+        for j, (src, dst) in enumerate(chunk):
+            rows, cols = src.shape
+            assert tuple(dst.shape) == (cols, rows) and src.is_contiguous() and dst.is_contiguous()
+            b.t[j] = _TrTask(src.data_ptr(), dst.data_ptr(), rows, cols, blk, 0)
+            blk += ((rows + 63) // 64) * ((cols + 63) // 64)
+        b.nblocks = blk
+        N.check(L.dtc_transpose_batch(ctypes.byref(b), N.stream_ptr(src.device)), "dtc_transpose_batch")
 
 
 def fill_(t: torch.Tensor, value: float):

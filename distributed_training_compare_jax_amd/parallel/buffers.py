@@ -73,6 +73,9 @@ class FlatParams:
         self.use_mirror = compute_dtype != torch.float32
         self.mirror = (torch.zeros(max(n_mirror, ALIGN), dtype=compute_dtype, device=self.device)
                        if self.use_mirror else None)
+        # transposed compute mirror (enable_transposed): name -> (slot, [in, out] bf16 view)
+        self.mirror_t: Dict[str, Tuple[Slot, torch.Tensor]] = {}
+        self._mirror_t_buf = None
 
     # -- init -----------------------------------------------------------------
     def init_canonical(self, seed: int):
@@ -87,6 +90,41 @@ class FlatParams:
             from ..ops.optim import cast_to_bf16
 
             cast_to_bf16(self.params[: self.n_mirror], self.mirror[: self.n_mirror])
+            self.refresh_transposed()
+
+    # -- transposed mirror --------------------------------------------------------
+    def enable_transposed(self, names: List[str]):
+        """Keep a transposed bf16 copy ``[in, out]`` of these 2-D mirrored weights (each rebuilt from
+        the mirror after every update: :meth:`refresh_transposed`).  With it a Dense's dgrad
+        dX = dY·W runs as an NT GEMM (both operands K-major) on the 8-wave kernels instead of reading
+        W k-strided (csrc/gemm.hip; measured in the step, profiles/r2_ab_dgrad_nt.log)."""
+        names = [n for n in names if n in self.slots and self.slots[n].spec.mirror and len(self.slots[n].shape) == 2]
+        if not names or not self.use_mirror:
+            return
+        total = sum(self.slots[n].numel for n in names)
+        self._mirror_t_buf = torch.zeros(total, dtype=self.compute_dtype, device=self.device)
+        off = 0
+        for n in names:
+            sl = self.slots[n]
+            rows, cols = sl.shape
+            self.mirror_t[n] = (sl, self._mirror_t_buf[off:off + sl.numel].view(cols, rows))
+            off += sl.numel
+        self.refresh_transposed()
+
+    def refresh_transposed(self, lo: int = 0, hi: int = None):
+        """Rebuild the transposed copies of the weights inside flat[lo:hi] from the bf16 mirror."""
+        if not self.mirror_t:
+            return
+        from ..ops.optim import transpose_batch
+
+        hi = self.numel if hi is None else hi
+        transpose_batch([(self._view(self.mirror, n), t) for n, (sl, t) in self.mirror_t.items()
+                         if sl.offset >= lo and sl.offset + sl.numel <= hi])
+
+    def wt(self, name: str):
+        """Transposed bf16 view ``[in, out]`` of a weight, or None when not kept."""
+        e = self.mirror_t.get(name)
+        return None if e is None else e[1]
 
     # -- views ----------------------------------------------------------------
     def _view(self, buf: torch.Tensor, name: str) -> torch.Tensor:

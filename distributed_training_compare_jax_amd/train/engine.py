@@ -61,6 +61,9 @@ class Engine:
         self.layout = StageLayout(layer_ranges[m.pp_idx], has_embed=m.pp_idx == 0, has_head=m.pp_idx == pp - 1)
         specs = stage_param_specs(model_cfg, self.layout.layers, self.layout.has_embed, self.layout.has_head)
         self.flat = FlatParams(specs, m.tp_idx, tp, self.device, compute_dtype=self.act_dtype)
+        if self.act_dtype == torch.bfloat16 and os.environ.get("DTC_DGRAD_NT", "1") == "1":
+            # fc1 / qkv dgrads as NT GEMMs on a transposed bf16 weight copy (buffers.enable_transposed)
+            self.flat.enable_transposed([f"h.{l}.{n}.w" for l in self.layout.layers for n in ("fc1", "qkv")])
         self.flat.init_canonical(train_cfg.seed)
 
         # ---- step program, comms, model, optimizer

@@ -141,6 +141,8 @@ class FusedAdamW:
         O.adamw_flat(f.params[lo:hi], f.grads[lo:hi], f.exp_avg[lo:hi], f.exp_avg_sq[lo:hi],
                      f.mirror[lo:lo + max(nm, 4)] if nm > 0 else None, nm, self.step_t, self.sumsq, c.lr, c.b1, c.b2,
                      c.eps, c.weight_decay, c.grad_clip, enable=enable, max_blocks=max_blocks)
+        if nm > 0:
+            f.refresh_transposed(lo, hi)
 
     def step(self):
         self.norm()

@@ -176,3 +176,25 @@ def test_fp32_mode_graph_steps(cuda):
     for a, b in zip(losses[False], losses[True]):
         assert abs(a - b) < 1e-4, (losses[False], losses[True])
     assert losses[True][-1] < losses[True][0]
+
+
+def test_dgrad_nt_matches_nn(cuda, monkeypatch):
+    """The fc1 / qkv dgrads on the transposed weight mirror (NT GEMMs, the 8-wave kernels at the
+    reference shapes) give the same gradients as the NN dgrads (summation order only)."""
+    grads = {}
+    for nt in ("1", "0"):
+        monkeypatch.setenv("DTC_DGRAD_NT", nt)
+        eng, mc = _engine(cuda, use_graph=False, preset="ref", vocab=50258, batch=8, dropout=0.1)
+        assert (eng.flat.wt("h.0.fc1.w") is not None) == (nt == "1")
+        eng.set_batch(next(get_batch_iterator(8, mc.max_seq_len + 1)))
+        eng.run_step()
+        torch.cuda.synchronize()
+        grads[nt] = {n: eng.flat.g(n).float().cpu() for n in eng.flat.slots}
+        if nt == "1":
+            for n in ("h.3.fc1.w", "h.7.qkv.w"):  # the transposed copy tracks the updated mirror
+                assert torch.equal(eng.flat.wt(n).cpu(), eng.flat.w(n).cpu().t())
+        del eng
+    for n, g in grads["1"].items():
+        go = grads["0"][n]
+        err = ((g - go).norm() / (go.norm() + 1e-12)).item()
+        assert err < 1e-2, f"{n}: NT vs NN dgrad relative grad difference {err:.3e}"

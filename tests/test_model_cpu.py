@@ -163,3 +163,26 @@ def test_adamw_matches_optax_semantics():
         rp = rp - 3e-4 * (mh / (vh.sqrt() + 1e-8) + 0.1 * rp)
         assert step.item() == t
     assert torch.allclose(p.double(), rp, atol=1e-6)
+
+
+def test_transposed_mirror_tracks_updates():
+    """FlatParams.enable_transposed: the [in, out] copy equals the mirror's transpose after init and
+    after every optimizer range update (CPU: fp32 'mirror' is the params; exercised via bf16 on GPU)."""
+    from distributed_training_compare_jax_amd.models.params import stage_param_specs
+    from distributed_training_compare_jax_amd.ops import optim as O
+    from distributed_training_compare_jax_amd.parallel.buffers import FlatParams
+
+    mc = model_config_from_preset("tiny", vocab_size=1000)
+    specs = stage_param_specs(mc, range(mc.n_layers), True, True)
+    f = FlatParams(specs, 0, 1, "cpu", compute_dtype=torch.bfloat16)
+    f.enable_transposed(["h.0.fc1.w", "h.1.qkv.w"])
+    f.init_canonical(0)
+    for n in ("h.0.fc1.w", "h.1.qkv.w"):
+        assert torch.equal(f.wt(n), f.w(n).t())
+    f.params.add_(0.5)
+    f.refresh_mirror()
+    assert torch.equal(f.wt("h.0.fc1.w"), f.w("h.0.fc1.w").t())
+    assert f.wt("h.0.qkv.w") is None
+    pairs = [(torch.randn(24, 40).bfloat16(), torch.empty(40, 24, dtype=torch.bfloat16))]
+    O.transpose_batch(pairs)
+    assert torch.equal(pairs[0][1], pairs[0][0].t())
