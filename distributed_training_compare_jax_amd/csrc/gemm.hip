@@ -1536,7 +1536,8 @@ WPlan dmaw_plan(int layout, int M, int N, int K, int epi, bool f32, bool has_col
     if (all && !f32 && (epi == EPI_STORE || epi == EPI_GELU) && K <= 1024 && tiles(256, 128) >= 128 &&
         tiles(256, 128) <= 512)
       w.cfg = W_256x128;
-    else if (f32 && (epi == EPI_RESID || epi == EPI_STORE) && K <= 4096 && tiles(128, 64) >= 192 && tiles(128, 64) <= 512)
+    else if ((f32 ? (epi == EPI_RESID || epi == EPI_STORE) : epi == EPI_STORE) && K <= 4096 && tiles(128, 64) >= 192 &&
+             tiles(128, 64) <= 512)
       w.cfg = W_128x64;
   } else if (layout == 1) {
     if (all && !f32 && epi == EPI_DGELU && K <= 1024 && tiles(256, 128) >= 128 && tiles(256, 128) <= 512)
@@ -1591,7 +1592,7 @@ template <bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_wcfg(const GemmArgs& a, const WPlan& w, hipStream_t st) {
   if constexpr (!OUTF32 && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU) && (AK && (BKM || EPI == EPI_DGELU)))
     if (w.cfg == W_256x128) return launch_w<256, 128, 2, 4, 2, AK, BKM, EPI, OUTF32>(a, w.split, st);
-  if constexpr (AK && OUTF32 && (EPI == EPI_STORE || (BKM && EPI == EPI_RESID)))
+  if constexpr (AK && ((OUTF32 && (EPI == EPI_STORE || (BKM && EPI == EPI_RESID))) || (BKM && !OUTF32 && EPI == EPI_STORE)))
     if (w.cfg == W_128x64) return launch_w<128, 64, 4, 4, 2, AK, BKM, EPI, OUTF32>(a, w.split, st);
   if constexpr (EPI == EPI_STORE && ((AK && !BKM) || (!AK && !BKM && OUTF32)))
     if (w.cfg == W_64x128) return launch_w<64, 128, 4, 2, 4, AK, BKM, EPI, OUTF32>(a, w.split, st);

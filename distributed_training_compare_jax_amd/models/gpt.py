@@ -235,8 +235,13 @@ class GPTStage:
             dy2 = self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False)
             tp.all_reduce_(dy2)
             dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
-            do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
-                                   out_dtype=self.act_dtype, pair=False)
+            wto = f.wt(p + "out.w")
+            if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
+                do = G.linear(dx2_c, wto)
+                G.wgrad(dx2_c, o, f.g(p + "out.w"), beta, red=red)
+            else:
+                do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
+                                       out_dtype=self.act_dtype, pair=False)
             dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                               self.heads_local).view(batch * T, -1)
             dy1 = self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True)
