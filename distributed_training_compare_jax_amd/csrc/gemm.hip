@@ -1698,6 +1698,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
       p.bm = p.bn = 128;
       return launch_t<128, 128, true, true, EPI_LMHEAD, false>(*a, p, st); }
     if (epi == EPI_GELU) return launch_sz<true, true, EPI_GELU, false>(*a, p, st);
+    if (epi == EPI_DGELU && !f32) return launch_sz<true, true, EPI_DGELU, false>(*a, p, st);  // NT dgrad (W^T)
     if (epi == EPI_RESID) return launch_sz<true, true, EPI_RESID, true>(*a, p, st);
     if (epi == EPI_STORE) return f32 ? launch_sz<true, true, EPI_STORE, true>(*a, p, st)
                                      : launch_sz<true, true, EPI_STORE, false>(*a, p, st);

@@ -211,6 +211,19 @@ def matmul_nn_dgelu(dy: torch.Tensor, w: torch.Tensor, u: torch.Tensor) -> torch
     return du
 
 
+def matmul_nt_dgelu(dy: torch.Tensor, wt: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """dU = (dY·W) ⊙ u with W given transposed (``wt`` = Wᵀ, [K, N]): the fc2 dgrad fused with the
+    GELU backward as an NT GEMM (both operands K-major)."""
+    M = dy.shape[0]
+    K = wt.shape[0]
+    if N.library_path(dy):
+        return ((_f32(dy) @ _f32(wt).t()) * _f32(u)).to(u.dtype)
+    _check2d(dy, "dy"); _check2d(wt, "wt")
+    du = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    _gemm_native(0, M, K, dy.shape[1], dy, dy.stride(0), wt, wt.stride(0), du, K, epi=N.EPI_DGELU, aux=u, ldaux=K)
+    return du
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0, red=None,
           db: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dW[N,K] = β·dW + dY[M,N]ᵀ·X[M,K]  (fp32 ``dw`` is a view into the flat grad buffer);

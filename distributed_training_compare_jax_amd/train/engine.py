@@ -63,9 +63,8 @@ class Engine:
         self.flat = FlatParams(specs, m.tp_idx, tp, self.device, compute_dtype=self.act_dtype)
         if self.act_dtype == torch.bfloat16 and os.environ.get("DTC_DGRAD_NT", "1") == "1":
             # fc1 / qkv dgrads as NT GEMMs on a transposed bf16 weight copy (buffers.enable_transposed)
-            nt = os.environ.get("DTC_DGRAD_NT_OUT", "1") == "1"
-            self.flat.enable_transposed([f"h.{l}.{n}.w" for l in self.layout.layers
-                                         for n in (("fc1", "qkv", "out") if nt else ("fc1", "qkv"))])
+            dense = ["fc1", "qkv", "out"] + (["fc2"] if os.environ.get("DTC_DGRAD_NT_FC2", "0") == "1" else [])
+            self.flat.enable_transposed([f"h.{l}.{n}.w" for l in self.layout.layers for n in dense])
         self.flat.init_canonical(train_cfg.seed)
 
         # ---- step program, comms, model, optimizer
