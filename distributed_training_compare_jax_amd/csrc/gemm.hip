@@ -1421,8 +1421,9 @@ int launch_sz(const GemmArgs& a, const Plan& p, hipStream_t st) {
 
 
 // The 256^2 kernel pays on lm_head-sized problems.  Returns the split-K factor (0 = use the
-// 128/64 kernels).  layout 0 (fwd): no split; layout 1 (dgrad through the lm_head, K = vocab):
-// split so ~256 blocks run; layout 2 (wgrad): no split (a 103 MB fp32 output; extra slab passes
+// 128/64 kernels).  layout 0 (fwd): whole tiles; layout 1 (dgrad through the lm_head, K = vocab):
+// split so ~256 blocks run (so does layout 0 at K >= 16384: the same dgrad as an NT GEMM on a
+// transposed lm_head weight, ~25% faster main loop with both operands K-major); layout 2 (wgrad): no split (a 103 MB fp32 output; extra slab passes
 // cost more than the last partial wave of tiles).
 int big_split(int layout, int M, int N, int K) {
   // DTC_GEMM256: bit mask of layouts allowed to use it (1 fwd, 2 dgrad, 4 wgrad; default all)
@@ -1432,10 +1433,9 @@ int big_split(int layout, int M, int N, int K) {
   if (layout == 2 && M % 8) return 0;              // MN-major A extent (wgrad)
   static const int min_tiles = [] { const char* v = getenv("DTC_BIG_MIN_TILES"); return v ? atoi(v) : 512; }();
   const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
-  if (layout == 0) return t >= min_tiles ? 1 : 0;
   if (layout == 2) return (t >= 256 && K >= 1024) ? 1 : 0;
-  if (K < 16384) return t >= min_tiles ? 1 : 0;   // dgrad, ordinary K: whole tiles
-  if (t > 256) return 0;                           // dgrad through the vocab: split-K
+  if (K < 16384) return t >= min_tiles ? 1 : 0;   // ordinary K: whole tiles
+  if (t > 256) return 0;                           // dgrad through the vocab (NN, or NT on W^T): split-K
   int split = (int)std::max(1L, 256 / t);
   while (split > 1 && (K / 64) / split < 8) --split;
   return split;
@@ -1685,7 +1685,9 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   }
   if (a->layout == 0) {
     Plan p = make_plan(a->M, a->N, a->K, 0);
-    if (big_split(0, a->M, a->N, a->K)) {
+    const int bs0 = big_split(0, a->M, a->N, a->K);
+    if (bs0 > 1 && epi == EPI_STORE && f32) return launch_big<true, true, EPI_STORE, true>(*a, bs0, st);
+    if (bs0 == 1) {
       if (epi == EPI_LMHEAD) return launch_big<true, true, EPI_LMHEAD, false>(*a, 1, st);
       if (epi == EPI_GELU) return launch_big<true, true, EPI_GELU, false>(*a, 1, st);
       if (epi == EPI_RESID) return launch_big<true, true, EPI_RESID, true>(*a, 1, st);

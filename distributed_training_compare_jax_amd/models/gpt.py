@@ -341,7 +341,8 @@ class GPTStage:
         dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale, colpart=True)
         # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
         # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
-        dyf = G.matmul_nn(dlogits, f.w("lm_head.w"))
+        wt = f.wt("lm_head.w")  # transposed mirror: NT split-K dgrad, both operands K-major
+        dyf = G.linear_resid(dlogits, wt, None, None) if wt is not None else G.matmul_nn(dlogits, f.w("lm_head.w"))
         red = self.red
         wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
                                                 G.colsum(cp, f.g("lm_head.b"), beta, red=red))

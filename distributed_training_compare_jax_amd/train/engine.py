@@ -62,9 +62,10 @@ class Engine:
         specs = stage_param_specs(model_cfg, self.layout.layers, self.layout.has_embed, self.layout.has_head)
         self.flat = FlatParams(specs, m.tp_idx, tp, self.device, compute_dtype=self.act_dtype)
         if self.act_dtype == torch.bfloat16 and os.environ.get("DTC_DGRAD_NT", "1") == "1":
-            # fc1 / qkv dgrads as NT GEMMs on a transposed bf16 weight copy (buffers.enable_transposed)
+            # Dense / lm_head dgrads as NT GEMMs on a transposed bf16 weight copy (buffers.enable_transposed)
             dense = ["fc1", "qkv", "out"] + (["fc2"] if os.environ.get("DTC_DGRAD_NT_FC2", "0") == "1" else [])
-            self.flat.enable_transposed([f"h.{l}.{n}.w" for l in self.layout.layers for n in dense])
+            head = ["lm_head.w"] if os.environ.get("DTC_DGRAD_NT_HEAD", "1") == "1" else []
+            self.flat.enable_transposed([f"h.{l}.{n}.w" for l in self.layout.layers for n in dense] + head)
         self.flat.init_canonical(train_cfg.seed)
 
         # ---- step program, comms, model, optimizer

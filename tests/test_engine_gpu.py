@@ -192,7 +192,7 @@ def test_dgrad_nt_matches_nn(cuda, monkeypatch):
         torch.cuda.synchronize()
         grads[nt] = {n: eng.flat.g(n).float().cpu() for n in eng.flat.slots}
         if nt == "1":
-            for n in ("h.3.fc1.w", "h.7.qkv.w", "h.5.out.w", "h.1.fc2.w"):  # the copies track the updated mirror
+            for n in ("h.3.fc1.w", "h.7.qkv.w", "h.5.out.w", "h.1.fc2.w", "lm_head.w"):  # the copies track the updated mirror
                 assert torch.equal(eng.flat.wt(n).cpu(), eng.flat.w(n).cpu().t())
         del eng
     for n, g in grads["1"].items():

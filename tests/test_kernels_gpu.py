@@ -82,6 +82,13 @@ def test_gemm_reference_shape_epilogues(cuda, N, K):
     _close(G.matmul_nn_dgelu(dy, w, uu), (dy.float() @ w.float()) * uu.float(), 1e-2, "dgelu")
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 512, 50304), (2048, 256, 50304), (4096, 512, 20480)])
+def test_gemm_nt_splitk_vocab(cuda, M, N, K):
+    """The lm_head dgrad as an NT GEMM on the transposed weight (K = vocab): 256^2 tiles, split-K slabs."""
+    dy, wt = _r(M, K, seed=47), _r(N, K, scale=0.05, seed=48)
+    _close(G.linear_resid(dy, wt, None, None), dy.float() @ wt.float().t(), 2e-3, "nt_splitk")
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 512, 1536), (4096, 2048, 512), (4096, 512, 50304), (256, 128, 64), (256, 64, 96),
                                    (256, 32, 64), (2000, 384, 40000)])
 def test_gemm_nn(cuda, M, N, K):
