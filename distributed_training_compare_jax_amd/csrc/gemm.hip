@@ -301,7 +301,8 @@ __device__ __forceinline__ void staged_f32_epilogue(const f32x4 (&acc)[TN][TM], 
 template <int TN, int TM>
 struct EpiPre {
   f32x4 bb[TN];
-  int lab[TM];
+  int lab[TM];                   // label of fragment row j*16 + (lane & 15)   (register epilogue)
+  int labr[(TM * 16 + 63) / 64];  // label of wave row q*64 + lane               (LDS-staged epilogue)
 };
 
 template <int TN, int TM>
@@ -318,58 +319,100 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int m_base, int n_bas
     const int m = m_base + j * 16 + (lane & 15);
     pre.lab[j] = (labels && m < e.M) ? e.labels[m] - e.vocab_start : -1;
   }
+#pragma unroll
+  for (int q = 0; q < (TM * 16 + 63) / 64; ++q) {
+    const int m = m_base + q * 64 + lane;
+    pre.labr[q] = (labels && m < e.M) ? e.labels[m] - e.vocab_start : -1;
+  }
 }
 
-template <int TN, int TM>
-__device__ __forceinline__ void lmhead_epilogue(const f32x4 (&acc)[TN][TM], const Epi& e, int m_base, int n_base,
-                                                int part_idx, int lane, const EpiPre<TN, TM>& pre,
-                                                bf16* stage = nullptr) {
+// Per-row (max, sum exp) of this wave's TN*16 logits + bf16 logits.  FULL: every column of the
+// wave is a real vocab entry (all tiles but the last), so no per-element validity selects.  The
+// staged form reads the label logit back from the LDS stage (one read per row) instead of
+// comparing every element against the label, and folds (v - max)*log2(e) into one fma.
+template <int TN, int TM, bool FULL, bool STAGED, bool ACCB>
+__device__ __forceinline__ void lmhead_rows(const f32x4 (&acc)[TN][TM], const Epi& e, int m_base, int n_base,
+                                            int part_idx, int lane, const EpiPre<TN, TM>& pre, bf16* stage) {
+  constexpr float L2E = 1.4426950408889634f;
   const int g4 = 4 * (lane >> 4);
   bool okv[TN][4];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {  // validity: once per column group, shared by all TM rows
     const int n = n_base + i * 16 + g4;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) okv[i][r] = (n + r) < e.n_valid && (n + r) < e.N;
+    for (int r = 0; r < 4; ++r) okv[i][r] = FULL || ((n + r) < e.n_valid && (n + r) < e.N);
   }
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
     const int m = m_base + j * 16 + (lane & 15);
     const bool mvalid = m < e.M;
-    const int lab = pre.lab[j];
     float v[TN][4];
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
       const int n = n_base + i * 16 + g4;
-      bf16x4 ob;
+      bf16x4 ob = __builtin_convertvector(ACCB ? acc[i][j] : acc[i][j] + pre.bb[i], bf16x4);  // 2 cvt_pk
+      const u32x2 pk = __builtin_bit_cast(u32x2, ob);  // the rounded logits back as f32: 1 op each
+      const float rv[4] = {__uint_as_float(pk[0] << 16), __uint_as_float(pk[0] & 0xffff0000u),
+                           __uint_as_float(pk[1] << 16), __uint_as_float(pk[1] & 0xffff0000u)};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        ob[r] = f2bf(acc[i][j][r] + pre.bb[i][r]);
-        v[i][r] = okv[i][r] ? (float)ob[r] : -INFINITY;
+        v[i][r] = okv[i][r] ? rv[r] : -INFINITY;
         mx = fmaxf(mx, v[i][r]);
       }
+      if (!FULL) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) if (!okv[i][r]) ob[r] = f2bf(-INFINITY);
-      if (stage) stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
-      else if (mvalid && n + 4 <= e.N) *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
-      if (lab >= n && lab < n + 4 && lab < e.n_valid) e.label_out[m] = v[i][lab - n];
+        for (int r = 0; r < 4; ++r) if (!okv[i][r]) ob[r] = f2bf(-INFINITY);
+      }
+      if (STAGED) {
+        stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
+      } else {
+        if (mvalid && n + 4 <= e.N) *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
+        const int lab = pre.lab[j];
+        if (lab >= n && lab < n + 4 && lab < e.n_valid) e.label_out[m] = v[i][lab - n];
+      }
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float sum = 0.f;
-    if (mx != -INFINITY) {
+    if (FULL || mx != -INFINITY) {
+      const float mxl = mx * L2E;
+      sum = __builtin_amdgcn_exp2f(fmaf(v[0][0], L2E, -mxl));
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sum += __expf(v[i][r] - mx);
+        for (int r = (i == 0); r < 4; ++r) sum += __builtin_amdgcn_exp2f(fmaf(v[i][r], L2E, -mxl));
     }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
     // part-major [nparts][M]: the 16 rows of a fragment write one contiguous 128-B line
     if (mvalid && lane < 16) *(f32x2*)(e.part + ((long)part_idx * e.M + m) * 2) = f32x2{mx, sum};
   }
-  if (stage) stage_out<TM * 16>(stage, (bf16*)e.C, e.ldc, m_base, n_base, e.M, e.N, lane);
+  if (STAGED) {
+    // label logit: row q*64 + lane, if its label falls in this wave's columns (same wave wrote the
+    // stage: LDS ops of one wave complete in order)
+#pragma unroll
+    for (int q = 0; q < (TM * 16 + 63) / 64; ++q) {
+      const int row = q * 64 + lane, m = m_base + row, d = pre.labr[q] - n_base;
+      if (row < TM * 16 && m < e.M && d >= 0 && d < TN * 16 && pre.labr[q] < e.n_valid)
+        e.label_out[m] = (float)stage[row * 64 + ((((d >> 2) ^ (row & 15))) << 2) + (d & 3)];
+    }
+    stage_out<TM * 16>(stage, (bf16*)e.C, e.ldc, m_base, n_base, e.M, e.N, lane);
+  }
+}
+
+// lm_head epilogue: logits (bf16) + per-row partial (max, sum exp) over this wave's TN*16 columns +
+// the label logit.  acc[i][j]: lane holds C[m_base + 16j + (lane&15)][n_base + 16i + 4(lane>>4) + r].
+// Epilogue operands loaded up front (all loads in flight together, ideally before the main loop
+// ends): one bias vector per column group and one label per fragment row.  ACCB: the accumulators
+// started from the bias (the main loop added onto it), so no bias add here.
+template <int TN, int TM, bool STAGED = false, bool ACCB = false>
+__device__ __forceinline__ void lmhead_epilogue(const f32x4 (&acc)[TN][TM], const Epi& e, int m_base, int n_base,
+                                                int part_idx, int lane, const EpiPre<TN, TM>& pre,
+                                                bf16* stage = nullptr) {
+  const bool full = n_base + TN * 16 <= min(e.n_valid, e.N);  // wave-uniform
+  if (full) lmhead_rows<TN, TM, true, STAGED, ACCB>(acc, e, m_base, n_base, part_idx, lane, pre, stage);
+  else lmhead_rows<TN, TM, false, STAGED, ACCB>(acc, e, m_base, n_base, part_idx, lane, pre, stage);
 }
 
 // LDS elements of the register-staged kernel (two stages of A and B tiles)
@@ -810,6 +853,12 @@ gemm256_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B,
   if (split == 1 && (EPI == EPI_LMHEAD || EPI == EPI_STORE))
     epi_prefetch<TN, TM>(e, m0 + wm * 128, n0 + wn * 64, lane, EPI == EPI_LMHEAD, pre);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (EPI == EPI_LMHEAD && split == 1) {  // the bias is the accumulators' starting value
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = pre.bb[i];
+  }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const bf16* sA = smem + (kt & 1) * 2 * IMG;
@@ -850,7 +899,7 @@ gemm256_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B,
   }
   bf16* stage = smem + wave * (128 * 64);  // main-loop buffers are free after the last barrier
   if (EPI == EPI_LMHEAD) {
-    lmhead_epilogue<TN, TM>(acc, e, m0 + wm * 128, n0 + wn * 64, tn_idx * 4 + wn, lane, pre, stage);
+    lmhead_epilogue<TN, TM, true, true>(acc, e, m0 + wm * 128, n0 + wn * 64, tn_idx * 4 + wn, lane, pre, stage);
     return;
   }
   if (EPI == EPI_STORE && !OUTF32) {
