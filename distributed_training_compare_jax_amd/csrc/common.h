@@ -83,29 +83,29 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
-// gelu (tanh approximation, jax.nn.gelu(approximate=True) = flax nn.gelu default)
-// tanh via one v_exp_f32 + one v_rcp_f32 (libm tanhf is ~40 VALU ops and made the fc1/fc2
-// epilogues VALU-bound: 11-15 VALU per MFMA in the PMC profile).  |err| ~1e-7, far below bf16.
-__device__ __forceinline__ float fast_tanh(float z) {
-  const float e = __expf(2.f * fminf(fmaxf(z, -15.f), 15.f));
-  return 1.f - 2.f * __frcp_rn(e + 1.f);
+// gelu (tanh approximation, jax.nn.gelu(approximate=True) = flax nn.gelu default), written with
+// h = (1 + tanh(x)) / 2 = 1 / (1 + exp(-2x)),  x = k0 (u + k1 u^3):
+//   gelu(u) = u h,   gelu'(u) = h + u h (1 - h) 2 k0 (1 + 3 k1 u^2)
+// = one v_exp_f32 + one v_rcp_f32 + ~8 VALU, no clamps (exp2 -> inf gives h = 0, -> 0 gives h = 1).
+// The earlier tanh form (IEEE-rounded division: div_scale/div_fmas/div_fixup per element) made
+// the fc1 epilogue ~2x longer.  |err| vs fp32 tanh ~1e-6 relative, far below bf16.
+__device__ __forceinline__ float gelu_h(float u, float s /* u*u */) {
+  constexpr float L2E = 1.4426950408889634f, k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float arg = u * fmaf(s, -2.f * k0 * k1 * L2E, -2.f * k0 * L2E);  // -2x log2(e)
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(arg));
 }
-__device__ __forceinline__ float gelu_tanh_f(float u) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float t = fast_tanh(k0 * (u + k1 * u * u * u));
-  return 0.5f * u * (1.f + t);
-}
-// gelu(u) and gelu'(u) sharing one tanh (the fc1 epilogue stores gelu'(u) for the backward)
+__device__ __forceinline__ float gelu_tanh_f(float u) { return u * gelu_h(u, u * u); }
+// gelu(u) and gelu'(u) sharing one exp + rcp (the fc1 epilogue stores gelu'(u) for the backward)
 __device__ __forceinline__ void gelu_tanh_and_grad_f(float u, float& gv, float& dgv) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float t = fast_tanh(k0 * (u + k1 * u * u * u));
-  gv = 0.5f * u * (1.f + t);
-  dgv = 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
+  constexpr float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float s = u * u, h = gelu_h(u, s);
+  gv = u * h;
+  dgv = fmaf(u * fmaf(s, 6.f * k0 * k1, 2.f * k0), fmaf(-h, h, h), h);
 }
 __device__ __forceinline__ float gelu_tanh_grad_f(float u) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float t = fast_tanh(k0 * (u + k1 * u * u * u));
-  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
+  float g, d;
+  gelu_tanh_and_grad_f(u, g, d);
+  return d;
 }
 
 // Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5 "XCD swizzle must

@@ -221,6 +221,16 @@ __device__ __forceinline__ void stage_put(bf16* st, int row, int chunk, bf16x4 v
 template <int ROWS>
 __device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int m_base, int n_base, int M, int N,
                                           int lane) {
+  if (m_base + ROWS <= M && n_base + 64 <= N) {  // interior tile (wave-uniform): no per-row checks
+#pragma unroll 4
+    for (int it = 0; it < ROWS / 8; ++it) {
+      const int row = it * 8 + (lane >> 3), p = lane & 7;
+      u32x4 v = *(const u32x4*)(st + row * 64 + ((p ^ ((row >> 1) & 7)) << 3));
+      if (row & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+      DTC_OUT_STORE((u32x4*)(C + (long)(m_base + row) * ldc + n_base + p * 8), v);
+    }
+    return;
+  }
 #pragma unroll 4
   for (int it = 0; it < ROWS / 8; ++it) {
     const int row = it * 8 + (lane >> 3), p = lane & 7;
