@@ -1532,9 +1532,9 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
 
 // Paired launch: a1 = dgrad (layout 1, whole-K tiles), a2 = weight gradient (layout 2, split-K slabs
 // left for the caller's batched reducer when split > 1).  Only register-staged, BK = 64 plans pair.
-template <class C1, class C2, int BM1, int BM2>
+template <class C1, class C2, int BM1, int BM2, bool BKM1 = false>
 int launch_pair_t(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const Plan& p2, hipStream_t st) {
-  const GemmLaunch g1 = make_launch<BM1, BM1, true, false>(a1, p1);
+  const GemmLaunch g1 = make_launch<BM1, BM1, true, BKM1>(a1, p1);
   const GemmLaunch g2 = make_launch<BM2, BM2, false, false>(a2, p2);
   if (g1.nblocks % 8 && g2.nblocks % 8) return 1100;  // XCD maps would disagree: not pairable
   // DTC_PAIR_WGRAD_FIRST=1: dispatch the weight-gradient blocks first (when their count keeps the XCD
@@ -1551,6 +1551,11 @@ template <int EPI1, bool F1>
 int launch_pair_w(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const Plan& p2, hipStream_t st) {
   using W128 = GemmCfg<128, 128, 64, false, false, EPI_STORE, true>;
   using W64 = GemmCfg<64, 64, 64, false, false, EPI_STORE, true>;
+  if (a1.layout == 0) {  // dgrad as NT on the transposed weight (both operands K-major)
+    if (p1.bm != 128 || p2.bm != 128) return 1100;
+    using D = GemmCfg<128, 128, 64, true, true, EPI1, F1>;
+    return launch_pair_t<D, W128, 128, 128, true>(a1, p1, a2, p2, st);
+  }
   if (p1.bm == 128) {
     using D = GemmCfg<128, 128, 64, true, false, EPI1, F1>;
     return p2.bm == 128 ? launch_pair_t<D, W128, 128, 128>(a1, p1, a2, p2, st)
@@ -1668,16 +1673,16 @@ extern "C" {
 // when split) of one Dense in one launch.  Returns 1100 when the pair cannot share a launch (the
 // caller then issues the two GEMMs separately).
 int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
-  if (a1->layout != 1 || a2->layout != 2) return 1100;
+  if ((a1->layout != 1 && a1->layout != 0) || a2->layout != 2) return 1100;
   if (a1->K % 64 || a2->K % 64 || a1->N % 8 || a2->M % 8 || a2->N % 8) return 1100;
   if (a1->lda % 8 || a1->ldb % 8 || a1->ldc % 4 || a2->lda % 8 || a2->ldb % 8 || a2->ldc % 4) return 1100;
   if (a1->M <= 0 || a1->N <= 0 || a2->M <= 0 || a2->N <= 0) return 1100;
   if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
-  if (big_split(1, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
-  if (dmaw_plan(1, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
+  if (big_split(a1->layout, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
+  if (dmaw_plan(a1->layout, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
       dmaw_plan(2, a2->M, a2->N, a2->K, a2->epi, a2->c_f32 != 0, a2->colsum != nullptr).cfg != W_NONE)
     return 1100;  // the 8-wave kernels run these as two launches
-  const Plan p1 = make_plan(a1->M, a1->N, a1->K, (a1->epi == EPI_STORE && a1->c_f32) ? 2 : 0);
+  const Plan p1 = make_plan(a1->M, a1->N, a1->K, (a1->layout == 1 && a1->epi == EPI_STORE && a1->c_f32) ? 2 : 0);
   const Plan p2 = make_plan(a2->M, a2->N, a2->K, 1);
   if (p1.split != 1 || p1.bk != 64 || p2.bk != 64) return 1100;
   if (p2.split > 1 && (!a2->defer_reduce || a2->ws_bytes < (long)p2.split * a2->M * a2->N * 4)) return 1100;

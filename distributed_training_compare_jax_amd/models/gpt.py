@@ -227,12 +227,9 @@ class GPTStage:
         if side.stream is None:
             # single stream: each Dense's dgrad and weight gradient share one launch
             # (G.linear_backward), weight-gradient reductions go to the layer's batched launch
-            wt2 = f.wt(p + "fc2.w")
-            if wt2 is not None:  # NT dgrad (+ GELU backward) on the transposed weight, then the weight gradient
-                du = G.matmul_nt_dgelu(dx3_c, wt2, u)
-                G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta, red=red)
-            else:
-                du = G.linear_backward(dx3_c, f.w(p + "fc2.w"), gact, f.g(p + "fc2.w"), beta, red=red, dgelu_u=u)
+            # with a transposed fc2 weight the paired dgrad runs NT (+ GELU backward), both operands K-major
+            du = G.linear_backward(dx3_c, f.w(p + "fc2.w"), gact, f.g(p + "fc2.w"), beta, red=red, dgelu_u=u,
+                                   wt=f.wt(p + "fc2.w"))
             if not fc2b_fused:
                 G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
             # paired launches measured per Dense (in-step, us): fc2 44.1 vs 46.8 and qkv 35.6 vs 38.1

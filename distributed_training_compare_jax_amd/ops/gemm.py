@@ -275,16 +275,20 @@ _PAIR = __import__("os").environ.get("DTC_GEMM_PAIR", "1") == "1"  # A/B knob fo
 
 def linear_backward(dy: torch.Tensor, w: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0,
                     red=None, db: Optional[torch.Tensor] = None, dgelu_u: Optional[torch.Tensor] = None,
-                    out_dtype=torch.float32, pair: bool = True) -> torch.Tensor:
+                    out_dtype=torch.float32, pair: bool = True, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Both backward GEMMs of a Dense ``y = x·Wᵀ (+b)``: returns dX = dY·W (⊙ gelu'(u) when
     ``dgelu_u`` is given — the fc2 dgrad fused with the GELU backward) and accumulates
     dW = β·dW + dYᵀ·X (+ db = β·db + Σ_rows dY).
 
     On the GPU with a batched reducer both GEMMs go out as ONE launch (``dtc_gemm_pair``: they
     read the same dY, the weight gradient's blocks fill the CUs the dgrad's last wave leaves
-    idle, one dependent kernel boundary less); otherwise two calls."""
+    idle, one dependent kernel boundary less); otherwise two calls.  ``wt``: the transposed weight
+    ``[in, out]`` (``FlatParams.wt``) — the dgrad then runs as an NT GEMM (both operands K-major)."""
     if N.library_path(dy) or red is None or not (_PAIR and pair):
-        dx = matmul_nn_dgelu(dy, w, dgelu_u) if dgelu_u is not None else matmul_nn(dy, w, out_dtype=out_dtype)
+        if wt is not None and not N.library_path(dy):
+            dx = matmul_nt_dgelu(dy, wt, dgelu_u) if dgelu_u is not None else linear(dy, wt, out_dtype=out_dtype)
+        else:
+            dx = matmul_nn_dgelu(dy, w, dgelu_u) if dgelu_u is not None else matmul_nn(dy, w, out_dtype=out_dtype)
         wgrad(dy, x, dw, beta, red=red, db=db)
         return dx
     _check2d(dy, "dy"); _check2d(w, "w"); _check2d(x, "x")
@@ -294,12 +298,15 @@ def linear_backward(dy: torch.Tensor, w: torch.Tensor, x: torch.Tensor, dw: torc
     K = w.shape[1]
     Kx = x.shape[1]
     assert w.shape[0] == Nn and x.shape[0] == M and tuple(dw.shape) == (Nn, Kx)
+    lay, bw = (0, wt) if wt is not None else (1, w)
+    if wt is not None:
+        assert tuple(wt.shape) == (K, Nn)
     if dgelu_u is not None:
         dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
-        a1 = _gemm_args(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), dx, K, epi=N.EPI_DGELU, aux=dgelu_u, ldaux=K)
+        a1 = _gemm_args(lay, M, K, Nn, dy, dy.stride(0), bw, bw.stride(0), dx, K, epi=N.EPI_DGELU, aux=dgelu_u, ldaux=K)
     else:
         dx = torch.empty(M, K, dtype=out_dtype, device=dy.device)
-        a1 = _gemm_args(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), dx, K)
+        a1 = _gemm_args(lay, M, K, Nn, dy, dy.stride(0), bw, bw.stride(0), dx, K)
     split = int(L.dtc_gemm_wgrad_split(Nn, Kx, M, 1 if db is not None else 0))
     fuse_cs = db is not None and bool(L.dtc_gemm_wgrad_fuses_colsum(Nn, Kx, M))
     mark = red.off
