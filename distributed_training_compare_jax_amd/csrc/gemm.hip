@@ -730,7 +730,7 @@ struct GemmLaunch {
   const bf16* B; long ldb; int b_bytes;
   int M, N, K, tiles_m, tiles_n, gm, split, kps, nblocks;
   float* slab;
-  Epi e;
+  Epi e{};
 };
 
 template <int BM, int BN, int BK, bool AK, bool BKM, int EPI, bool OUTF32>
@@ -1396,6 +1396,7 @@ template <int BM, int BN, bool AK, bool BKM>
 GemmLaunch make_launch(const GemmArgs& a, const Plan& p) {
   GemmLaunch g;
   Epi& e = g.e;
+  e = Epi{};
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
@@ -1419,7 +1420,7 @@ GemmLaunch make_launch(const GemmArgs& a, const Plan& p) {
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
-  Epi e;
+  Epi e{};
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
@@ -1504,7 +1505,7 @@ inline int big_kps(int K, int split) { return ((K / 64 + split - 1) / split) * 6
 
 template <bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_big(const GemmArgs& a, int split, hipStream_t st) {
-  Epi e;
+  Epi e{};
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
@@ -1626,7 +1627,7 @@ WPlan dmaw_plan(int layout, int M, int N, int K, int epi, bool f32, bool has_col
 
 template <int BM, int BN, int NS, int WGM, int WGN, bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_w(const GemmArgs& a, int split, hipStream_t st) {
-  Epi e;
+  Epi e{};
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out; e.colsum = nullptr;
