@@ -17,8 +17,9 @@ are optional and default to the reference behaviour:
 * ``TrainConfig.data`` (``synthetic`` | ``fineweb``), ``use_graph``, ``profile`` (roctx
   ranges, device step times and a Chrome trace under ``<output_dir>/trace/``, see
   ``utils/trace.py``), ``watchdog_s`` (abort a rank whose step stalls that long, 0 = off),
-  ``dp_bucket_mb`` / ``dp_tail_mb`` (DP grad bucket sizes; the last bucket is kept small
-  because its all-reduce is exposed), ``dp_embed_gather`` (DP: all-gather the embedding
+  ``dp_bucket_mb`` / ``dp_tail_mb`` (DP grad bucket sizes, cut at layer boundaries and issued as
+  soon as their last layer's grads are final; the last bucket is kept small because its
+  all-reduce is exposed: for the reference model 98 / 48 / 48 / 36 / 12 MB), ``dp_embed_gather`` (DP: all-gather the embedding
   output grads and rebuild wte/wpe grads locally instead of all-reducing the 103 MB table),
   ``warmup_steps`` (reference hard-codes 5, ``train/train.py:64``), ``ckpt_every``/``resume``,
   ``tp_comm`` (``auto`` | ``p2p`` | ``rccl``: TP activation all-reduces as in-graph xGMI
@@ -118,7 +119,7 @@ class TrainConfig:
     tp_comm: str = "auto"
     defer_optimizer: bool = False
     defer_groups: int = 4
-    dp_bucket_mb: float = 64.0
+    dp_bucket_mb: float = 40.0
     dp_tail_mb: float = 16.0
     dp_embed_gather: bool = True
     zero_stage: int = 0  # 1 = ZeRO-1: Adam state sharded over the DP group (train/optimizer.py)

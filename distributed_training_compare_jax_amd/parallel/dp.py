@@ -28,10 +28,16 @@ class GradBuckets:
     ``bucket_mb`` sizes the bulk buckets; the LAST bucket (complete only when backward ends,
     so its all-reduce is exposed) is cut to about ``tail_mb``.  ``local_names`` are params
     whose grads every rank computes identically on its own (the DP embedding gather); they must
-    form the tail of the buffer and are excluded from the all-reduce."""
+    form the tail of the buffer and are excluded from the all-reduce.
+
+    ``boundaries``: offsets where grads become final together (the head's and each layer's end,
+    in backward order).  Buckets then end only there, so each is issued the moment its last layer
+    is done; cut at arbitrary param boundaries, a bucket straddling two layers waits for the later
+    one (for the reference model the second-to-last 64 MB bucket used to wait for the END of
+    backward, its all-reduce fully exposed)."""
 
     def __init__(self, flat: FlatParams, group, dp: int, program, bucket_mb: float = 64.0, tail_mb: float = 16.0,
-                 local_names=()):
+                 local_names=(), boundaries=None):
         self.flat = flat
         self.group = group
         self.dp = dp
@@ -48,12 +54,18 @@ class GradBuckets:
         self.reduce_end = end
         bounds: List[Tuple[int, int]] = [(s.offset, s.offset + s.numel) for s in flat.slots.values()
                                          if s.offset < end]
+        if boundaries:  # units = the spans between consecutive boundaries (layer-aligned buckets)
+            xs = sorted({int(x) for x in boundaries if 0 < int(x) < end} | {end})
+            bounds = list(zip([0] + xs[:-1], xs))
         # tail bucket: the last params adding up to ~tail_cap elements
         i_tail = len(bounds)
         acc = 0
         while i_tail > 1 and acc < tail_cap:
+            u = bounds[i_tail - 1][1] - bounds[i_tail - 1][0]
+            if boundaries and acc > 0 and acc + u > tail_cap:
+                break  # layer-aligned: the tail stays within tail_mb (at least one unit)
             i_tail -= 1
-            acc += bounds[i_tail][1] - bounds[i_tail][0]
+            acc += u
         cuts: List[int] = []  # exclusive end offsets of each bucket
         lo = None
         for a, b in bounds[:i_tail]:

@@ -98,9 +98,15 @@ class Engine:
             warnings.warn("defer_optimizer ignored under zero_stage=1 (the sharded update ends the step)")
         self.embed_gather = bool(dp > 1 and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed
                                  and not self.zero)
+        bnd = None
+        if pp == 1 and len(self.layout.layers):
+            names = list(self.flat.slots)
+            ends = [self.flat.range_of([n for n in names if n.startswith(f"h.{l}.")])[1] for l in self.layout.layers]
+            head = [n for n in names if n.startswith("lm_head") or n.startswith("lnf")]
+            bnd = ends + ([self.flat.range_of(head)[1]] if head else [])
         self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb,
                                    tail_mb=train_cfg.dp_tail_mb,
-                                   local_names=("wte", "wpe") if self.embed_gather else ())
+                                   local_names=("wte", "wpe") if self.embed_gather else (), boundaries=bnd)
         if self.zero:
             self.opt = ShardedAdamW(self.flat, opt_cfg, self.program, m.dp_group, dp, m.dp_idx)
         else:
@@ -287,16 +293,24 @@ class Engine:
             opt.ready_upto(bk.head_end_offset(), side)
             hook = lambda l: opt.ready_upto(bk.layer_end_offset(l), side)
         else:
-            # A bucket's all-reduce cuts the graph, which joins the side stream (capture needs it);
-            # issuing with a one-layer lag means the join finds that layer's weight-gradient
-            # GEMMs (which ran under the next layer's dgrads) already done instead of blocking
-            # the dgrad chain on them.  The first layer's bucket waits for the embedding gather
-            # (that collective feeds compute; the bucket only the optimizer).
+            # Single stream: layer l's grads are final once its reduction launch is queued (before
+            # the hook), so its bucket goes out right away; the head's bucket right after the head
+            # backward.  With the backward side stream a bucket's all-reduce cuts the graph, which
+            # joins that stream, so buckets go out with a one-layer lag (the join then finds that
+            # layer's weight-gradient GEMMs already done instead of blocking the dgrad chain).  The
+            # first layer's bucket waits for the embedding gather (that collective feeds compute;
+            # the bucket only the optimizer).
             layers = list(self.layout.layers)
             first = layers[0]
+            lag = st.side.stream is not None
+            if not lag and not self.zero:  # (ZeRO-1 reduce-scatters all grads in ShardedAdamW.step)
+                bk.ready_upto(bk.head_end_offset())
 
             def hook(l):
                 if self.embed_gather and l == first:
+                    return
+                if not lag:
+                    bk.ready_upto(bk.layer_end_offset(l))
                     return
                 nxt = l + 1
                 bk.ready_upto(bk.layer_end_offset(nxt) if nxt in layers else bk.head_end_offset())
