@@ -108,6 +108,30 @@ __device__ __forceinline__ float gelu_tanh_grad_f(float u) {
   return d;
 }
 
+// Cross-entropy backward of 8 consecutive vocab columns v0..v0+7 of one row:
+//   g = (softmax - onehot) * scale = exp2(l * log2(e) + cr) - [v == label] * scale,
+//   cr = log2(scale) - lse * log2(e)  (ce_row_c, once per row): one fma + one v_exp per element.
+// Columns >= n_valid (vocab padding) give 0: the lm_head forward writes -inf logits there and
+// exp2(-inf) = 0, so only a chunk that straddles n_valid is masked explicitly.  Shared by the
+// ce_bwd kernels and the fused lm_head dgrad (csrc/gemm.hip ce_dgrad256_kernel), so both produce
+// bit-identical dlogits.
+__device__ __forceinline__ float ce_row_c(float lse, float scale) {
+  return __builtin_amdgcn_logf(scale) - lse * 1.4426950408889634f;  // v_log_f32 is log2
+}
+__device__ __forceinline__ void ce_grad8(const bf16x8& l8, int v0, float cr, int lab, int n_valid, float scale,
+                                         float (&g)[8]) {
+  constexpr float L2E = 1.4426950408889634f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = __builtin_amdgcn_exp2f(fmaf((float)l8[e], L2E, cr));
+  if ((unsigned)(lab - v0) < 8u || v0 + 8 > n_valid) {  // the label's chunk / a chunk past n_valid (rare)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (v0 + e >= n_valid) g[e] = 0.f;
+      if (v0 + e == lab) g[e] -= scale;
+    }
+  }
+}
+
 // Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5 "XCD swizzle must
 // be bijective"): blocks that the dispatcher deals to the same XCD (b % 8) get a contiguous
 // range of logical tile ids, so neighbouring tiles share that XCD's L2.

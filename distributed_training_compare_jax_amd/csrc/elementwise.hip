@@ -249,7 +249,7 @@ __global__ void ce_loss_reduce(const float* __restrict__ lse, const float* __res
   }
 }
 
-// dlogits = (exp(l - lse) - onehot) * scale, in place, 8 bf16 per thread
+// dlogits = (exp(l - lse) - onehot) * scale (common.h ce_grad8), in place, 8 bf16 per thread
 __global__ void ce_bwd_kernel(bf16* __restrict__ logits, long ld, const float* __restrict__ lse,
                               const int* __restrict__ labels, int M, int V, int vstart, int n_valid, float scale) {
   const int V8 = V / 8;
@@ -258,17 +258,12 @@ __global__ void ce_bwd_kernel(bf16* __restrict__ logits, long ld, const float* _
   int m = (int)(i / V8);
   int n = (int)(i % V8) * 8;
   bf16x8* p = (bf16x8*)(logits + (long)m * ld + n);
-  bf16x8 v = *p;
-  const float l = lse[m];
-  const int lab = labels[m] - vstart;
+  const bf16x8 v = *p;
+  float g[8];
+  ce_grad8(v, n, ce_row_c(lse[m], scale), labels[m] - vstart, n_valid, scale, g);
   bf16x8 o;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    int c = n + r;
-    float g = c < n_valid ? __expf((float)v[r] - l) : 0.f;
-    if (c == lab) g -= 1.f;
-    o[r] = f2bf(g * scale);
-  }
+  for (int r = 0; r < 8; ++r) o[r] = f2bf(g[r]);
   *p = o;
 }
 
@@ -289,17 +284,13 @@ __global__ void __launch_bounds__(256) ce_bwd_colsum_kernel(bf16* __restrict__ l
   for (int m = m0; m < m1; ++m) {
     bf16x8* p = (bf16x8*)(logits + (long)m * ld + n);
     const bf16x8 v = *p;
-    const float l = lse[m];
-    const int lab = labels[m] - vstart;
+    float g[8];
+    ce_grad8(v, n, ce_row_c(lse[m], scale), labels[m] - vstart, n_valid, scale, g);
     bf16x8 o;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const int c = n + r;
-      float g = c < n_valid ? __expf((float)v[r] - l) : 0.f;
-      if (c == lab) g -= 1.f;
-      g *= scale;
-      cs[r] += g;
-      o[r] = f2bf(g);
+      cs[r] += g[r];
+      o[r] = f2bf(g[r]);
     }
     *p = o;
   }

@@ -950,6 +950,167 @@ gemm256_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B,
     }
 }
 
+// ============================================================================================
+// lm_head backward with the cross-entropy backward fused into the dgrad's A operand.
+//   dlogits[t][v] = (exp(logit[t][v] - lse[t]) - [v == label[t]]) * scale   (pad columns 0)
+//   dX[t][:]      = sum_v dlogits[t][v] * W[v][:]    (NT split-K on W^T, as the unfused dgrad)
+//   colpart       = column sums of dlogits (the lm_head bias gradient's partials)
+// The logits tile is register-staged (not DMA'd) so each element is transformed once per block on
+// its way into the LDS image — the K-major image layout of dma_tile<true> — and the unfused
+// ce_bwd pass (read 412 MB + write 412 MB) disappears: n-tile-0 blocks store the bf16 dlogits (the
+// weight gradient's input) and the column sums, the latter as MFMAs of a ones operand with
+// transposed reads of the A image (any k order sums the same), 16 columns per wave and k-step.
+// Each thread stages the SAME 16-B vocab chunk of 4 rows (the swizzle term (row>>1)&7 does not
+// depend on the 64-row step), so its label / lse values stay in registers for the whole block.
+__device__ __forceinline__ bf16x8 ce_colsum_frag(const bf16* img, int r0, int vt, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int row = r0 + 4 * g + q;  // rows r0 + {4g+q} and +16: every row of r0..r0+31 once
+  const int ch = 2 * vt + (pp >> 1);
+  const bf16* p0 = img + row * 64 + ((ch ^ ((row >> 1) & 7)) << 3) + (pp & 1) * 4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0 + 16 * 64));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+struct CeDgradArgs {
+  const bf16* logits; long ldl;
+  const float* lse; const int* labels; int vocab_start, n_valid; float scale;
+  const bf16* wt; long ldw;        // W^T [N = d][K = vocab] bf16, K-major
+  bf16* dlogits; long ldd;         // [M][K] bf16 out (n-tile 0 blocks)
+  float* colpart;                  // [2 * tiles_m][K] fp32 out (n-tile 0 blocks)
+  float* slab;                     // split-K fp32 slabs [split][M][N]
+  int M, N, K, tiles_m, tiles_n, gm, split, kps;
+};
+
+__global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
+  constexpr int TM = 8, TN = 4;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = a.tiles_m * a.tiles_n;
+  const int lid = xcd_remap(blockIdx.x, ntiles * a.split);
+  const int tile = lid % ntiles, z = lid / ntiles;
+  const int grp = tile / (a.gm * a.tiles_n), in_g = tile % (a.gm * a.tiles_n);
+  const int gm_eff = min(a.gm, a.tiles_m - grp * a.gm);
+  const int tm_idx = grp * a.gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
+  const int kbeg = z * a.kps;
+  const int nk = min(a.kps, a.K - kbeg) / 64;
+  // the dlogits stores + column sums of k-step kt go to n-tile kt % 2 (the two n-tiles share them)
+  const int nown = min(a.tiles_n, 2);
+  auto owns = [&](int kt) { return tn_idx < nown && kt % nown == tn_idx; };
+
+  // staging coordinates: rows q*64 + srow (q = 0..3), 16-B chunk schunk of the 64-wide k-step,
+  // stored at LDS chunk position lane & 7 (the dma_tile<true> image)
+  const int srow = wave * 8 + (lane >> 3), spos = lane & 7, schunk = spos ^ ((srow >> 1) & 7);
+  float cr_r[4];
+  int lab_r[4];
+  bool ok_r[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + q * 64 + srow;
+    ok_r[q] = m < a.M;
+    cr_r[q] = ce_row_c(ok_r[q] ? a.lse[m] : 0.f, a.scale);
+    lab_r[q] = ok_r[q] ? a.labels[m] - a.vocab_start : -1;
+  }
+  u32x4 R[4];
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = min(m0 + q * 64 + srow, a.M - 1);
+      R[q] = *(const u32x4*)(a.logits + (long)m * a.ldl + k0 + schunk * 8);
+    }
+  };
+  // transform the staged logits into dlogits: LDS image + (lead) global dlogits
+  auto put_a = [&](int k0, bf16* img, bool lead) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bf16x8 l8 = __builtin_bit_cast(bf16x8, R[q]);
+      const int v0 = k0 + schunk * 8;
+      float gv[8];
+      ce_grad8(l8, v0, cr_r[q], lab_r[q], a.n_valid, a.scale, gv);  // as ce_bwd: identical dlogits bits
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = ok_r[q] ? f2bf(gv[e]) : f2bf(0.f);
+      const int row = q * 64 + srow;
+      *(bf16x8*)(img + row * 64 + spos * 8) = o;
+      if (lead && ok_r[q]) *(bf16x8*)(a.dlogits + (long)(m0 + row) * a.ldd + v0) = o;
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  const int cs_vt = wave & 3, cs_half = wave >> 2;
+
+  // prologue: k-step 0 staged, the logits of k-step 1 already in registers
+  dma_tile<true>(a.wt, a.ldw, n0, a.N, kbeg, smem + IMG, wave, lane);
+  if (nk > 0) {
+    load_a(kbeg);
+    put_a(kbeg, smem, owns(0));
+  }
+  if (nk > 1) load_a(kbeg + 64);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // iteration kt: B(kt+1) DMA; A(kt+1) (registers, loaded one iteration ago) transformed into the
+  // other buffer; A(kt+2) loads issued; then the MFMAs of k-step kt, under which those loads land.
+  // The barrier waits only for the DMA: every vector-memory op issued after it (dlogits stores,
+  // the A(kt+2) loads, the column-sum store) may stay in flight (vmcnt counts in issue order).
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16* sA = smem + (kt & 1) * 2 * IMG;
+    const bf16* sB = sA + IMG;
+    bf16* nA = smem + ((kt + 1) & 1) * 2 * IMG;
+    const bool more = kt + 1 < nk, more2 = kt + 2 < nk;
+    const int k1 = kbeg + (kt + 1) * 64;
+    if (more) dma_tile<true>(a.wt, a.ldw, n0, a.N, k1, nA + IMG, wave, lane);
+    const bool st1 = more && owns(kt + 1);
+    if (more) put_a(k1, nA, st1);
+    if (more2) load_a(k1 + 64);
+    const bool cs_own = owns(kt);
+    if (cs_own) {  // column sums of this k-step's dlogits tile: 4 MFMAs per wave
+      f32x4 cs = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) cs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, ce_colsum_frag(sA, cs_half * 128 + 32 * s4, cs_vt, lane), cs, 0, 0, 0);
+      if (lane < 16) a.colpart[(long)(2 * tm_idx + cs_half) * a.K + kbeg + kt * 64 + cs_vt * 16 + lane] = cs[0];
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = big_frag<true>(sA, wm * 8 + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = big_frag<true>(sB, wn * 4 + i, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    // ops issued after the DMA: 4 stores (every staged row valid), 4 loads, 1 column-sum store
+    const int after = ((st1 && m0 + BIG <= a.M) ? 4 : 0) + (more2 ? 4 : 0) + (cs_own ? 1 : 0);
+    if (after >= 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if (after >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after >= 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if (after >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (after >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const int g4 = 4 * (lane >> 4);
+  float* sl = a.slab + (long)z * a.M * a.N;  // split-K slab z (splitk_reduce sums them in order)
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+      const int n = n0 + wn * 64 + i * 16 + g4;
+      if (m < a.M && n < a.N) *(f32x4*)(sl + (long)m * a.N + n) = acc[i][j];
+    }
+}
+
 // C = beta*C + sum_z slab[z]   (fp32, deterministic order)
 __global__ void splitk_reduce(const float* __restrict__ slab, int split, long MN, float* __restrict__ C, long ldc,
                               int N, float beta) {
@@ -1693,6 +1854,41 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   if (a1->epi == EPI_STORE && a1->c_f32) return launch_pair_w<EPI_STORE, true>(*a1, p1, *a2, p2, st);
   if (a1->epi == EPI_STORE && !a1->c_f32) return launch_pair_w<EPI_STORE, false>(*a1, p1, *a2, p2, st);
   return 1100;
+}
+
+// Fused lm_head backward (ce_dgrad256_kernel): dX [M][N] fp32 (= sum of the split-K slabs, written
+// by splitk_reduce), dlogits [M][K] bf16, colpart [2*ceil(M/256)][K] fp32.  K % 64 == 0, N % 8 == 0.
+long dtc_ce_dgrad_workspace_bytes(int M, int N, int K) {
+  const int split = big_split(1, M, N, K);
+  return split > 1 ? (long)split * M * N * 4 : (long)M * N * 4;
+}
+int dtc_ce_dgrad_colpart_rows(int M) { return 2 * ((M + BIG - 1) / BIG); }
+
+int dtc_ce_dgrad(const bf16* logits, long ldl, const float* lse, const int* labels, int vocab_start, int n_valid,
+                 float scale, const bf16* wt, long ldw, bf16* dlogits, long ldd, float* colpart, float* dx, int M, int N,
+                 int K, float* ws, long ws_bytes, hipStream_t st) {
+  if (K % 64 || N % 8 || ldl % 8 || ldw % 8 || ldd % 8) return 1300;
+  int split = big_split(1, M, N, K);
+  if (split < 1) split = 1;
+  if (ws_bytes < (long)split * M * N * 4) return 1301;
+  CeDgradArgs a;
+  a.logits = logits; a.ldl = ldl; a.lse = lse; a.labels = labels; a.vocab_start = vocab_start; a.n_valid = n_valid;
+  a.scale = scale; a.wt = wt; a.ldw = ldw; a.dlogits = dlogits; a.ldd = ldd; a.colpart = colpart; a.slab = ws;
+  a.M = M; a.N = N; a.K = K;
+  a.tiles_m = (M + BIG - 1) / BIG;
+  a.tiles_n = (N + BIG - 1) / BIG;
+  const int ntiles = a.tiles_m * a.tiles_n;
+  a.gm = a.tiles_m;
+  if (a.tiles_n <= 16) a.gm = std::max(1, std::min(a.tiles_m, (ntiles * split / 8 + a.tiles_n - 1) / a.tiles_n));
+  a.split = split;
+  a.kps = big_kps(K, split);
+  hipLaunchKernelGGL(ce_dgrad256_kernel, dim3(ntiles * split), dim3(NT2), 0, st, a);
+  DTC_CHECK_LAUNCH();
+  const long MN = (long)M * N;
+  hipLaunchKernelGGL(splitk_reduce, dim3((int)((MN / 4 + 255) / 256)), dim3(256), 0, st, (const float*)ws, split, MN,
+                     dx, (long)N, N, 0.f);
+  DTC_CHECK_LAUNCH();
+  return 0;
 }
 
 int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }

@@ -43,6 +43,7 @@ _LMHEAD_WGRAD_MAIN = _os.environ.get("DTC_LMHEAD_WGRAD", "side") == "main"
 # side-stream schedule: 1 = the previous layer's weight gradients are forked one at a time between
 # this layer's dgrad GEMMs; 0 = one fork per layer after its dgrad chain
 _SIDE_INTERLEAVE = _os.environ.get("DTC_SIDE_INTERLEAVE", "0") == "1"  # measured: 1 is slower
+_CE_FUSED = _os.environ.get("DTC_CE_FUSED", "1") == "1"  # ops/xent.py ce_dgrad_fused
 
 
 class NoComm:
@@ -334,12 +335,18 @@ class GPTStage:
     def head_backward(self, ctx: Dict, grad_scale: float, beta: float):
         f = self.flat
         x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
-        # one pass: dlogits in place + column partials of it (the bias gradient's input)
-        dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale, colpart=True)
-        # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
-        # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
         wt = f.wt("lm_head.w")  # transposed mirror: NT split-K dgrad, both operands K-major
-        dyf = G.linear_resid(dlogits, wt, None, None) if wt is not None else G.matmul_nn(dlogits, f.w("lm_head.w"))
+        if wt is not None and _CE_FUSED and logits.is_cuda:
+            # CE backward fused into the dgrad's operand staging (no separate 824 MB dlogits pass)
+            dyf, dlogits, colp = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt)
+        else:
+            # one pass: dlogits in place + column partials of it (the bias gradient's input)
+            dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale,
+                                                  colpart=True)
+            # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
+            # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
+            dyf = (G.linear_resid(dlogits, wt, None, None) if wt is not None
+                   else G.matmul_nn(dlogits, f.w("lm_head.w")))
         red = self.red
         wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
                                                 G.colsum(cp, f.g("lm_head.b"), beta, red=red))

@@ -112,6 +112,9 @@ def _declare(lib):
         "dtc_tr_max_tasks": ([], i),
         "dtc_tr_task_bytes": ([], i),
         "dtc_fill_f32": ([vp, f, l, vp], i),
+        "dtc_ce_dgrad": ([vp, l, vp, vp, i, i, f, vp, l, vp, l, vp, vp, i, i, i, vp, l, vp], i),
+        "dtc_ce_dgrad_workspace_bytes": ([i, i, i], l),
+        "dtc_ce_dgrad_colpart_rows": ([i], i),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)

@@ -114,3 +114,32 @@ def ce_backward_inplace(logits: torch.Tensor, lse: torch.Tensor, labels: torch.T
     N.check(L.dtc_ce_bwd(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), M, Vl, vocab_start,
                          n_valid, grad_scale, N.ptr(cp), N.stream_ptr(logits.device)), "dtc_ce_bwd")
     return (logits, cp) if colpart else logits
+
+
+def ce_dgrad_fused(logits: torch.Tensor, lse: torch.Tensor, labels: torch.Tensor, vocab_start: int, n_valid: int,
+                   grad_scale: float, wt: torch.Tensor):
+    """The lm_head backward's first half in ONE kernel (``csrc/gemm.hip`` ce_dgrad256_kernel): the
+    cross-entropy backward applied to the logits as they are staged into the dgrad GEMM.
+
+    Returns ``(dx, dlogits, colpart)``: dx = dlogits·W (fp32 [M, d], ``wt`` = Wᵀ [d, V] bf16),
+    dlogits (bf16 [M, V], bitwise equal to :func:`ce_backward_inplace`'s, for the weight gradient)
+    and the column partial sums of dlogits (fp32 [R, V], the bias gradient's input — summed from
+    the bf16 dlogits, where :func:`ce_backward_inplace` sums the fp32 values before rounding).
+    The logits are left untouched.  GPU bf16 path only."""
+    from .gemm import _workspace
+
+    M, Vl = logits.shape
+    D = wt.shape[0]
+    assert wt.shape[1] == Vl and logits.dtype == torch.bfloat16 and wt.dtype == torch.bfloat16
+    assert logits.is_contiguous() and wt.is_contiguous()
+    L = N.lib()
+    dl = torch.empty_like(logits)
+    cp = torch.empty(int(L.dtc_ce_dgrad_colpart_rows(M)), Vl, dtype=torch.float32, device=logits.device)
+    dx = torch.empty(M, D, dtype=torch.float32, device=logits.device)
+    nbytes = int(L.dtc_ce_dgrad_workspace_bytes(M, D, Vl))
+    ws = _workspace(logits.device, nbytes)
+    N.check(L.dtc_ce_dgrad(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), vocab_start, n_valid,
+                           grad_scale, wt.data_ptr(), wt.stride(0), dl.data_ptr(), dl.stride(0), cp.data_ptr(),
+                           dx.data_ptr(), M, D, Vl, ws.data_ptr(), ws.numel(), N.stream_ptr(logits.device)),
+            "dtc_ce_dgrad")
+    return dx, dl, cp

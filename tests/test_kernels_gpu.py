@@ -267,6 +267,27 @@ def test_lmhead_ce(cuda, M, D, V, Vp):
     assert logits[:, V:].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("M,D,V,Vp,vstart", [(4096, 512, 50258, 50304, 0), (1024, 256, 25129, 25152, 25129),
+                                             (512, 256, 1000, 1024, 0)])
+def test_ce_dgrad_fused_matches_unfused(cuda, M, D, V, Vp, vstart):
+    """ce_dgrad_fused (CE backward inside the lm_head dgrad's operand staging) == ce_backward_inplace +
+    the NT dgrad on W^T: identical dlogits bits, the same dX up to summation order, and column
+    sums of the (rounded) dlogits.  vstart > 0: a vocab-parallel shard (labels outside it too)."""
+    g = torch.Generator().manual_seed(31)
+    logits = (torch.randn(M, Vp, generator=g) * 3).to(torch.bfloat16)
+    logits[:, V:] = float("-inf")
+    logits = logits.to(cuda)
+    lse = torch.logsumexp(logits.float(), -1).contiguous()
+    labels = torch.randint(0, 2 * V if vstart else V, (M,), dtype=torch.int32, generator=g).to(cuda)
+    wt = _r(D, Vp, scale=0.05, seed=32)
+    dx, dl, cp = X.ce_dgrad_fused(logits, lse, labels, vstart, V, 1.0 / M, wt)
+    ref_dl, ref_cp = X.ce_backward_inplace(logits.clone(), lse, labels, vstart, V, 1.0 / M, colpart=True)
+    assert torch.equal(dl, ref_dl)
+    _close(dx, dl.float() @ wt.float().t(), 2e-3, "dx")
+    _close(cp.sum(0), dl.float().sum(0), 1e-4, "colsum")
+    _close(cp.sum(0), ref_cp.sum(0), 5e-3, "colsum_vs_fp32")
+
+
 def test_lmhead_raw_partials_match_combined(cuda):
     """combine=False (one vocab shard: raw per-tile partials, a label logit written for every row,
     no zero-fill) gives the same logits, label logits and loss as the combined row statistics."""
