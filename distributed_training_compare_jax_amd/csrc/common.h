@@ -123,11 +123,16 @@ __device__ __forceinline__ void ce_grad8(const bf16x8& l8, int v0, float cr, int
   constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) g[e] = __builtin_amdgcn_exp2f(fmaf((float)l8[e], L2E, cr));
-  if ((unsigned)(lab - v0) < 8u || v0 + 8 > n_valid) {  // the label's chunk / a chunk past n_valid (rare)
+  // the label's chunk / a chunk past n_valid: rare, so a WAVE-uniform branch around the fix-up
+  // (a lane-level if gets predicated into compares + selects on every element)
+  const bool fix = (unsigned)(lab - v0) < 8u || v0 + 8 > n_valid;
+  if (__builtin_amdgcn_ballot_w64(fix)) {
+    if (fix) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (v0 + e >= n_valid) g[e] = 0.f;
-      if (v0 + e == lab) g[e] -= scale;
+      for (int e = 0; e < 8; ++e) {
+        if (v0 + e >= n_valid) g[e] = 0.f;
+        if (v0 + e == lab) g[e] -= scale;
+      }
     }
   }
 }

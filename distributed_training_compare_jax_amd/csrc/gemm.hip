@@ -1010,7 +1010,7 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
   for (int q = 0; q < 4; ++q) {
     const int m = m0 + q * 64 + srow;
     ok_r[q] = m < a.M;
-    cr_r[q] = ce_row_c(ok_r[q] ? a.lse[m] : 0.f, a.scale);
+    cr_r[q] = ok_r[q] ? ce_row_c(a.lse[m], a.scale) : -INFINITY;  // rows past M: exp2(-inf) = 0
     lab_r[q] = ok_r[q] ? a.labels[m] - a.vocab_start : -1;
   }
   u32x4 R[4];
@@ -1031,7 +1031,7 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
       ce_grad8(l8, v0, cr_r[q], lab_r[q], a.n_valid, a.scale, gv);  // as ce_bwd: identical dlogits bits
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = ok_r[q] ? f2bf(gv[e]) : f2bf(0.f);
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(gv[e]);
       const int row = q * 64 + srow;
       *(bf16x8*)(img + row * 64 + spos * 8) = o;
       if (lead && ok_r[q]) *(bf16x8*)(a.dlogits + (long)(m0 + row) * a.ldd + v0) = o;
