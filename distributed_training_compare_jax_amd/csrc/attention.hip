@@ -51,6 +51,9 @@ __device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// raw v_exp_f32 (softmax arguments are <= 0: no overflow range handling needed; the libm exp2f
+// wraps every call in ldexp/compare/select denormal scaffolding)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // stage a [rows][HD] tile (rows starting at token t0) of slot `which` (0 q, 1 k, 2 v) into LDS [rows][ld]
 template <int HD, int ROWS>
@@ -173,14 +176,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16* __restrict__ 
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);  // m = -inf on the first tile -> 0
+    const float alpha = fast_exp2(m - mn);  // m = -inf on the first tile -> 0
     m = mn;
     float ls = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float pv = exp2f(s[st][r] - mn);
+        float pv = fast_exp2(s[st][r] - mn);
         s[st][r] = pv;
         ls += pv;
       }
@@ -279,7 +282,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const bf16* __restri
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qr + r;
-        float pv = (key <= qq && qq < T && key < T) ? exp2f(s[r] * c - l4[r] * LOG2E) : 0.f;
+        float pv = (key <= qq && qq < T && key < T) ? fast_exp2(s[r] * c - l4[r] * LOG2E) : 0.f;
         p[qt][r] = pv;
         ds[qt][r] = pv * (dp[r] - d4[r]);
       }
@@ -354,7 +357,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kk = k0 + kt * 16 + 4 * g + r;
-        float pv = (kk <= q && kk < T && q < T) ? exp2f(s[r] * c - lq) : 0.f;
+        float pv = (kk <= q && kk < T && q < T) ? fast_exp2(s[r] * c - lq) : 0.f;
         ds[kt][r] = pv * (dp[r] - dq_);
       }
     }
@@ -387,10 +390,6 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const bf16* __restrict
 // interleaves 4 waves.
 constexpr int RES_THREADS = 1024;
 constexpr int RES_MAXT = 512;  // 16 waves x 2 blocks x 16 rows
-
-// raw v_exp_f32 (softmax arguments are <= 0: no overflow range handling needed; the libm exp2f
-// wraps every call in ldexp/compare/select denormal scaffolding)
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // max / sum over the 4 lane groups (lanes j, j+16, j+32, j+48) with the gfx950 row swaps instead
 // of ds_bpermute round trips through LDS
