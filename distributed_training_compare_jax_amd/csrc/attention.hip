@@ -70,16 +70,16 @@ __device__ __forceinline__ void stage_tile(bf16* lds, int ld, const bf16* __rest
 
 // Register-staged pair of [ROWS][HD] tiles (K&V, Q&dO, ...) for a 2-deep software pipeline:
 // tile i+2 is loaded into registers while LDS holds tile i and registers hold tile i+1 (T14).
-template <int HD, int ROWS>
+template <int HD, int ROWS, int NTH = 256>
 struct PairStage {
   static constexpr int CH = ROWS * HD / 8;             // 16-B chunks per tile
-  static constexpr int CPT = (CH + 255) / 256;         // per thread
+  static constexpr int CPT = (CH + NTH - 1) / NTH;     // per thread
   u32x4 x[CPT], y[CPT];
   __device__ __forceinline__ void load(const bf16* __restrict__ bx, long sx, const bf16* __restrict__ by, long sy,
                                        int t0, int T, int tid) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + 256 * i;
+      const int c = tid + NTH * i;
       const int r = c / (HD / 8), col = (c % (HD / 8)) * 8, t = t0 + r;
       const bool ok = c < CH && t < T;
       x[i] = ok ? *(const u32x4*)(bx + (long)t * sx + col) : u32x4{0, 0, 0, 0};
@@ -89,7 +89,7 @@ struct PairStage {
   __device__ __forceinline__ void store(bf16* lx, int ldx, bf16* ly, int ldy, int tid) const {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + 256 * i;
+      const int c = tid + NTH * i;
       if (c < CH) {
         const int r = c / (HD / 8), col = (c % (HD / 8)) * 8;
         *(u32x4*)(lx + r * ldx + col) = x[i];
@@ -101,7 +101,7 @@ struct PairStage {
 
 // Runs body(ldsX, ldsY, it) for it = 0..n-1 over tiles starting at token t0_of(it), with the
 // tiles streamed through two LDS stages and two register stages (one barrier per tile).
-template <int HD, int ROWS, typename T0, typename Body>
+template <int HD, int ROWS, int NTH = 256, typename T0, typename Body>
 __device__ __forceinline__ void pipelined_tiles(int n, T0 t0_of, const bf16* bx, long sx, const bf16* by, long sy,
                                                 int T, bf16* lds, int ldx, int ldy, int tid, Body body) {
   if (n <= 0) return;
@@ -109,7 +109,7 @@ __device__ __forceinline__ void pipelined_tiles(int n, T0 t0_of, const bf16* bx,
   bf16* Y0 = X0 + ROWS * ldx;
   bf16* X1 = Y0 + ROWS * ldy;
   bf16* Y1 = X1 + ROWS * ldx;
-  PairStage<HD, ROWS> p0, p1;
+  PairStage<HD, ROWS, NTH> p0, p1;
   p0.load(bx, sx, by, sy, t0_of(0), T, tid);
   if (n > 1) p1.load(bx, sx, by, sy, t0_of(1), T, tid);
   p0.store(X0, ldx, Y0, ldy, tid);
@@ -525,6 +525,110 @@ __global__ void __launch_bounds__(RES_THREADS) attn_fwd_res_kernel(const bf16* _
       acc[t] = mfma(tr_frag(tV, L::VLD, 32, t * 16, lane), pf1, acc[t]);
     }
   }
+  l = group_sum(l);
+  if (q < T) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long)b * T + q) * H * HD + h * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+      *(bf16x4*)(orow + t * 16 + 4 * g) =
+          bf16x4{f2bf(acc[t][0] * inv), f2bf(acc[t][1] * inv), f2bf(acc[t][2] * inv), f2bf(acc[t][3] * inv)};
+    if (g == 0) lse[((long)b * H + h) * T + q] = (m + __log2f(l)) * LN2;
+  }
+}
+
+// Chunked forward for sequences the resident kernel cannot hold (T > RES_MAXT, or head_dim 64:
+// GPT-2 medium is T 1024 / hd 64).  A 1024-thread block (16 waves x 16 query rows = 256 queries of
+// one (b, h)) streams K/V in 128-key chunks through a 2-stage LDS + 2-stage register pipeline:
+// one barrier per 128 keys shared by 16 waves (the 256-thread tiled kernel pays a barrier and a
+// K/V load per 64 keys per 4 waves, and was latency-bound at ~25 TF/s).  Each wave skips the
+// 64-key tiles past its rows and masks only the tiles that cross its diagonal.
+constexpr int CH_THREADS = 1024, CH_KEYS = 128, CH_QROWS = 256;
+template <int HD>
+__host__ __device__ constexpr int ch_lds_fwd() { return 2 * CH_KEYS * (AttnLds<HD>::KLD + AttnLds<HD>::VLD) * 2; }
+
+template <int HD>
+__global__ void __launch_bounds__(CH_THREADS) attn_fwd_chunk_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+                                                                   float* __restrict__ lse, int B, int T, int H,
+                                                                   float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (T + CH_QROWS - 1) / CH_QROWS;
+  const int qblk = nqb - 1 - (int)(blockIdx.x % nqb);  // heavy (late) query blocks first
+  const int bh = blockIdx.x / nqb, b = bh / H, h = bh % H;
+  const long ts = 3L * H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const int qbase = qblk * CH_QROWS + 16 * w;  // this wave's rows qbase .. qbase + 15
+  const int q = qbase + j;
+  bf16x8 qf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) qf[kc] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + kc * 32 + 8 * g) : bf16x8{};
+  const float c = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 acc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto body = [&](const bf16* sK, const bf16* sV, int it) {
+#pragma unroll
+    for (int t2 = 0; t2 < CH_KEYS / 64; ++t2) {
+      const int kb = it * CH_KEYS + t2 * 64;
+      if (kb > qbase + 15 || qbase >= T) continue;  // wave-uniform: tile entirely past this wave's rows
+      const bool diag = kb + 63 > qbase;            // crosses the diagonal (or the sequence end)
+      const bf16* tK = sK + t2 * 64 * L::KLD;
+      const bf16* tV = sV + t2 * 64 * L::VLD;
+      f32x4 sc[4];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        sc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) sc[st] = mfma(row_frag(tK, L::KLD, st * 16, kc * 32, lane), qf[kc], sc[st]);
+      }
+      float mt = -INFINITY;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = sc[st][r];
+          if (diag) {
+            const int key = kb + st * 16 + 4 * g + r;
+            x = (key <= q && key < T) ? x : -INFINITY;
+          }
+          sc[st][r] = x;
+          mt = fmaxf(mt, x);
+        }
+      mt = group_max(mt) * c;
+      const float mn = fmaxf(m, mt);
+      const float alpha = fast_exp2(m - mn);
+      m = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = fast_exp2(fmaf(sc[st][r], c, -mn));
+          sc[st][r] = pv;
+          ls += pv;
+        }
+      l = l * alpha + ls;
+#pragma unroll
+      for (int t = 0; t < HT; ++t) acc[t] *= alpha;
+      const bf16x8 pf0 = pack_p(sc[0], sc[1]), pf1 = pack_p(sc[2], sc[3]);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        acc[t] = mfma(tr_frag(tV, L::VLD, 0, t * 16, lane), pf0, acc[t]);
+        acc[t] = mfma(tr_frag(tV, L::VLD, 32, t * 16, lane), pf1, acc[t]);
+      }
+    }
+  };
+  const int nch = (min(T, qblk * CH_QROWS + CH_QROWS) + CH_KEYS - 1) / CH_KEYS;
+  pipelined_tiles<HD, CH_KEYS, CH_THREADS>(nch, [](int it) { return it * CH_KEYS; }, Kb, ts, Vb, ts, T, lds, L::KLD,
+                                           L::VLD, tid, body);
   l = group_sum(l);
   if (q < T) {
     const float inv = 1.f / l;
@@ -1051,6 +1155,20 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
     // flags bit 0: plain wave -> query-group order (A/B of the SIMD-balanced order)
     hipLaunchKernelGGL(attn_fwd_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_fwd(T, HD), st, qkv, o,
                        lse, B, T, H, scale, (int)!(flags & 1));
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
+  // chunked kernel (DTC_ATTN_CHUNK=0: the 256-thread tiled kernel)
+  static const int chunk = [] { const char* v = getenv("DTC_ATTN_CHUNK"); return v ? atoi(v) : 1; }();
+  if (chunk && (HD == 32 || HD == 64)) {
+    const dim3 g(B * H * ((T + CH_QROWS - 1) / CH_QROWS));
+    if (HD == 64) {
+      allow_lds(attn_fwd_chunk_kernel<64>, ch_lds_fwd<64>());
+      hipLaunchKernelGGL(attn_fwd_chunk_kernel<64>, g, dim3(CH_THREADS), ch_lds_fwd<64>(), st, qkv, o, lse, B, T, H, scale);
+    } else {
+      allow_lds(attn_fwd_chunk_kernel<32>, ch_lds_fwd<32>());
+      hipLaunchKernelGGL(attn_fwd_chunk_kernel<32>, g, dim3(CH_THREADS), ch_lds_fwd<32>(), st, qkv, o, lse, B, T, H, scale);
+    }
     DTC_CHECK_LAUNCH();
     return 0;
   }

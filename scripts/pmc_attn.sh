@@ -12,5 +12,5 @@ i=0
 for P in "$P1" "$P2"; do
   i=$((i + 1))
   timeout -s KILL 90 rocprofv3 --pmc $P -d gpurun_out/pmc_attn$i -o pmc --output-format csv -- \
-    python benchmarks/attn_micro.py > gpurun_out/pmc_attn$i.log 2>&1 || exit $?
+    python benchmarks/attn_micro.py > gpurun_out/pmc_attn$i.log 2>&1 || exit $?  # ATTN_SHAPE=medium: T 1024 / hd 64
 done

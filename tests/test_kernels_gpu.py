@@ -207,7 +207,8 @@ def test_embedding_bwd_sorted_deterministic(cuda, B, T, D, V, skew):
     _close(dwpe.cpu(), 2 * ref_p, 2e-6, "dwpe_acc")
 
 
-@pytest.mark.parametrize("B,T,H,hd", [(2, 512, 4, 32), (1, 256, 2, 64), (2, 128, 3, 32), (2, 200, 3, 32), (1, 520, 2, 32)])
+@pytest.mark.parametrize("B,T,H,hd", [(2, 512, 4, 32), (1, 256, 2, 64), (2, 128, 3, 32), (2, 200, 3, 32), (1, 520, 2, 32),
+                                      (1, 1024, 2, 64), (1, 1000, 2, 64), (1, 700, 3, 32)])
 def test_attention(cuda, B, T, H, hd):
     qkv = _r(B, T, 3 * H * hd, seed=20)
     o, lse = A.attn_fwd(qkv, H)
