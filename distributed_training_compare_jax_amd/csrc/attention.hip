@@ -556,9 +556,12 @@ __global__ void __launch_bounds__(CH_THREADS) attn_fwd_chunk_kernel(const bf16* 
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nqb = (T + CH_QROWS - 1) / CH_QROWS;
-  const int qblk = nqb - 1 - (int)(blockIdx.x % nqb);  // heavy (late) query blocks first
-  const int bh = blockIdx.x / nqb, b = bh / H, h = bh % H;
+  // heavy (late) query blocks first ACROSS the grid: at ~2 blocks per CU a per-(b, h) order leaves
+  // CUs with two heavy blocks (1.6x the mean work); grid-wide LPT pairs each heavy block with a
+  // light one on the same CU
+  const int nqb = (T + CH_QROWS - 1) / CH_QROWS, nbh = B * H;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);
+  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
   const long ts = 3L * H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
   const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
