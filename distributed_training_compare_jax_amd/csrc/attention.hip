@@ -644,6 +644,183 @@ __global__ void __launch_bounds__(CH_THREADS) attn_fwd_chunk_kernel(const bf16* 
   }
 }
 
+// Chunked backward for T > RES_MAXT / head_dim 64 (the tiled kernels above with 16 waves = 256
+// rows per block, 128-row Q/dO or K/V chunks, wave-uniform tile skips, diagonal-only masks and a
+// grid-wide heavy-first block order; see attn_fwd_chunk_kernel).
+template <int HD>
+__host__ __device__ constexpr int ch_lds_bwd() { return 4 * CH_KEYS * AttnLds<HD>::VLD * 2; }
+
+// dK, dV: block = (b, h, NTH/4 keys); wave w owns keys kb0 + 16w .. +15 (key on the lane).  512
+// threads: the dk/dv/p/ds accumulators spill at the 128 VGPRs of a 1024-thread block (hd 64)
+constexpr int CHB_THREADS = 512, CHB_KROWS = CHB_THREADS / 4;
+template <int HD>
+__global__ void __launch_bounds__(CHB_THREADS) attn_bwd_dkdv_chunk_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbh = B * H;
+  const int kblk = (int)(blockIdx.x / nbh);  // key block 0 sweeps every query: heaviest, dispatched first
+  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const float* lseb = lse + ((long)b * H + h) * T;
+  const float* delb = delta + ((long)b * H + h) * T;
+  const int kb0 = kblk * CHB_KROWS, kmin = kb0 + 16 * w;  // this wave's keys kmin .. kmin + 15
+  const int key = kmin + j;
+  bf16x8 kf[KC], vf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    kf[kc] = key < T ? *(const bf16x8*)(Kb + (long)key * ts + kc * 32 + 8 * g) : bf16x8{};
+    vf[kc] = key < T ? *(const bf16x8*)(Vb + (long)key * ts + kc * 32 + 8 * g) : bf16x8{};
+  }
+  const float c = scale * LOG2E;
+  f32x4 dk[HT], dv[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) { dk[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
+  const int cq0 = kb0 / CH_KEYS * CH_KEYS;  // first query chunk (queries >= the block's keys)
+
+  auto body = [&](const bf16* sQ, const bf16* sD, int it) {
+#pragma unroll
+    for (int t2 = 0; t2 < CH_KEYS / 64; ++t2) {
+      const int q0 = cq0 + it * CH_KEYS + t2 * 64;
+      if (q0 + 63 < kmin || kmin >= T || q0 >= T) continue;  // wave-uniform: every query before the keys
+      const bool diag = q0 < kmin + 15 || q0 + 64 > T;
+      const bf16* tQ = sQ + t2 * 64 * L::VLD;
+      const bf16* tD = sD + t2 * 64 * L::VLD;
+      f32x4 p[4], ds[4];
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) {
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          sv = mfma(row_frag(tQ, L::VLD, qt * 16, kc * 32, lane), kf[kc], sv);  // S[q][key]
+          dp = mfma(row_frag(tD, L::VLD, qt * 16, kc * 32, lane), vf[kc], dp);  // dP[q][key]
+        }
+        const int qr = q0 + qt * 16 + 4 * g;
+        f32x4 l4 = {0.f, 0.f, 0.f, 0.f}, d4 = {0.f, 0.f, 0.f, 0.f};
+        if (qr + 4 <= T) { l4 = *(const f32x4*)(lseb + qr); d4 = *(const f32x4*)(delb + qr); }
+        else for (int r = 0; r < 4; ++r) if (qr + r < T) { l4[r] = lseb[qr + r]; d4[r] = delb[qr + r]; }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = qr + r;
+          float pv = fast_exp2(fmaf(sv[r], c, -l4[r] * LOG2E));
+          if (diag) pv = (key <= qq && qq < T && key < T) ? pv : 0.f;
+          p[qt][r] = pv;
+          ds[qt][r] = pv * (dp[r] - d4[r]);
+        }
+      }
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {
+        const bf16x8 pb = pack_p(p[2 * hq], p[2 * hq + 1]), dsb = pack_p(ds[2 * hq], ds[2 * hq + 1]);
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+          dv[t] = mfma(tr_frag(tD, L::VLD, 32 * hq, t * 16, lane), pb, dv[t]);
+          dk[t] = mfma(tr_frag(tQ, L::VLD, 32 * hq, t * 16, lane), dsb, dk[t]);
+        }
+      }
+    }
+  };
+  const int nch = (T - cq0 + CH_KEYS - 1) / CH_KEYS;
+  pipelined_tiles<HD, CH_KEYS, CHB_THREADS>(nch, [cq0](int it) { return cq0 + it * CH_KEYS; }, Qb, ts, dOb, dts, T, lds,
+                                            L::VLD, L::VLD, tid, body);
+  if (key < T) {
+    bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
+    bf16* pv = dqkv + ((long)b * T + key) * ts + (2 * H + h) * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      *(bf16x4*)(pk + t * 16 + 4 * g) = bf16x4{f2bf(dk[t][0] * scale), f2bf(dk[t][1] * scale), f2bf(dk[t][2] * scale),
+                                               f2bf(dk[t][3] * scale)};
+      *(bf16x4*)(pv + t * 16 + 4 * g) = bf16x4{f2bf(dv[t][0]), f2bf(dv[t][1]), f2bf(dv[t][2]), f2bf(dv[t][3])};
+    }
+  }
+}
+
+// dQ: block = (b, h, 256 queries); wave w owns queries qb0 + 16w .. +15 (query on the lane)
+template <int HD>
+__global__ void __launch_bounds__(CH_THREADS) attn_bwd_dq_chunk_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  constexpr int KC = HD / 32, HT = HD / 16;
+  using L = AttnLds<HD>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (T + CH_QROWS - 1) / CH_QROWS, nbh = B * H;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);  // the last query block sweeps every key: first
+  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const int qbase = qblk * CH_QROWS + 16 * w;
+  const int q = qbase + j;
+  bf16x8 qf[KC], df[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    qf[kc] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + kc * 32 + 8 * g) : bf16x8{};
+    df[kc] = q < T ? *(const bf16x8*)(dOb + (long)q * dts + kc * 32 + 8 * g) : bf16x8{};
+  }
+  const float lq = q < T ? lse[((long)b * H + h) * T + q] * LOG2E : 0.f;
+  const float dlt = q < T ? delta[((long)b * H + h) * T + q] : 0.f;
+  const float c = scale * LOG2E;
+  f32x4 acc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto body = [&](const bf16* sK, const bf16* sV, int it) {
+#pragma unroll
+    for (int t2 = 0; t2 < CH_KEYS / 64; ++t2) {
+      const int k0 = it * CH_KEYS + t2 * 64;
+      if (k0 > qbase + 15 || qbase >= T) continue;  // wave-uniform: keys past every query of the wave
+      const bool diag = k0 + 63 > qbase;
+      const bf16* tK = sK + t2 * 64 * L::VLD;
+      const bf16* tV = sV + t2 * 64 * L::VLD;
+      f32x4 ds[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          sv = mfma(row_frag(tK, L::VLD, kt * 16, kc * 32, lane), qf[kc], sv);  // S^T[key][q]
+          dp = mfma(row_frag(tV, L::VLD, kt * 16, kc * 32, lane), df[kc], dp);  // dP^T[key][q]
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = fast_exp2(fmaf(sv[r], c, -lq));
+          if (diag) {
+            const int kk = k0 + kt * 16 + 4 * g + r;
+            pv = (kk <= q && kk < T && q < T) ? pv : 0.f;
+          }
+          ds[kt][r] = pv * (dp[r] - dlt);
+        }
+      }
+#pragma unroll
+      for (int hk = 0; hk < 2; ++hk) {
+        const bf16x8 dsb = pack_p(ds[2 * hk], ds[2 * hk + 1]);
+#pragma unroll
+        for (int t = 0; t < HT; ++t) acc[t] = mfma(tr_frag(tK, L::VLD, 32 * hk, t * 16, lane), dsb, acc[t]);
+      }
+    }
+  };
+  const int nch = (min(T, qblk * CH_QROWS + CH_QROWS) + CH_KEYS - 1) / CH_KEYS;
+  pipelined_tiles<HD, CH_KEYS, CH_THREADS>(nch, [](int it) { return it * CH_KEYS; }, Kb, ts, Vb, ts, T, lds, L::VLD,
+                                           L::VLD, tid, body);
+  if (q < T) {
+    bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+      *(bf16x4*)(pq + t * 16 + 4 * g) = bf16x4{f2bf(acc[t][0] * scale), f2bf(acc[t][1] * scale),
+                                               f2bf(acc[t][2] * scale), f2bf(acc[t][3] * scale)};
+  }
+}
+
 // delta = rowsum(dO * O) of one 8-wide chunk pair, combined over the 4 chunks of a 32-wide head
 // row in the order (c0 + c2) + (c1 + c3) — the dQ (group_sum) and dK/dV (xor shuffles) paths
 // produce bitwise identical values
@@ -1131,6 +1308,12 @@ bool use_resident(int T, int HD) {
          res_lds_dkdv(T, HD) <= LDS_MAX && res_lds_dq(T, HD) <= LDS_MAX;
 }
 
+// chunked kernels for what the resident ones cannot hold (DTC_ATTN_CHUNK=0: the 256-thread tiled kernels)
+bool attn_chunk_enabled() {
+  static const int v = [] { const char* e = getenv("DTC_ATTN_CHUNK"); return e ? atoi(e) : 1; }();
+  return v != 0;
+}
+
 template <typename K>
 void allow_lds(K kernel, long bytes) {  // > 64 KB of dynamic LDS must be opted into per kernel
   (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -1161,9 +1344,7 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
     DTC_CHECK_LAUNCH();
     return 0;
   }
-  // chunked kernel (DTC_ATTN_CHUNK=0: the 256-thread tiled kernel)
-  static const int chunk = [] { const char* v = getenv("DTC_ATTN_CHUNK"); return v ? atoi(v) : 1; }();
-  if (chunk && (HD == 32 || HD == 64)) {
+  if (attn_chunk_enabled() && (HD == 32 || HD == 64)) {
     const dim3 g(B * H * ((T + CH_QROWS - 1) / CH_QROWS));
     if (HD == 64) {
       allow_lds(attn_fwd_chunk_kernel<64>, ch_lds_fwd<64>());
@@ -1212,6 +1393,25 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
     allow_lds(attn_bwd_res_kernel<32>, lds_b);
     hipLaunchKernelGGL(attn_bwd_res_kernel<32>, dim3(B * H * 4), dim3(RES_THREADS), lds_b, st, qkv, o, dout, lse,
                        dqkv, B, T, H, scale);
+  } else if (attn_chunk_enabled() && (HD == 32 || HD == 64)) {
+    const dim3 g(B * H * ((T + CH_QROWS - 1) / CH_QROWS)), gk(B * H * ((T + CHB_KROWS - 1) / CHB_KROWS));
+    if (HD == 64) {
+      hipLaunchKernelGGL(attn_delta_kernel<64>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
+      allow_lds(attn_bwd_dkdv_chunk_kernel<64>, ch_lds_bwd<64>());
+      allow_lds(attn_bwd_dq_chunk_kernel<64>, ch_lds_bwd<64>());
+      hipLaunchKernelGGL(attn_bwd_dkdv_chunk_kernel<64>, gk, dim3(CHB_THREADS), ch_lds_bwd<64>(), st, qkv, dout, lse, ws,
+                         dqkv, B, T, H, scale);
+      hipLaunchKernelGGL(attn_bwd_dq_chunk_kernel<64>, g, dim3(CH_THREADS), ch_lds_bwd<64>(), st, qkv, dout, lse, ws,
+                         dqkv, B, T, H, scale);
+    } else {
+      hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
+      allow_lds(attn_bwd_dkdv_chunk_kernel<32>, ch_lds_bwd<32>());
+      allow_lds(attn_bwd_dq_chunk_kernel<32>, ch_lds_bwd<32>());
+      hipLaunchKernelGGL(attn_bwd_dkdv_chunk_kernel<32>, gk, dim3(CHB_THREADS), ch_lds_bwd<32>(), st, qkv, dout, lse, ws,
+                         dqkv, B, T, H, scale);
+      hipLaunchKernelGGL(attn_bwd_dq_chunk_kernel<32>, g, dim3(CH_THREADS), ch_lds_bwd<32>(), st, qkv, dout, lse, ws,
+                         dqkv, B, T, H, scale);
+    }
   } else if (HD == 32) {
     hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<32>, grid, dim3(256), 0, st, qkv, dout, lse, ws, dqkv, B, T, H, scale);
