@@ -742,11 +742,14 @@ __global__ void __launch_bounds__(CHB_THREADS) attn_bwd_dkdv_chunk_kernel(
   }
 }
 
-// dQ: block = (b, h, 256 queries); wave w owns queries qb0 + 16w .. +15 (query on the lane)
+// dQ: block = (b, h, 256 queries); wave w owns queries qb0 + 16w .. +15 (query on the lane).  Also
+// computes delta = rowsum(dO * O) of its queries (from the dO / O fragments it holds) and writes
+// it for the dK/dV kernel, which runs after it: no separate delta pass.
 template <int HD>
 __global__ void __launch_bounds__(CH_THREADS) attn_bwd_dq_chunk_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
+    float scale) {
   constexpr int KC = HD / 32, HT = HD / 16;
   using L = AttnLds<HD>;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
@@ -769,7 +772,15 @@ __global__ void __launch_bounds__(CH_THREADS) attn_bwd_dq_chunk_kernel(
     df[kc] = q < T ? *(const bf16x8*)(dOb + (long)q * dts + kc * 32 + 8 * g) : bf16x8{};
   }
   const float lq = q < T ? lse[((long)b * H + h) * T + q] * LOG2E : 0.f;
-  const float dlt = q < T ? delta[((long)b * H + h) * T + q] : 0.f;
+  float dpart = 0.f;  // this lane's share of rowsum(dO * O): hd columns kc*32 + 8g .. +7
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    const bf16x8 of = q < T ? *(const bf16x8*)(o + ((long)b * T + q) * dts + h * HD + kc * 32 + 8 * g) : bf16x8{};
+#pragma unroll
+    for (int r = 0; r < 8; ++r) dpart += (float)of[r] * (float)df[kc][r];
+  }
+  const float dlt = group_sum(dpart);
+  if (g == 0 && q < T) delta[((long)b * H + h) * T + q] = dlt;
   const float c = scale * LOG2E;
   f32x4 acc[HT];
 #pragma unroll
@@ -1396,20 +1407,20 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
   } else if (attn_chunk_enabled() && (HD == 32 || HD == 64)) {
     const dim3 g(B * H * ((T + CH_QROWS - 1) / CH_QROWS)), gk(B * H * ((T + CHB_KROWS - 1) / CHB_KROWS));
     if (HD == 64) {
-      hipLaunchKernelGGL(attn_delta_kernel<64>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
       allow_lds(attn_bwd_dkdv_chunk_kernel<64>, ch_lds_bwd<64>());
       allow_lds(attn_bwd_dq_chunk_kernel<64>, ch_lds_bwd<64>());
+      // dQ first: it writes delta (ws) for the dK/dV kernel
+      hipLaunchKernelGGL(attn_bwd_dq_chunk_kernel<64>, g, dim3(CH_THREADS), ch_lds_bwd<64>(), st, qkv, o, dout, lse,
+                         ws, dqkv, B, T, H, scale);
       hipLaunchKernelGGL(attn_bwd_dkdv_chunk_kernel<64>, gk, dim3(CHB_THREADS), ch_lds_bwd<64>(), st, qkv, dout, lse, ws,
                          dqkv, B, T, H, scale);
-      hipLaunchKernelGGL(attn_bwd_dq_chunk_kernel<64>, g, dim3(CH_THREADS), ch_lds_bwd<64>(), st, qkv, dout, lse, ws,
-                         dqkv, B, T, H, scale);
     } else {
-      hipLaunchKernelGGL(attn_delta_kernel<32>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
       allow_lds(attn_bwd_dkdv_chunk_kernel<32>, ch_lds_bwd<32>());
       allow_lds(attn_bwd_dq_chunk_kernel<32>, ch_lds_bwd<32>());
+      // dQ first: it writes delta (ws) for the dK/dV kernel
+      hipLaunchKernelGGL(attn_bwd_dq_chunk_kernel<32>, g, dim3(CH_THREADS), ch_lds_bwd<32>(), st, qkv, o, dout, lse,
+                         ws, dqkv, B, T, H, scale);
       hipLaunchKernelGGL(attn_bwd_dkdv_chunk_kernel<32>, gk, dim3(CHB_THREADS), ch_lds_bwd<32>(), st, qkv, dout, lse, ws,
-                         dqkv, B, T, H, scale);
-      hipLaunchKernelGGL(attn_bwd_dq_chunk_kernel<32>, g, dim3(CH_THREADS), ch_lds_bwd<32>(), st, qkv, dout, lse, ws,
                          dqkv, B, T, H, scale);
     }
   } else if (HD == 32) {
