@@ -268,7 +268,7 @@ def test_lmhead_ce(cuda, M, D, V, Vp):
     assert logits[:, V:].abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize("M,D,V,Vp,vstart", [(4096, 512, 50258, 50304, 0), (1024, 256, 25129, 25152, 25129),
+@pytest.mark.parametrize("M,D,V,Vp,vstart", [(4096, 512, 50258, 50304, 0), (1024, 256, 25129, 25152, 25129), (1000, 256, 30000, 30016, 0),
                                              (512, 256, 1000, 1024, 0)])
 def test_ce_dgrad_fused_matches_unfused(cuda, M, D, V, Vp, vstart):
     """ce_dgrad_fused (CE backward inside the lm_head dgrad's operand staging) == ce_backward_inplace +
