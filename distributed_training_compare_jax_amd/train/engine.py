@@ -199,9 +199,10 @@ class Engine:
     def _reserve_workspaces(self):
         from ..ops.gemm import reserve_workspace
 
-        reserve_workspace(self.device, 64 << 20)
+        # split-K slabs: the lm_head dgrad (fused CE, split 8 at the reference size) needs 67 MB
+        reserve_workspace(self.device, 96 << 20)
         if self.stage.side.stream is not None:
-            reserve_workspace(self.device, 64 << 20, role="side")
+            reserve_workspace(self.device, 96 << 20, role="side")
 
     @property
     def tokens_per_step(self) -> int:
