@@ -218,7 +218,11 @@ __device__ __forceinline__ void stage_put(bf16* st, int row, int chunk, bf16x4 v
   *(bf16x4*)(st + row * 64 + ((chunk ^ (row & 15)) << 2)) = v;
 }
 
-template <int ROWS>
+// NT: non-temporal stores (streamed past L2/MALL) for outputs no kernel reads soon: the 412 MB of
+// logits, gelu'(u) (read in the backward).  Measured per kernel in the step: those gain (lm_head
+// forward -19 us, and the CE backward reading after it -17 us), while outputs the NEXT kernel
+// reads (qkv -> attention, dgrads -> LayerNorm backward) lose as much as their producer gains.
+template <int ROWS, bool NT = false>
 __device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int m_base, int n_base, int M, int N,
                                           int lane) {
   if (m_base + ROWS <= M && n_base + 64 <= N) {  // interior tile (wave-uniform): no per-row checks
@@ -227,7 +231,9 @@ __device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int
       const int row = it * 8 + (lane >> 3), p = lane & 7;
       u32x4 v = *(const u32x4*)(st + row * 64 + ((p ^ ((row >> 1) & 7)) << 3));
       if (row & 1) v = u32x4{v[2], v[3], v[0], v[1]};
-      DTC_OUT_STORE((u32x4*)(C + (long)(m_base + row) * ldc + n_base + p * 8), v);
+      u32x4* dst = (u32x4*)(C + (long)(m_base + row) * ldc + n_base + p * 8);
+      if (NT) __builtin_nontemporal_store(v, dst);
+      else DTC_OUT_STORE(dst, v);
     }
     return;
   }
@@ -240,7 +246,8 @@ __device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int
     if (m >= M) continue;
     bf16* c = C + (long)m * ldc + n;
     if (n + 8 <= N) {
-      DTC_OUT_STORE((u32x4*)c, v);
+      if (NT) __builtin_nontemporal_store(v, (u32x4*)c);
+      else DTC_OUT_STORE((u32x4*)c, v);
     } else {
       const bf16x8 b = __builtin_bit_cast(bf16x8, v);
       for (int r = 0; r < 8; ++r) if (n + r < N) c[r] = b[r];
@@ -407,7 +414,7 @@ __device__ __forceinline__ void lmhead_rows(const f32x4 (&acc)[TN][TM], const Ep
       if (row < TM * 16 && m < e.M && d >= 0 && d < TN * 16 && pre.labr[q] < e.n_valid)
         e.label_out[m] = (float)stage[row * 64 + ((((d >> 2) ^ (row & 15))) << 2) + (d & 3)];
     }
-    stage_out<TM * 16>(stage, (bf16*)e.C, e.ldc, m_base, n_base, e.M, e.N, lane);
+    stage_out<TM * 16, true>(stage, (bf16*)e.C, e.ldc, m_base, n_base, e.M, e.N, lane);  // logits: NT
   }
 }
 
@@ -701,7 +708,9 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
           }
           stage_put(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
         }
-      stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
+      // GELU pass 0 = gelu'(u), read only in the backward: non-temporal
+      if (EPI == EPI_GELU && pass == 0) stage_out<WM, true>(stg, (bf16*)e.C, e.ldc, mb, nb, M, N, lane);
+      else stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
     }
     return;
   }
@@ -1481,7 +1490,9 @@ gemm_dmaw_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ 
           }
           stage_put(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
         }
-      stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
+      // GELU pass 0 = gelu'(u), read only in the backward: non-temporal
+      if (EPI == EPI_GELU && pass == 0) stage_out<WM, true>(stg, (bf16*)e.C, e.ldc, mb, nb, M, N, lane);
+      else stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
     }
     return;
   }
