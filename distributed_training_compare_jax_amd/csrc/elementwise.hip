@@ -466,7 +466,14 @@ __global__ void __launch_bounds__(256) transpose_batch_kernel(TrBatch batch) {
     bf16x8 v;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = tile[ch + e][dr];
-    if (c0 + dr < T.cols && r0 + ch + 8 <= T.rows) *(bf16x8*)(T.dst + (long)(c0 + dr) * T.rows + r0 + ch) = v;
+    // non-temporal: the transposed mirror is read only in the backward (DTC_TR_CACHED: cached stores)
+    if (c0 + dr < T.cols && r0 + ch + 8 <= T.rows) {
+#ifdef DTC_TR_CACHED
+      *(bf16x8*)(T.dst + (long)(c0 + dr) * T.rows + r0 + ch) = v;
+#else
+      __builtin_nontemporal_store(v, (bf16x8*)(T.dst + (long)(c0 + dr) * T.rows + r0 + ch));
+#endif
+    }
   }
 }
 
