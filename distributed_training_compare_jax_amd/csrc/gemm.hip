@@ -1043,7 +1043,9 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
       for (int e = 0; e < 8; ++e) o[e] = f2bf(gv[e]);
       const int row = q * 64 + srow;
       *(bf16x8*)(img + row * 64 + spos * 8) = o;
-      if (lead && ok_r[q]) *(bf16x8*)(a.dlogits + (long)(m0 + row) * a.ldd + v0) = o;
+      // non-temporal: 412 MB that would otherwise push the last layers' saved activations out of
+      // the Infinity Cache right before their backward (measured -12..-29 us/step)
+      if (lead && ok_r[q]) __builtin_nontemporal_store(o, (bf16x8*)(a.dlogits + (long)(m0 + row) * a.ldd + v0));
     }
   };
 
