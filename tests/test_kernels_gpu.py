@@ -101,8 +101,10 @@ def test_gemm_nn(cuda, M, N, K):
 
 
 @pytest.mark.parametrize("Mtok,N,K", [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048),
-                                      (4096, 50304, 512), (128, 64, 64), (512, 200, 96), (3072, 50000, 384)])
+                                      (4096, 50304, 512), (128, 64, 64), (512, 200, 96), (3072, 50000, 384),
+                                      (4096, 45000, 512), (1024, 32768, 512)])
 def test_gemm_wgrad(cuda, Mtok, N, K):
+    """Weight gradients; the vocab-sized ones (32768-50304 rows) run on the 256^2 kernel."""
     dy, x = _r(Mtok, N, seed=8), _r(Mtok, K, seed=9)
     dw = torch.full((N, K), 3.0, device=cuda)
     G.wgrad(dy, x, dw, beta=0.0)
