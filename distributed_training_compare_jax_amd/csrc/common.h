@@ -65,7 +65,35 @@ struct RedBatch {
   RedTask t[RED_MAX_TASKS];
 };
 
-enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_LMHEAD = 4, EPI_NONE = 99 /* microbench: no store */ };
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_LMHEAD = 4,
+       EPI_RESID_LN = 5,  // x = resid + acc + bias (fp32 C) and y = LayerNorm(x) (bf16) + row mean/rstd
+       EPI_LN_BWD = 6,    // acc = dy: C = dres + LayerNorm'(dy) (fp32) + bf16 copy + dgamma/dbeta/dbias partials
+       EPI_NONE = 99 /* microbench: no store */ };
+
+// Mirror of ops/_native.py LnArgs (keep field order and types identical): a layer GEMM with the
+// LayerNorm that follows it fused into the epilogue (csrc/gemm.hip dtc_gemm_ln).
+struct LnArgs {
+  int bwd;                  // 0: EPI_RESID_LN, 1: EPI_LN_BWD
+  int M, N, K;
+  const void* A; long lda;  // bf16 [M][K]
+  const void* B; long ldb;  // bf16 [N][K] (the weight, or the transposed weight of an NT dgrad)
+  float* C;                 // fp32 [M][N]: fwd x = resid + A.B^T + bias; bwd dx
+  const float* bias;        // fwd
+  const float* resid;       // fwd residual / bwd residual gradient dres (may be null in bwd)
+  const float* gamma;
+  const float* beta;        // fwd
+  void* y;                  // bf16 [M][N]: fwd LayerNorm(x); bwd bf16 copy of dx
+  float* mean;              // fwd out, bwd in
+  float* rstd;              // fwd out, bwd in
+  const float* x;           // bwd: the LayerNorm input
+  float* part;              // bwd: column partials [M/128][nslab][N] (dgamma, dbeta[, dbias = sum dx])
+  int nslab;
+  float eps;
+  unsigned long long* sync; // dtc_gemm_ln_sync_words(M, N) words, zero-initialised once
+  const long long* step;    // device step counter: epoch = step * nsites + site + 1
+  int site, nsites;
+  unsigned* err;            // set when a row-statistics wait timed out (outputs are NaN then)
+};
 
 #define DTC_CHECK_LAUNCH() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
 

@@ -136,6 +136,16 @@ __device__ __forceinline__ void colsum_store(const float (&cs)[8], float* red, f
   }
 }
 
+// LayerNorm fused into a layer GEMM's epilogue (EPI_RESID_LN / EPI_LN_BWD; see ln_fwd_epilogue)
+struct LnEpi {
+  const float* gamma; const float* beta;
+  bf16* y; float* mean; float* rstd;
+  const float* x; float* part; int nslab;
+  float eps;
+  unsigned long long* sync; const long long* step; int site, nsites;
+  unsigned* err;
+};
+
 struct Epi {
   int M, N;
   void* C; long ldc;
@@ -147,6 +157,7 @@ struct Epi {
   float* part; int nparts;
   float* label_out;
   float* colsum;
+  LnEpi ln;
 };
 
 // Output stores of the GEMM epilogues.  DTC_NT_STORES: non-temporal (streamed past L2), so a
@@ -309,6 +320,248 @@ __device__ __forceinline__ void staged_f32_epilogue(const f32x4 (&acc)[TN][TM], 
       stage_put_f32<WN>(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), v);
     }
   stage_out_f32<WM, WN>(stg, C, ldc, mb, nb, M, N, lane, res, ldres, beta);
+}
+
+// ---- LayerNorm fused into the layer GEMM epilogue (tp = pp = 1) ---------------------------------
+// The GEMM that writes the fp32 residual stream x (out_proj / fc2 forward) also emits y = LN(x) in
+// bf16 with the row mean / rstd, and the NT dgrad that produces a LayerNorm's output gradient dy
+// (fc1 / qkv backward) finishes the LayerNorm backward itself (dy is never stored): one launch and
+// one full [M, D] pass less per LayerNorm.  A row of D columns is spread over D/64 blocks (2 waves
+// of 32 columns each), so the row statistics are exchanged INSIDE the launch
+// (cdna_hip_programming.md Guideline 16, R1): every wave stores one packed pair of partials per
+// (row, 32-column chunk) with write-through `sc1` stores (agent-scope relaxed atomics) and drains
+// them (vmcnt(0)); after a block barrier one lane raises the block's flag = epoch; wave 0 of every
+// block polls its row group's D/64 flags (one per lane, relaxed), and after a barrier every wave
+// reads the partials with `sc1` loads only (no acquire fence needed).  The fp32 output stores are
+// issued between publishing and waiting, so they drain while the row group catches up.
+// epoch = step * nsites + site + 1 (device step counter, so it advances under hipGraph replay; sites
+// numbered in execution order, so two consecutive uses of the shared buffer never carry the same tag).
+// Liveness: the fused launches map blocks so that each XCD's dispatch order visits a row group's
+// D/64 tiles consecutively, so a group only waits on blocks dispatched before any later group's;
+// every spin is bounded (LN_SPIN_MAX): on a timeout the rows' statistics become NaN (so does the
+// loss) and `err` is set, never a hang.
+// Forward statistics: per-chunk mean and M2 = sum (x - mean_c)^2, combined with Chan's formula in a
+// fixed order (bitwise reproducible, two-pass accuracy).
+// sync layout (u64 words): partials [M][D/32] (lo = first, hi = second float), flags [M/128][D/64].
+#ifndef LN_SPIN_MAX
+#define LN_SPIN_MAX (1u << 17)
+#endif
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+
+__device__ __forceinline__ void pay_store(unsigned long long* p, float a, float b) {
+  __hip_atomic_store((gu64_t*)p, ((unsigned long long)__float_as_uint(b) << 32) | __float_as_uint(a), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f32x2 pay_load(const unsigned long long* p) {
+  const unsigned long long u = __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return f32x2{__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32))};
+}
+
+// every wave's sc1 partial stores drained, then ONE lane raises this block's flag
+__device__ __forceinline__ void ln_publish(unsigned long long* flag, unsigned epoch, int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store((gu64_t*)flag, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 polls the row group's `n` flags (lane k <- flag k), the result is broadcast through LDS
+__device__ __forceinline__ bool ln_wait_group(const unsigned long long* flags, int n, unsigned epoch, int* lds_ok,
+                                              int wave, int lane) {
+  if (wave == 0) {
+    bool ok = false;
+    for (unsigned spins = 0;; ++spins) {
+      bool mine = true;
+      if (lane < n)
+        mine = (unsigned)__hip_atomic_load((gu64_t*)(flags + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (__all(mine)) {
+        ok = true;
+        break;
+      }
+      if (spins >= LN_SPIN_MAX) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *lds_ok = ok ? 1 : 0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the poll
+  return *lds_ok != 0;
+}
+
+__device__ __forceinline__ float sum8(float v) {  // over the 8 lanes of a row (xor butterfly: same in all 8)
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v;
+}
+
+__device__ __forceinline__ void ln_flag_error(const LnEpi& L, int lane) {
+  if (lane == 0) __hip_atomic_store((gu32_t*)L.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// EPI_RESID_LN.  Wave tile WM x 32 (TM x 2 fragments).  Row pass as stage_out_f32: lane handles row
+// it*8 + lane/8, columns 4*(lane%8) .. +3 of the wave's 32.
+template <int TN, int TM, int WM, int WN, int WGM, int WGN>
+__device__ __forceinline__ void ln_fwd_epilogue(const f32x4 (&acc)[TN][TM], float* stg, int* lds_ok, const Epi& e,
+                                                int m0, int n0, int wm, int wn, int wave, int lane, int tid,
+                                                const f32x4 (&bb)[TN]) {
+  static_assert(WN == 32 && WM % 8 == 0, "LN epilogue: 32-column wave tiles");
+  constexpr int IT = WM / 8;
+  const LnEpi& L = e.ln;
+  const int mb = m0 + wm * WM, nb = n0 + wn * WN;
+  const int N = e.N, nch = N / 32, nq = nch / 8, chunk = nb / 32, tiles_n = N / (WN * WGN);
+  const int rr = lane >> 3, p = lane & 7, n = nb + p * 4;
+  const f32x4 gv = *(const f32x4*)(L.gamma + n), bv = *(const f32x4*)(L.beta + n);
+  const unsigned epoch = (unsigned)(*L.step) * (unsigned)L.nsites + (unsigned)L.site + 1u;
+  unsigned long long* pay = L.sync;
+  unsigned long long* flags = L.sync + (long)e.M * nch + (long)(m0 / (WM * WGM)) * tiles_n;
+#pragma unroll
+  for (int j = 0; j < TM; ++j)
+#pragma unroll
+    for (int i = 0; i < TN; ++i) stage_put_f32<WN>(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), acc[i][j] + bb[i]);
+  f32x4 xv[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int row = it * 8 + rr, m = mb + row;
+    f32x4 v = *(const f32x4*)(stg + row * WN + ((p ^ (row & 7)) << 2));
+    v += *(const f32x4*)((const float*)e.aux + (long)m * e.ldaux + n);
+    xv[it] = v;
+    const float mc = sum8((v[0] + v[1]) + (v[2] + v[3])) * (1.f / 32.f);
+    const f32x4 d = v - mc;
+    const float m2 = sum8((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]));
+    if (p == 0) pay_store(pay + (long)m * nch + chunk, mc, m2);
+  }
+  ln_publish(flags + n0 / (WN * WGN), epoch, tid);
+#pragma unroll
+  for (int it = 0; it < IT; ++it)  // the residual stream itself drains while the row group catches up
+    *(f32x4*)((float*)e.C + (long)(mb + it * 8 + rr) * e.ldc + n) = xv[it];
+  const bool ok = ln_wait_group(flags, tiles_n, epoch, lds_ok, wave, lane);
+  if (!ok) ln_flag_error(L, lane);
+  const float inv_nch = 1.f / (float)nch, inv_n = 1.f / (float)N;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int m = mb + it * 8 + rr;
+    f32x2 pv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pv[q] = q < nq ? pay_load(pay + (long)m * nch + p + 8 * q) : f32x2{0.f, 0.f};
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) if (q < nq) s += pv[q][0];
+    const float mean = sum8(s) * inv_nch;
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < nq) {
+        const float d = pv[q][0] - mean;
+        t += fmaf(32.f * d, d, pv[q][1]);
+      }
+    float rstd = rsqrtf(sum8(t) * inv_n + L.eps);
+    const float mu = ok ? mean : __builtin_nanf("");
+    if (!ok) rstd = __builtin_nanf("");
+    const f32x4 o = (xv[it] - mu) * rstd * gv + bv;
+    *(bf16x4*)(L.y + (long)m * N + n) = __builtin_convertvector(o, bf16x4);
+    if (chunk == 0 && p == 0) {
+      L.mean[m] = mu;
+      L.rstd[m] = rstd;
+    }
+  }
+}
+
+// EPI_LN_BWD: acc = dy (the LayerNorm's output gradient, never stored).  C = dres + LN'(dy) (fp32),
+// ln.y = bf16 copy, and this block's column partials over its BM rows of dgamma = sum dy*xhat,
+// dbeta = sum dy (and dbias = sum dx when nslab == 3) -> part[m0/BM][s][n].  `red`: LDS scratch of
+// NW*3*32 floats past the per-wave stages.
+template <int TN, int TM, int WM, int WN, int WGM, int WGN>
+__device__ __forceinline__ void ln_bwd_epilogue(const f32x4 (&acc)[TN][TM], float* stg, float* red, int* lds_ok,
+                                                const Epi& e, int m0, int n0, int wm, int wn, int wave, int lane,
+                                                int tid) {
+  static_assert(WN == 32 && WM % 8 == 0, "LN epilogue: 32-column wave tiles");
+  constexpr int IT = WM / 8;
+  const LnEpi& L = e.ln;
+  const int mb = m0 + wm * WM, nb = n0 + wn * WN;
+  const int N = e.N, nch = N / 32, nq = nch / 8, chunk = nb / 32, tiles_n = N / (WN * WGN);
+  const int rr = lane >> 3, p = lane & 7, n = nb + p * 4;
+  const f32x4 gv = *(const f32x4*)(L.gamma + n);
+  const unsigned epoch = (unsigned)(*L.step) * (unsigned)L.nsites + (unsigned)L.site + 1u;
+  unsigned long long* pay = L.sync;
+  unsigned long long* flags = L.sync + (long)e.M * nch + (long)(m0 / (WM * WGM)) * tiles_n;
+#pragma unroll
+  for (int j = 0; j < TM; ++j)
+#pragma unroll
+    for (int i = 0; i < TN; ++i) stage_put_f32<WN>(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), acc[i][j]);
+  f32x4 gd[IT], xh[IT];
+  float rs[IT];
+  f32x4 cg = {0.f, 0.f, 0.f, 0.f}, cb = cg, co = cg;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int row = it * 8 + rr, m = mb + row;
+    const f32x4 dy = *(const f32x4*)(stg + row * WN + ((p ^ (row & 7)) << 2));
+    const f32x4 xv = *(const f32x4*)(L.x + (long)m * N + n);
+    rs[it] = L.rstd[m];
+    xh[it] = (xv - L.mean[m]) * rs[it];
+    gd[it] = dy * gv;
+    cg += dy * xh[it];
+    cb += dy;
+    const float s1 = sum8((gd[it][0] + gd[it][1]) + (gd[it][2] + gd[it][3]));
+    const f32x4 t2 = gd[it] * xh[it];
+    const float s2 = sum8((t2[0] + t2[1]) + (t2[2] + t2[3]));
+    if (p == 0) pay_store(pay + (long)m * nch + chunk, s1, s2);
+  }
+  ln_publish(flags + n0 / (WN * WGN), epoch, tid);
+  const float* dres = (const float*)e.aux;
+  f32x4 rv[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it)  // residual-gradient loads in flight while the row group catches up
+    rv[it] = dres ? *(const f32x4*)(dres + (long)(mb + it * 8 + rr) * e.ldaux + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool ok = ln_wait_group(flags, tiles_n, epoch, lds_ok, wave, lane);
+  if (!ok) ln_flag_error(L, lane);
+  const float inv_n = 1.f / (float)N;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int m = mb + it * 8 + rr;
+    f32x2 pv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pv[q] = q < nq ? pay_load(pay + (long)m * nch + p + 8 * q) : f32x2{0.f, 0.f};
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < nq) {
+        a += pv[q][0];
+        b += pv[q][1];
+      }
+    float c1 = sum8(a) * inv_n;
+    const float c2 = sum8(b) * inv_n;
+    if (!ok) c1 = __builtin_nanf("");
+    const f32x4 o = (gd[it] - c1 - xh[it] * c2) * rs[it] + rv[it];
+    *(f32x4*)((float*)e.C + (long)m * e.ldc + n) = o;
+    *(bf16x4*)(L.y + (long)m * N + n) = __builtin_convertvector(o, bf16x4);
+    co += o;
+  }
+  // column partials: over the wave's 4 row groups of 8 lanes (same p), then over the WGM waves along M
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      cg[r] += __shfl_xor(cg[r], o, 64);
+      cb[r] += __shfl_xor(cb[r], o, 64);
+      co[r] += __shfl_xor(co[r], o, 64);
+    }
+  }
+  const int w = wm * WGN + wn;
+  if (rr == 0) {
+    *(f32x4*)(red + (w * 3 + 0) * 32 + p * 4) = cg;
+    *(f32x4*)(red + (w * 3 + 1) * 32 + p * 4) = cb;
+    *(f32x4*)(red + (w * 3 + 2) * 32 + p * 4) = co;
+  }
+  __syncthreads();
+  const int nslab = L.nslab;
+  if (tid < nslab * WGN * 32) {
+    const int s = tid / (WGN * 32), c = tid % (WGN * 32), cw = c / 32, cc = c % 32;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < WGM; ++k) v += red[((k * WGN + cw) * 3 + s) * 32 + cc];
+    L.part[((long)(m0 / (WM * WGM)) * nslab + s) * N + n0 + c] = v;
+  }
 }
 
 // lm_head epilogue: logits (bf16) + per-row partial (max, sum exp) over this wave's TN*16 columns +
@@ -1367,7 +1620,10 @@ gemm_dmaw_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ 
   const int tile = lid % ntiles, z = lid / ntiles;
   const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
   const int gm_eff = min(gm, tiles_m - grp * gm);
-  const int m0 = (grp * gm + in_g % gm_eff) * BM, n0 = (in_g / gm_eff) * BN;
+  // LayerNorm epilogues: N fastest, so a row group's tiles are consecutive in each XCD's dispatch order
+  constexpr bool LNE = EPI == EPI_RESID_LN || EPI == EPI_LN_BWD;
+  const int m0 = LNE ? (tile / tiles_n) * BM : (grp * gm + in_g % gm_eff) * BM;
+  const int n0 = LNE ? (tile % tiles_n) * BN : (in_g / gm_eff) * BN;
   const int kbeg = z * k_per_split;
   const int nk = min(k_per_split, K - kbeg) / 64;
   const int g4 = 4 * (lane >> 4);
@@ -1445,6 +1701,19 @@ gemm_dmaw_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ 
   }
   if (nk > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   raw_barrier();  // every wave's last fragment reads are done: the ring is free for the stages
+  if constexpr (EPI == EPI_RESID_LN) {
+    static_assert(OUTF32 && (NW * WM * WN + 1) * 4 <= LDS_BYTES, "LN epilogue stage");
+    ln_fwd_epilogue<TN, TM, WM, WN, WGM, WGN>(acc, (float*)smem + wave * (WM * WN), (int*)((float*)smem + NW * WM * WN),
+                                              e, m0, n0, wm, wn, wave, lane, tid, bpre);
+    return;
+  }
+  if constexpr (EPI == EPI_LN_BWD) {
+    static_assert(OUTF32 && (NW * WM * WN + NW * 3 * 32 + 1) * 4 <= LDS_BYTES, "LN epilogue stage");
+    float* const red = (float*)smem + NW * WM * WN;
+    ln_bwd_epilogue<TN, TM, WM, WN, WGM, WGN>(acc, (float*)smem + wave * (WM * WN), red, (int*)(red + NW * 3 * 32), e, m0,
+                                              n0, wm, wn, wave, lane, tid);
+    return;
+  }
   if constexpr (ST32) {
     if (split > 1 || (OUTF32 && (EPI == EPI_STORE || EPI == EPI_RESID))) {
       const bool sp = split > 1;
@@ -1903,6 +2172,38 @@ int dtc_ce_dgrad(const bf16* logits, long ldl, const float* lse, const int* labe
   DTC_CHECK_LAUNCH();
   return 0;
 }
+
+// Layer GEMM (NT, both operands K-major) with the LayerNorm that follows it fused into the epilogue:
+// a->bwd == 0: C = resid + A.B^T + bias, y = LN(C) (bf16), mean/rstd;  a->bwd == 1: dy = A.B^T (never
+// stored), C = dres + LN'(dy), y = bf16(C), column partials in `part`.  128x64 tiles on the 8-wave DMA
+// kernel (the plan the unfused fp32 forwards / dgrads of these shapes use).  Shapes: M % 128, N % 256,
+// N <= 1024, K % 64.
+int dtc_gemm_ln(const LnArgs* a, hipStream_t st) {
+  if (a->M <= 0 || a->M % 128 || a->N % 256 || a->N > 1024 || a->K <= 0 || a->K % 64) return 1400;
+  if (a->lda % 8 || a->ldb % 8) return 1400;
+  if (!a->sync || !a->step || !a->gamma || !a->err || !a->C || !a->y || !a->mean || !a->rstd) return 1401;
+  if (a->bwd ? (!a->x || !a->part || a->nslab < 2 || a->nslab > 3) : (!a->resid || !a->beta)) return 1402;
+  Epi e{};
+  e.M = a->M; e.N = a->N; e.C = a->C; e.ldc = a->N; e.bias = a->bwd ? nullptr : a->bias;
+  e.aux = a->resid; e.ldaux = a->N; e.alpha = 1.f;
+  e.ln.gamma = a->gamma; e.ln.beta = a->beta; e.ln.y = (bf16*)a->y; e.ln.mean = a->mean; e.ln.rstd = a->rstd;
+  e.ln.x = a->x; e.ln.part = a->part; e.ln.nslab = a->nslab; e.ln.eps = a->eps;
+  e.ln.sync = a->sync; e.ln.step = a->step; e.ln.site = a->site; e.ln.nsites = a->nsites; e.ln.err = a->err;
+  const int tiles_m = a->M / 128, tiles_n = a->N / 64;
+  const dim3 grid(tiles_m * tiles_n), block(512);
+  if (a->bwd)
+    hipLaunchKernelGGL((gemm_dmaw_kernel<128, 64, 4, 4, 2, true, true, EPI_LN_BWD, true>), grid, block, 0, st,
+                       (const bf16*)a->A, a->lda, (const bf16*)a->B, a->ldb, a->M, a->N, a->K, tiles_m, tiles_n, tiles_m,
+                       1, a->K, nullptr, e);
+  else
+    hipLaunchKernelGGL((gemm_dmaw_kernel<128, 64, 4, 4, 2, true, true, EPI_RESID_LN, true>), grid, block, 0, st,
+                       (const bf16*)a->A, a->lda, (const bf16*)a->B, a->ldb, a->M, a->N, a->K, tiles_m, tiles_n, tiles_m,
+                       1, a->K, nullptr, e);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+long dtc_gemm_ln_sync_words(int M, int N) { return (long)M * (N / 32) + (long)(M / 128) * (N / 64); }
 
 int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N + 255) / 256) * 4 : ((N + 127) / 128) * 2; }
 

@@ -30,6 +30,7 @@ from ..ops import attention as A
 from ..ops import embedding as E
 from ..ops import gemm as G
 from ..ops import layernorm as LN
+from ..ops import ln_fused as LF
 from ..ops import xent as X
 from ..ops.reduce import GradReducer
 from ..parallel.buffers import FlatParams
@@ -146,6 +147,28 @@ class GPTStage:
         self.v_start = self.tp.rank * self.v_local
         self.v_valid = max(0, min(self.v_local, cfg.vocab_size - self.v_start))
         self.eps = cfg.layernorm_eps
+        # LayerNorm fused into the layer GEMMs (ops/ln_fused.py), set up by enable_ln_fusion
+        self.ln_sync: Optional[LF.LnSync] = None
+        self._fuse_fwd = self._fuse_bwd = False
+
+    def enable_ln_fusion(self, tokens: int, step: torch.Tensor, fwd: bool, bwd: bool) -> bool:
+        """Fuse the LayerNorms into the GEMMs that produce their input (forward) and their output
+        gradient (backward).  Needs tp = 1 (no all-reduce between the GEMM and the LayerNorm), one
+        call per site and step (no pipeline microbatches) and the transposed weight mirror for the
+        NT dgrads; ``tokens`` = rows of every call.  Returns whether anything was enabled."""
+        D, L = self.cfg.d_model, len(self.layout.layers)
+        if self.tp.size != 1 or not L or not LF.supported(tokens, D, 64) or not (fwd or bwd):
+            return False
+        self.ln_sync = LF.LnSync(self.flat.device, tokens, D, nsites=4 * L, step=step)
+        self._fuse_fwd, self._fuse_bwd = bool(fwd), bool(bwd)
+        return True
+
+    def _ln_site(self, l: int, k: int, backward: bool) -> int:
+        """Execution-order index of a fused LayerNorm call: forward k = 0 (out_proj → ln2) / 1 (fc2 →
+        the next ln1 or lnf) of layer l; backward k = 0 (ln2) / 1 (ln1), layers in reverse."""
+        L = len(self.layout.layers)
+        li = l - self.layout.layers[0]
+        return 2 * L + 2 * (L - 1 - li) + k if backward else 2 * li + k
 
     # ------------------------------------------------------------------ embed
     def embed_forward(self, ids: torch.Tensor, step: torch.Tensor, row0: int, ctx: Dict,
@@ -201,16 +224,30 @@ class GPTStage:
         tp = self.tp
         lead = tp.rank == 0  # row-parallel bias + residual are added by exactly one TP rank
         T = x.shape[0] // batch
-        y1, mu1, rs1 = LN.layernorm_fwd(x, f.p(p + "ln1.g"), f.p(p + "ln1.b"), self.eps, self.act_dtype)
+        pre = ctx.pop(("ln1", l), None)  # LN1 already produced by the previous layer's fc2 GEMM
+        if pre is None:
+            pre = LN.layernorm_fwd(x, f.p(p + "ln1.g"), f.p(p + "ln1.b"), self.eps, self.act_dtype)
+        y1, mu1, rs1 = pre
         qkv = G.linear(y1, f.w(p + "qkv.w"), f.p(p + "qkv.b"))
         o, lse = A.attn_fwd(qkv.view(batch, T, -1), self.heads_local)
         o = o.view(batch * T, -1)
-        x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
-        tp.all_reduce_(x2)
-        y2, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
+        if self._fuse_fwd:
+            x2, (y2, mu2, rs2) = LF.linear_resid_ln(o, f.w(p + "out.w"), f.p(p + "out.b"), x, f.p(p + "ln2.g"),
+                                                    f.p(p + "ln2.b"), self.eps, self.ln_sync, self._ln_site(l, 0, False))
+        else:
+            x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
+            tp.all_reduce_(x2)
+            y2, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
         u, gact = G.linear_gelu(y2, f.w(p + "fc1.w"), f.p(p + "fc1.b"))  # u = gelu'(pre-activation)
-        x3 = G.linear_resid(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b") if lead else None, x2 if lead else None)
-        tp.all_reduce_(x3)
+        # the LayerNorm that reads x3: the next layer's ln1, or the final one after the last layer
+        nxt = f"h.{l + 1}.ln1" if (l + 1) in self.layout.layers else ("lnf" if self.layout.has_head else None)
+        if self._fuse_fwd and nxt is not None:
+            x3, pre_next = LF.linear_resid_ln(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b"), x2, f.p(nxt + ".g"),
+                                              f.p(nxt + ".b"), self.eps, self.ln_sync, self._ln_site(l, 1, False))
+            ctx[("ln1", l + 1) if nxt != "lnf" else "lnf_pre"] = pre_next
+        else:
+            x3 = G.linear_resid(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b") if lead else None, x2 if lead else None)
+            tp.all_reduce_(x3)
         ctx[l] = (x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch)
         return x3
 
@@ -235,9 +272,18 @@ class GPTStage:
                 G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
             # paired launches measured per Dense (in-step, us): fc2 44.1 vs 46.8 and qkv 35.6 vs 38.1
             # separate; fc1 48.7 vs 48.1 and out_proj 22.4 vs 21.7 -> those two stay separate
-            dy2 = self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False)
-            tp.all_reduce_(dy2)
-            dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
+            wt1 = f.wt(p + "fc1.w")
+            if self._fuse_bwd and wt1 is not None:
+                # fc1 dgrad with the LN2 backward in its epilogue (+ out_proj.b's gradient), then fc1's
+                # weight gradient
+                dx2, dx2_c = LF.dgrad_ln_bwd(du, wt1, x2, f.p(p + "ln2.g"), mu2, rs2, dx3, f.g(p + "ln2.g"),
+                                             f.g(p + "ln2.b"), beta, dbias=f.g(p + "out.b"), red=red,
+                                             sync=self.ln_sync, site=self._ln_site(l, 0, True))
+                G.wgrad(du, y2, f.g(p + "fc1.w"), beta, red=red, db=f.g(p + "fc1.b"))
+            else:
+                dy2 = self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False)
+                tp.all_reduce_(dy2)
+                dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
             wto = f.wt(p + "out.w")
             if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
                 do = G.linear(dx2_c, wto)
@@ -247,6 +293,14 @@ class GPTStage:
                                        out_dtype=self.act_dtype, pair=False)
             dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                               self.heads_local).view(batch * T, -1)
+            wtq = f.wt(p + "qkv.w")
+            if self._fuse_bwd and wtq is not None:
+                bg = self._prev_fc2b(l)
+                out = LF.dgrad_ln_bwd(dqkv, wtq, x, f.p(p + "ln1.g"), mu1, rs1, dx2, f.g(p + "ln1.g"), f.g(p + "ln1.b"),
+                                      beta, dbias=None if bg is None else f.g(bg), red=red, sync=self.ln_sync,
+                                      site=self._ln_site(l, 1, True))
+                G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta, red=red, db=f.g(p + "qkv.b"))
+                return out
             dy1 = self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True)
             tp.all_reduce_(dy1)
             return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
@@ -318,7 +372,9 @@ class GPTStage:
         Returns a device scalar ``loss_scale · Σ_tokens CE`` (1-element fp32 tensor)."""
         self._await_params("head")
         f = self.flat
-        yf, muf, rsf = LN.layernorm_fwd(x, f.p("lnf.g"), f.p("lnf.b"), self.eps, self.act_dtype)
+        pre = ctx.pop("lnf_pre", None)  # produced by the last layer's fc2 GEMM (fused LayerNorm)
+        yf, muf, rsf = pre if pre is not None else LN.layernorm_fwd(x, f.p("lnf.g"), f.p("lnf.b"), self.eps,
+                                                                     self.act_dtype)
         lab = labels.reshape(-1)
         tp1 = self.tp.size == 1
         logits, rowstat, lab_logit = X.lmhead_logits_partials(yf, f.w("lm_head.w"), f.p("lm_head.b"), lab,

@@ -58,6 +58,25 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class LnArgs(ctypes.Structure):
+    """Mirror of ``struct LnArgs`` in csrc/common.h (keep in sync): a layer GEMM with its LayerNorm
+    fused into the epilogue (``ops/ln_fused.py``)."""
+
+    _fields_ = [
+        ("bwd", c_int),
+        ("M", c_int), ("N", c_int), ("K", c_int),
+        ("A", c_vp), ("lda", c_long),
+        ("B", c_vp), ("ldb", c_long),
+        ("C", c_vp),
+        ("bias", c_vp), ("resid", c_vp), ("gamma", c_vp), ("beta", c_vp),
+        ("y", c_vp), ("mean", c_vp), ("rstd", c_vp),
+        ("x", c_vp), ("part", c_vp), ("nslab", c_int),
+        ("eps", c_float),
+        ("sync", c_vp), ("step", c_vp), ("site", c_int), ("nsites", c_int),
+        ("err", c_vp),
+    ]
+
+
 EPI_STORE = 0       # C = alpha*acc (+bias) (+beta*C if fp32)
 EPI_RESID = 1       # C(f32) = aux(f32) + acc + bias
 EPI_GELU = 2        # u = acc+bias: C(bf16) = gelu_tanh'(u) ; aux_out(bf16) = gelu_tanh(u)
@@ -78,6 +97,8 @@ def _declare(lib):
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, i, vp], i),
         "dtc_gemm_wgrad_split": ([i, i, i, i], i),
         "dtc_gemm_pair": ([ctypes.POINTER(GemmArgs), ctypes.POINTER(GemmArgs), vp], i),
+        "dtc_gemm_ln": ([ctypes.POINTER(LnArgs), vp], i),
+        "dtc_gemm_ln_sync_words": ([i, i], l),
         "dtc_gemm_wgrad_fuses_colsum": ([i, i, i], i),
         "dtc_reduce_tasks": ([vp, vp], i),
         "dtc_red_max_tasks": ([], i),

@@ -192,6 +192,17 @@ class Engine:
                 self._opt_groups.append((ls[0], [(lo, hi)]))
             if self.layout.has_head:
                 self._opt_groups.append(("head", [(0, bk.head_end_offset())]))
+        # LayerNorms fused into the layer GEMMs (ops/ln_fused.py).  DTC_LN_FUSE bits: 1 forward
+        # (out_proj / fc2 emit the next LayerNorm's output), 2 backward (the fc1 / qkv NT dgrads finish
+        # the LayerNorm backward).  Needs tp = pp = 1 (no all-reduce between GEMM and LayerNorm, one call
+        # per site and step), a single stream (the row-statistics exchange wants the whole chip for the
+        # launch) and, for the backward, the transposed weight mirror.
+        lnf = int(os.environ.get("DTC_LN_FUSE", "2"))
+        if (lnf and on_gpu and self.act_dtype == torch.bfloat16 and tp == 1 and pp == 1 and not self.defer_opt
+                and self.stage.side.stream is None):
+            has_wt = len(self.layout.layers) > 0 and self.flat.wt(f"h.{self.layout.layers[0]}.fc1.w") is not None
+            self.stage.enable_ln_fusion(self.b_local * T, self.opt.step_t, fwd=bool(lnf & 1),
+                                        bwd=bool(lnf & 2) and has_wt)
         if on_gpu:
             self._reserve_workspaces()
 
@@ -379,9 +390,16 @@ class Engine:
     def loss_value(self) -> float:
         """Blocking read of the global mean loss (reference: float(np.asarray(loss)), train.py:82)."""
         v = float(self.loss.item())
+        self.check_health()
+        return v / self.mesh.dp
+
+    def check_health(self):
+        """Raise if a device-side wait of this rank timed out (P2P all-reduce flags, fused LayerNorm
+        row statistics).  Blocking: call outside pipelined loops."""
         if self.p2p is not None:
             self.p2p.check()
-        return v / self.mesh.dp
+        if self.stage.ln_sync is not None:
+            self.stage.ln_sync.check()
 
     # -- host pipelining: read step t's loss while step t+1 is already queued --------------
     def loss_handle(self):

@@ -111,9 +111,11 @@ def test_profile_device_step_times(cuda, tmp_path):
     assert any(e["name"].startswith("device step") for e in tr["traceEvents"])
 
 
-def test_deferred_optimizer_matches_immediate(cuda):
+def test_deferred_optimizer_matches_immediate(cuda, monkeypatch):
     """defer_optimizer (AdamW under the next step's forward) is an exact reordering: same losses and
-    bit-identical parameters / Adam state after a flush, incl. a flush mid-run (then more steps)."""
+    bit-identical parameters / Adam state after a flush, incl. a flush mid-run (then more steps).
+    (The deferred optimizer's side stream turns the fused LayerNorms off: both runs use the unfused ones.)"""
+    monkeypatch.setenv("DTC_LN_FUSE", "0")
     runs = []
     for defer in (False, True):
         eng, mc = _engine(cuda, use_graph=True, preset="ref", vocab=50258, batch=8, defer_optimizer=defer)
@@ -199,3 +201,26 @@ def test_dgrad_nt_matches_nn(cuda, monkeypatch):
         go = grads["0"][n]
         err = ((g - go).norm() / (go.norm() + 1e-12)).item()
         assert err < 1e-2, f"{n}: NT vs NN dgrad relative grad difference {err:.3e}"
+
+
+def test_ln_fusion_matches_unfused(cuda, monkeypatch):
+    """LayerNorms fused into the layer GEMMs (DTC_LN_FUSE=3, the default) give the same loss and
+    gradients as the separate LayerNorm kernels (DTC_LN_FUSE=0) on the reference model, to bf16
+    rounding of the fused outputs; and the fused run really took the fused path."""
+    res = {}
+    for v in ("0", "3"):
+        monkeypatch.setenv("DTC_LN_FUSE", v)
+        eng, mc = _engine(cuda, use_graph=False, preset="ref", vocab=50258, batch=2, dropout=0.1)
+        assert (eng.stage.ln_sync is not None) == (v == "3")
+        b = next(get_batch_iterator(2, mc.max_seq_len + 1))
+        eng.set_batch(b)
+        eng.run_step()  # forward + backward + AdamW
+        loss = eng.loss_value()
+        torch.cuda.synchronize()
+        res[v] = (loss, eng.flat.grads.clone(), {n: eng.flat.g(n).clone() for n in eng.flat.slots})
+        del eng
+    assert abs(res["0"][0] - res["3"][0]) < 2e-3, (res["0"][0], res["3"][0])
+    for n, g0 in res["0"][2].items():
+        g3 = res["3"][2][n]
+        err = ((g3 - g0).norm() / (g0.norm() + 1e-12)).item()
+        assert err < 2e-2, f"{n}: fused vs unfused relative grad difference {err:.3e}"

@@ -429,3 +429,60 @@ def test_linear_backward_pair(cuda, M, Nout, Kin, mode):
         assert torch.equal(db_a, db_b), "bias grad"
     ref = dy.float().t() @ x.float()  # last iteration: beta = 1 onto the seed-45 tensor
     _close(dw_b, _r(Nout, Kin, dtype=torch.float32, seed=45) + ref, 2e-3, "wgrad vs fp32")
+
+
+@pytest.mark.parametrize("M,D,K", [(4096, 512, 512), (4096, 512, 2048), (1024, 768, 256), (2048, 1024, 128)])
+def test_gemm_resid_ln_fused(cuda, M, D, K):
+    """Residual-stream GEMM + LayerNorm in one launch (ops/ln_fused.py) vs the fp32 reference; two calls
+    on one granule buffer with an advancing step (stale tags of the first call must not satisfy the second)."""
+    from distributed_training_compare_jax_amd.ops import ln_fused as LF
+
+    a, w = _r(M, K, seed=31), _r(D, K, scale=0.05, seed=32)
+    b = _r(D, dtype=torch.float32, seed=33)
+    res = _r(M, D, dtype=torch.float32, seed=34) * 2 + 0.5
+    g, be = _r(D, dtype=torch.float32, seed=35), _r(D, dtype=torch.float32, seed=36)
+    step = torch.zeros(1, dtype=torch.int64, device=cuda)
+    sync = LF.LnSync(cuda, M, D, nsites=2, step=step)
+    for it in range(2):
+        x, (y, mu, rs) = LF.linear_resid_ln(a, w, b, res, g, be, 1e-6, sync, site=it)
+        xr = res + a.float() @ w.float().t() + b
+        _close(x, xr, 2e-5, "x")
+        mr = xr.mean(-1)
+        rr = torch.rsqrt((xr - mr[:, None]).pow(2).mean(-1) + 1e-6)
+        _close(mu, mr, 1e-5, "mean")
+        _close(rs, rr, 1e-4, "rstd")
+        _close(y, (xr - mr[:, None]) * rr[:, None] * g + be, 1e-2, "y")
+        a = _r(M, K, seed=40 + it)  # new data for the second call
+        step += 1
+    torch.cuda.synchronize()
+    sync.check()
+
+
+@pytest.mark.parametrize("M,D,K,nslab", [(4096, 512, 2048, 3), (4096, 512, 1536, 2), (1024, 768, 256, 3)])
+def test_dgrad_ln_bwd_fused(cuda, M, D, K, nslab):
+    """NT dgrad + LayerNorm backward in one launch vs the unfused dgrad + ln_bwd kernels."""
+    from distributed_training_compare_jax_amd.ops import ln_fused as LF
+
+    dY, wt = _r(M, K, seed=51), _r(D, K, scale=0.05, seed=52)
+    x = _r(M, D, dtype=torch.float32, seed=53) * 3 + 1
+    g = _r(D, dtype=torch.float32, seed=54)
+    _, mu, rs = LN.layernorm_fwd(x, g, g, 1e-6, torch.bfloat16)
+    dres = _r(M, D, dtype=torch.float32, seed=55)
+    step = torch.full((1,), 7, dtype=torch.int64, device=cuda)
+    sync = LF.LnSync(cuda, M, D, nsites=3, step=step)
+    outs = [torch.zeros(D, device=cuda) for _ in range(3)]
+    dbias = outs[2] if nslab == 3 else None
+    dx, dxc = LF.dgrad_ln_bwd(dY, wt, x, g, mu, rs, dres, outs[0], outs[1], 0.0, dbias=dbias, sync=sync, site=2)
+    refs = [torch.zeros(D, device=cuda) for _ in range(3)]
+    dy = G.linear_resid(dY, wt, None, None)
+    dxr = LN.layernorm_bwd(dy, x, g, mu, rs, dres, refs[0], refs[1], 0.0, dbias=refs[2] if nslab == 3 else None)
+    _close(dx, dxr, 1e-4, "dx")
+    _close(dxc, dxr, 1e-2, "dx_bf16")
+    for s, name in enumerate(("dgamma", "dbeta", "dbias")[:nslab]):
+        _close(outs[s], refs[s], 1e-4, name)
+    # accumulate mode (beta = 1) adds onto the existing gradients
+    dx2, _ = LF.dgrad_ln_bwd(dY, wt, x, g, mu, rs, None, outs[0], outs[1], 1.0, dbias=dbias, sync=sync, site=0)
+    _close(outs[0], 2 * refs[0], 1e-4, "dgamma_acc")
+    _close(dx2, dxr - dres, 1e-4, "dx_no_dres")
+    torch.cuda.synchronize()
+    sync.check()
