@@ -317,6 +317,9 @@ class Engine:
             lag = st.side.stream is not None
             if not lag and not self.zero:  # (ZeRO-1 reduce-scatters all grads in ShardedAdamW.step)
                 bk.ready_upto(bk.head_end_offset())
+            # the loss is final since head_forward: its DP mean goes out now, under the backward,
+            # instead of as an exposed collective at the end of the step
+            self._loss_allreduce(name="loss_dp")
 
             def hook(l):
                 if self.embed_gather and l == first:
@@ -341,20 +344,26 @@ class Engine:
         if not self.zero:
             bk.ready_all()
             bk.wait_all()
-        self._loss_allreduce()
+        if dp > 1:
+            self.program.wait("loss_dp")
         self._finish_optimizer()
         return self.loss
 
-    def _loss_allreduce(self):
+    def _loss_allreduce(self, name: Optional[str] = None):
+        """Sum the loss over the DP (and PP) groups.  With ``name`` (DP only) the all-reduce is
+        asynchronous: :meth:`StepProgram.wait` joins it later."""
         m = self.mesh
         groups = []
         if m.dp > 1:
             groups.append(m.dp_group)
-        if m.pp > 1:
+        if m.pp > 1 and name is None:
             groups.append(m.pp_group)
         for g in groups:
             t = self.loss
-            self.program.comm(lambda g=g, t=t: dist.all_reduce(t, group=g))
+            if name is not None:
+                self.program.comm(lambda g=g, t=t: dist.all_reduce(t, group=g, async_op=True), name=name)
+            else:
+                self.program.comm(lambda g=g, t=t: dist.all_reduce(t, group=g))
 
     def _step_fn_pp(self):
         from ..parallel.pp import run_pipeline
