@@ -449,7 +449,10 @@ __global__ void __launch_bounds__(256) transpose_batch_kernel(TrBatch batch) {
   const int b = blockIdx.x - T.blk0;
   const int tcols = (T.cols + 63) / 64;
   const int r0 = (b / tcols) * 64, c0 = (b % tcols) * 64;
-  __shared__ bf16 tile[64][64 + 8];  // +8: a column read walks rows 16 B apart in bank space
+  // row length 65: a column read (8 lanes per row group, rows 8 apart) lands rows 4 banks apart -> the 64
+  // lanes cover 32 distinct banks (+8 padding: ~6 bank conflicts per LDS instruction under PMC).  Time-neutral
+  // (18.6 vs 18.5-20.0 us per call): the kernel is bound by its 86 MB read + 86 MB write, not by LDS
+  __shared__ bf16 tile[64][64 + 1];
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {  // 64 rows x 8 chunks of 8
