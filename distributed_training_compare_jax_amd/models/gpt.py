@@ -251,8 +251,10 @@ class GPTStage:
         ctx[l] = (x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch)
         return x3
 
-    def block_backward(self, l: int, ctx: Dict, dx3: torch.Tensor, dx3_c: torch.Tensor, beta: float):
-        """dx3 fp32 (and its compute-dtype copy) → (dx, dx_c) wrt the block input."""
+    def block_backward(self, l: int, ctx: Dict, dx3: torch.Tensor, dx3_c: torch.Tensor, beta: float, dx_hook=None):
+        """dx3 fp32 (and its compute-dtype copy) → (dx, dx_c) wrt the block input.  ``dx_hook(dx)``
+        (optional) is called as soon as dx is final, before the layer's remaining weight-gradient
+        work (the DP embedding gather starts there, under that work)."""
         f, p = self.flat, f"h.{l}."
         tp = self.tp
         x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch = ctx.pop(l)
@@ -299,11 +301,16 @@ class GPTStage:
                 out = LF.dgrad_ln_bwd(dqkv, wtq, x, f.p(p + "ln1.g"), mu1, rs1, dx2, f.g(p + "ln1.g"), f.g(p + "ln1.b"),
                                       beta, dbias=None if bg is None else f.g(bg), red=red, sync=self.ln_sync,
                                       site=self._ln_site(l, 1, True))
+                if dx_hook is not None:
+                    dx_hook(out[0])
                 G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta, red=red, db=f.g(p + "qkv.b"))
                 return out
             dy1 = self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True)
             tp.all_reduce_(dy1)
-            return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
+            out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
+            if dx_hook is not None:
+                dx_hook(out[0])
+            return out
         # MLP (dgrad chain on the main stream, weight grads on the side stream)
         if fc2b_fused:
             side.defer(lambda: G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta, red=red), dx3_c, gact)
@@ -329,7 +336,10 @@ class GPTStage:
         dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
         side.flush_one()
         tp.all_reduce_(dy1)
-        return self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
+        out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
+        if dx_hook is not None:
+            dx_hook(out[0])
+        return out
 
     def _dgrad_wgrad(self, dy, dense: str, x, beta, red, pair: bool):
         """dX = dY·W (fp32) and dW/db of a Dense with a bias.  With the transposed weight mirror
@@ -424,10 +434,12 @@ class GPTStage:
         if self.red is not None:
             self.red.flush()
 
-    def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None):
-        """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist."""
+    def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None, dx_hook=None):
+        """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist,
+        ``dx_hook(dx)`` as soon as the stage's input gradient is final (inside the first layer)."""
+        first = self.layout.layers[0] if len(self.layout.layers) else None
         for l in reversed(list(self.layout.layers)):
-            dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta)
+            dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta, dx_hook=dx_hook if l == first else None)
             self.side.flush()
             self.flush_reductions()  # layer l's grads are final after this launch
             if hook is not None:

@@ -331,10 +331,14 @@ class Engine:
                 bk.ready_upto(bk.layer_end_offset(nxt) if nxt in layers else bk.head_end_offset())
         if self.zero:
             hook = None  # grads are reduce-scattered in one call by ShardedAdamW.step
-        dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=hook)
+        dx_hook = None
         if self.embed_gather:
-            out, g = self.dh_all, self.mesh.dp_group
-            self.program.comm(lambda: dist.all_gather_into_tensor(out, dx, group=g))
+            # the embedding-output gradients go out the moment the first layer's dgrad produces them,
+            # under that layer's remaining weight-gradient work
+            def dx_hook(d, out=self.dh_all, g=self.mesh.dp_group):
+                self.program.comm(lambda: dist.all_gather_into_tensor(out, d, group=g))
+        dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=hook, dx_hook=dx_hook)
+        if self.embed_gather:
             bk.ready_all()
             st.embed_backward(ctx, self.dh_all, step, 0.0, gathered=gathered)
             opt.chunk_ready(len(opt.chunks) - 1, side)  # local wte/wpe grads: overlaps the tail bucket
