@@ -186,3 +186,39 @@ def test_transposed_mirror_tracks_updates():
     pairs = [(torch.randn(24, 40).bfloat16(), torch.empty(40, 24, dtype=torch.bfloat16))]
     O.transpose_batch(pairs)
     assert torch.equal(pairs[0][1], pairs[0][0].t())
+
+
+def test_ln_fused_cpu_fallback_and_site_order():
+    """ops/ln_fused.py without a granule buffer (CPU / fp32 parity) is exactly the unfused pair of ops, and
+    the fused LayerNorm sites of a stage are numbered in execution order (forward, then backward in
+    reverse layer order), each once — the epoch-tag scheme relies on consecutive uses differing."""
+    from distributed_training_compare_jax_amd.ops import layernorm as LN
+    from distributed_training_compare_jax_amd.ops import ln_fused as LF
+
+    g = torch.Generator().manual_seed(0)
+    M, K, D = 64, 48, 32
+    a, w = torch.randn(M, K, generator=g), torch.randn(D, K, generator=g) * 0.1
+    b, res = torch.randn(D, generator=g), torch.randn(M, D, generator=g)
+    gam, bet = torch.randn(D, generator=g), torch.randn(D, generator=g)
+    x, (y, mu, rs) = LF.linear_resid_ln(a, w, b, res, gam, bet, 1e-6)
+    xr = G.linear_resid(a, w, b, res)
+    yr, mur, rsr = LN.layernorm_fwd(xr, gam, bet, 1e-6)
+    assert torch.equal(x, xr) and torch.equal(y, yr) and torch.equal(mu, mur) and torch.equal(rs, rsr)
+    dY, wt = torch.randn(M, K, generator=g), torch.randn(D, K, generator=g) * 0.1
+    dres = torch.randn(M, D, generator=g)
+    dg, db, dbias = torch.zeros(D), torch.zeros(D), torch.zeros(D)
+    dx, dxc = LF.dgrad_ln_bwd(dY, wt, x, gam, mu, rs, dres, dg, db, 0.0, dbias=dbias)
+    dgr, dbr, dbiasr = torch.zeros(D), torch.zeros(D), torch.zeros(D)
+    dxr = LN.layernorm_bwd(G.linear_resid(dY, wt, None, None), x, gam, mu, rs, dres, dgr, dbr, 0.0, dbias=dbiasr)
+    assert torch.allclose(dx, dxr) and torch.allclose(dg, dgr) and torch.allclose(db, dbr)
+    assert torch.allclose(dbias, dbiasr) and dxc is dx
+    assert LF.supported(4096, 512, 2048) and not LF.supported(4096, 64, 512) and not LF.supported(1000, 512, 512)
+
+    mc = build_configs("configs/train_config_dp.yaml")[1]
+    for layers in (range(0, 12), range(4, 8)):
+        st = GPTStage.__new__(GPTStage)
+        st.layout = StageLayout(layers, True, True)
+        order = [st._ln_site(l, k, False) for l in layers for k in (0, 1)]
+        order += [st._ln_site(l, k, True) for l in reversed(layers) for k in (0, 1)]
+        assert order == list(range(4 * len(layers))), order
+    assert mc.d_model == 512
