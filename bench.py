@@ -1,6 +1,6 @@
 """Headline benchmark: training throughput of the reference GPT on N MI355X GPUs.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--parallel dp|tp|pp] [--model ref|gpt2-small|gpt2-medium]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--parallel dp|tp|pp] [--tp T] [--model ref|gpt2-small|gpt2-medium]
 
 Metric (BASELINE.json): avg step time (ms) + tokens/sec of the reference model
 (``configs/model_config.yaml``: d_model 512, 12 layers, 16 heads, d_ff 2048, seq 512,
@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--parallel", default="dp", choices=["dp", "tp", "pp"])
+    ap.add_argument("--tp", type=int, default=1,
+                    help="with --parallel dp: hybrid DP x TP mesh (BASELINE.json config 5 is dp4 x tp2)")
     ap.add_argument("--model", default="ref")
     ap.add_argument("--batch_per_gpu", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
@@ -86,15 +88,18 @@ def main():
     world = dinfo.world
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     mc = model_config_from_preset(args.model)
-    if args.parallel == "dp":
-        global_batch, micro, scaling = args.batch_per_gpu * world, 1, "weak"
+    hybrid = args.parallel == "dp" and args.tp > 1
+    if hybrid and world % args.tp:
+        raise SystemExit(f"--tp {args.tp} does not divide {world} GPUs")
+    if args.parallel == "dp":  # weak scaling: batch_per_gpu sequences per DP group
+        global_batch, micro, scaling = args.batch_per_gpu * (world // args.tp), 1, "weak"
     elif args.parallel == "tp":
         global_batch, micro, scaling = args.batch_per_gpu, 1, "strong"
     else:
         global_batch, micro, scaling = args.batch_per_gpu, max(2, min(args.batch_per_gpu, 2 * world)), "strong"
     tc = TrainConfig(seed=0, parallel=args.parallel, batch=global_batch, steps=args.steps, log_every=10 ** 9,
                      output_dir="/tmp/bench", pp_microbatches=micro, use_graph=not args.no_graph,
-                     pp_schedule=args.pp_schedule, **_overrides(args.set))
+                     pp_schedule=args.pp_schedule, **({"tp": args.tp} if hybrid else {}), **_overrides(args.set))
     oc = OptimConfig(lr=3e-4, weight_decay=0.1, grad_clip=1.0)
     eng = Engine(mc, tc, oc, dinfo)
     data = get_batch_iterator(global_batch, mc.max_seq_len + 1, seed=0, row0=eng.feed_row0, nrows=eng.feed_rows)
@@ -143,6 +148,8 @@ def main():
     if dinfo.rank == 0:
         base = BASELINE_TOKENS_PER_S.get(args.parallel) if args.model == "ref" else None
         par = {"dp": f"dp{world}", "tp": f"tp{world}", "pp": f"pp{world}"}[args.parallel]
+        if hybrid:
+            par = f"dp{world // args.tp}xtp{args.tp}"
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": scaling,
