@@ -14,11 +14,13 @@ Here:
   partials; ``dy`` itself is never stored.
 
 A row of ``d_model`` columns spans ``d_model / 64`` blocks, so the row statistics are exchanged
-inside the launch through epoch-tagged granules (``csrc/gemm.hip`` ``ln_fwd_epilogue``): ``sync`` is
-a zero-initialised int64 buffer shared by all sites of a stage, ``step`` the device step counter,
-``site`` the call's index in execution order (``nsites`` per step).  A timed-out wait sets ``err``
-and makes the affected rows NaN (never a hang).  Numerics match the unfused kernels to fp32
-rounding (per-chunk mean/M2 combined with Chan's formula instead of one two-pass row).
+inside the launch (``csrc/gemm.hip`` "LayerNorm fused into the layer GEMM epilogue"): write-through
+partials plus one epoch flag per block in ``sync`` (a zero-initialised int64 buffer shared by all
+sites of a stage); epoch = ``step`` (the device step counter) * ``nsites`` + ``site`` (the call's index
+in execution order) + 1.  A timed-out wait sets ``err`` and makes the affected rows NaN (never a
+hang).  Numerics match the unfused kernels to fp32 rounding (forward: per-chunk mean/M2 combined
+with Chan's formula instead of one two-pass row).  Only the backward fusion is on by default
+(``DTC_LN_FUSE``, ``profiles/r2_ab_ln_fuse.log``).
 """
 
 from __future__ import annotations
@@ -47,7 +49,12 @@ class LnSync:
 
 
 def supported(M: int, D: int, K: int) -> bool:
-    return M % 128 == 0 and D % 256 == 0 and D <= 1024 and K % 64 == 0
+    """Shapes the fused kernels take AND where they pay: at most 512 tiles of 128 x 64, i.e. where the
+    unfused NT dgrad runs the same 8-wave 128 x 64 plan (csrc/gemm.hip dmaw_plan).  Beyond that (GPT-2
+    small / medium at T = 1024: 768 / 1024 tiles) the fused launch measured slower than the unfused
+    dgrad + LayerNorm kernels (15.53 vs 14.87 and 37.96 vs 36.81 ms/step)."""
+    return (M % 128 == 0 and D % 256 == 0 and D <= 1024 and K % 64 == 0
+            and (M // 128) * (D // 64) <= 512)
 
 
 def _args(bwd: int, a: torch.Tensor, w: torch.Tensor, c: torch.Tensor, sync: LnSync, site: int, **kw) -> "N.LnArgs":

@@ -213,6 +213,7 @@ def test_ln_fused_cpu_fallback_and_site_order():
     assert torch.allclose(dx, dxr) and torch.allclose(dg, dgr) and torch.allclose(db, dbr)
     assert torch.allclose(dbias, dbiasr) and dxc is dx
     assert LF.supported(4096, 512, 2048) and not LF.supported(4096, 64, 512) and not LF.supported(1000, 512, 512)
+    assert not LF.supported(8192, 768, 3072) and not LF.supported(8192, 1024, 4096)  # GPT-2 small / medium: slower
 
     mc = build_configs("configs/train_config_dp.yaml")[1]
     for layers in (range(0, 12), range(4, 8)):
