@@ -298,6 +298,10 @@ class Engine:
             gathered = (self.ids_all, 0, (hk, None) if hk is not None else st.embed_keys(self.ids_all))
         h = st.stage_forward(h, b, ctx)
         st.head_forward(h, self.labels, 1.0 / (b * T), ctx, loss_out=self.loss)
+        if dp > 1:
+            # the loss is final here: its DP mean goes out now, under the whole backward, instead of
+            # as an exposed collective at the end of the step (joined before the optimizer)
+            self._loss_allreduce(name="loss_dp")
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
         bk, opt = self.buckets, self.opt
         side = st.red if st.red is not None else st.side.defer  # where grad-norm chunks are queued
@@ -317,9 +321,6 @@ class Engine:
             lag = st.side.stream is not None
             if not lag and not self.zero:  # (ZeRO-1 reduce-scatters all grads in ShardedAdamW.step)
                 bk.ready_upto(bk.head_end_offset())
-            # the loss is final since head_forward: its DP mean goes out now, under the backward,
-            # instead of as an exposed collective at the end of the step
-            self._loss_allreduce(name="loss_dp")
 
             def hook(l):
                 if self.embed_gather and l == first:
