@@ -97,6 +97,18 @@ struct LnArgs {
 
 #define DTC_CHECK_LAUNCH() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
 
+// Bounds / invariant checks of the debug build (csrc/build.py --debug: -O1 -g -DDTC_DEBUG).  In a
+// device function a failed check prints the condition and aborts the kernel (HIP device assert);
+// in the release build it compiles to nothing.  DTC_HOST_CHECK validates launch arguments on the
+// host (returns hipErrorInvalidValue from the entry point) in both builds where it is used.
+#ifdef DTC_DEBUG
+#include <cassert>
+#define DTC_ASSERT(cond) assert(cond)
+#else
+#define DTC_ASSERT(cond) ((void)0)
+#endif
+#define DTC_HOST_CHECK(cond) do { if (!(cond)) return (int)hipErrorInvalidValue; } while (0)
+
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 

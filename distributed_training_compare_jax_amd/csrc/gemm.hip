@@ -171,6 +171,7 @@ struct Epi {
 
 template <int EPI, bool OUTF32>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4 v) {
+  DTC_ASSERT(m >= 0 && m < e.M && n >= 0 && n < e.N);
   const bool full = (n + 4 <= e.N);
   float b[4] = {0.f, 0.f, 0.f, 0.f};
   if (e.bias) {
@@ -1380,6 +1381,7 @@ __global__ void splitk_reduce(const float* __restrict__ slab, int split, long MN
                               int N, float beta) {
   long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i4 >= MN) return;
+  DTC_ASSERT(N % 4 == 0 && i4 + 4 <= MN);
   long m = i4 / N;
   int n = (int)(i4 % N);
   f32x4 s = *(const f32x4*)(slab + i4);

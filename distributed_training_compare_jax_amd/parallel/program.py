@@ -21,6 +21,7 @@ produced in one segment and consumed in a later one stay valid.
 
 from __future__ import annotations
 
+import time
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -40,6 +41,50 @@ class StepProgram:
         # called before every cut/collective: forked streams (e.g. the backward side stream)
         # must re-join the capture stream before a graph segment ends / a collective reads data
         self.before_comm: List[Callable[[], None]] = []
+        # observability (metrics.json comm_ms / comm_calls_per_step): with time_comms on, every
+        # collective (and every wait on an async one) issued in eager mode or replay is bracketed
+        # by timing events on the issuing stream, i.e. the EXPOSED time the step's stream spends
+        # in it; a host clock on CPU (gloo is synchronous there)
+        self.time_comms = False
+        self.step_comms = 0
+        self._ev: List[List[Any]] = []  # per step (FIFO): [(start, end) event pairs | host ms floats]
+
+    def begin_step(self):
+        self.step_comms = 0
+        if self.time_comms:
+            self._ev.append([])
+
+    def _timed(self, fn):
+        self.step_comms += 1
+        if not self.time_comms or self.recording or not self._ev:
+            return fn()
+        if self.device.type == "cuda":
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = fn()
+            e.record()
+            self._ev[-1].append((s, e))
+            return r
+        t = time.perf_counter()
+        r = fn()
+        self._ev[-1].append(1e3 * (time.perf_counter() - t))
+        return r
+
+    def take_comm_ms(self) -> float:
+        """Exposed collective time (ms) of the OLDEST timed step not yet taken (synchronises on that
+        step's events only, so a step already queued behind it keeps running)."""
+        if not self._ev:
+            return 0.0
+        ms = 0.0
+        for x in self._ev.pop(0):
+            if isinstance(x, float):
+                ms += x
+            else:
+                s, e = x
+                e.synchronize()
+                ms += s.elapsed_time(e)
+        return ms
 
     # -------------------------------------------------------------- step-code API
     def comm(self, fn: Callable[[], Any], name: Optional[str] = None):
@@ -54,7 +99,7 @@ class StepProgram:
                 self._handles[name] = res
             self._begin()
             return res
-        res = fn()
+        res = self._timed(fn)
         if name is not None:
             self._handles[name] = res
         return res
@@ -68,7 +113,7 @@ class StepProgram:
             self._wait(name)
             self._begin()
         else:
-            self._wait(name)
+            self._timed(lambda: self._wait(name))
 
     def _wait(self, name):
         h = self._handles.pop(name, None)
@@ -138,11 +183,11 @@ class StepProgram:
             if kind == "graph":
                 obj.replay()
             elif kind == "comm":
-                res = obj()
+                res = self._timed(obj)
                 if name is not None:
                     self._handles[name] = res
             else:
-                self._wait(name)
+                self._timed(lambda: self._wait(name))
 
     @property
     def n_graphs(self) -> int:

@@ -198,8 +198,10 @@ class Engine:
         # per site and step), a single stream (the row-statistics exchange wants the whole chip for the
         # launch) and, for the backward, the transposed weight mirror.
         lnf = int(os.environ.get("DTC_LN_FUSE", "2"))
-        if (lnf and on_gpu and self.act_dtype == torch.bfloat16 and tp == 1 and pp == 1 and not self.defer_opt
-                and self.stage.side.stream is None):
+        # dp == 1 too: under DP the bucket all-reduces (RCCL kernels on other CUs) run during the
+        # backward, and the in-launch row-statistics exchange needs all of its blocks co-resident.
+        if (lnf and on_gpu and self.act_dtype == torch.bfloat16 and tp == 1 and pp == 1 and dp == 1
+                and not self.defer_opt and self.stage.side.stream is None):
             has_wt = len(self.layout.layers) > 0 and self.flat.wt(f"h.{self.layout.layers[0]}.fc1.w") is not None
             self.stage.enable_ln_fusion(self.b_local * T, self.opt.step_t, fwd=bool(lnf & 1),
                                         bwd=bool(lnf & 2) and has_wt)
@@ -388,6 +390,7 @@ class Engine:
     def run_step(self) -> torch.Tensor:
         """Enqueue one full training step on the static inputs; returns the (device) loss."""
         p = self.program
+        p.begin_step()
         if not p.use_graph:
             self._step_fn()
         elif not p.recorded:
@@ -416,31 +419,52 @@ class Engine:
             self.stage.ln_sync.check()
 
     # -- host pipelining: read step t's loss while step t+1 is already queued --------------
+    def _err_words(self):
+        """Device error words of this rank's in-launch waits (P2P all-reduce flags, fused LayerNorm
+        row statistics): nonzero = a wait timed out and that step computed NaN."""
+        out = []
+        if self.p2p is not None:
+            out.append(("p2p", self.p2p.err))
+        if self.stage.ln_sync is not None:
+            out.append(("ln", self.stage.ln_sync.err))
+        return out
+
     def loss_handle(self):
-        """Queue a copy of this step's loss to pinned host memory (2-slot ring) + an event.
+        """Queue a copy of this step's loss (and of the error words) to pinned host memory (2-slot
+        ring) + an event.
 
         With the step replayed from a graph, the host can enqueue step t+1 (its H2D batch copy
         and graph launch) before blocking on step t's loss, so the GPU never idles on the host
-        between steps; every step's loss is still read (one step later)."""
+        between steps; every step's loss is still read (one step later), and a timed-out device
+        wait raises at that read instead of letting NaN losses through silently."""
         if self.device.type != "cuda":
             return self.loss_value()
+        words = self._err_words()
         if not hasattr(self, "_loss_host"):
             self._loss_host = [torch.zeros(1, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+            self._err_host = [torch.zeros(max(1, len(words)), dtype=torch.int32, pin_memory=True) for _ in range(2)]
             self._loss_slot = 0
-        slot = self._loss_host[self._loss_slot]
+        i = self._loss_slot
+        slot, eslot = self._loss_host[i], self._err_host[i]
         self._loss_slot ^= 1
         slot.copy_(self.loss, non_blocking=True)
+        for j, (_, w) in enumerate(words):
+            eslot[j:j + 1].copy_(w, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return slot, ev
+        return slot, ev, eslot
 
     def read_loss(self, handle) -> float:
         if not isinstance(handle, tuple):
             return handle
-        slot, ev = handle
+        slot, ev, eslot = handle
         ev.synchronize()
-        if self.p2p is not None:
-            self.p2p.check()
+        for j, (name, _) in enumerate(self._err_words()):
+            e = int(eslot[j])
+            if e:
+                if name == "p2p":
+                    raise RuntimeError(f"P2P all-reduce: rank {self.p2p.rank} timed out waiting for rank {e - 1000}")
+                raise RuntimeError("fused LayerNorm: a row-statistics wait timed out (outputs were NaN)")
         return float(slot.item()) / self.mesh.dp
 
     def grad_norm(self) -> float:

@@ -70,6 +70,8 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
 
     barrier()
     say("Start measuring")
+    eng.program.time_comms = True  # metrics.json comm_ms (events around the collectives)
+    comm_ms, comm_calls = [], []
     running, history, elapsed = [], [], []
     batch = next(data)
     t0 = time.perf_counter()
@@ -84,6 +86,7 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
         nonlocal running
         with tr.span("loss sync"):
             loss = eng.read_loss(handle)
+        comm_ms.append(eng.program.take_comm_ms())
         dog.beat(s)
         tr.collect()
         running.append(loss)
@@ -98,6 +101,7 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
         eng.set_batch(batch)
         with tr.device_step(step):
             eng.run_step()
+        comm_calls.append(eng.program.step_comms)
         handle = eng.loss_handle()
         if step < train_config.steps:
             with tr.span("data"):
@@ -126,7 +130,14 @@ def train(train_config: TrainConfig, model_config: ModelConfig, opt_config: Opti
                   mesh=dict(dp=eng.mesh.dp, tp=eng.mesh.tp, pp=eng.mesh.pp),
                   model=model_config.name, global_batch=eng.global_batch, seq_len=eng.T,
                   dtype=str(eng.act_dtype).replace("torch.", ""), n_graphs=eng.program.n_graphs,
-                  n_comms=eng.program.n_comms)
+                  n_comms=eng.program.n_comms,
+                  # collective calls issued per step (graph replay or eager) and their exposed time
+                  comm_calls_per_step=int(np.max(comm_calls)) if comm_calls else 0,
+                  comm_ms_mean=float(np.mean(comm_ms)) if comm_ms else 0.0,
+                  # model FLOPs (fwd+bwd matmuls + attention, ModelConfig.flops_per_token) / step time
+                  tflops=model_config.flops_per_token() * eng.tokens_per_step * train_config.steps / max(total, 1e-9) / 1e12,
+                  world_size=dinfo.world)
+    result["tflops_per_gpu"] = result["tflops"] / max(1, dinfo.world)
     if tr.enabled:
         path = tr.write()
         n_warm = train_config.warmup_steps

@@ -12,7 +12,8 @@ _READ = [re.compile(r'environ(?:\.get)?\(\s*"(DTC_[A-Z0-9_]+)"'),
          re.compile(r'getenv\(\s*"(DTC_[A-Z0-9_]+)"'),
          re.compile(r'#\s*if(?:n?def)\s+(DTC_[A-Z0-9_]+)')]
 # header guards / helpers that are code, not switches
-_NOT_SWITCHES = {"DTC_CHECK_LAUNCH", "DTC_LDS", "DTC_OUT_STORE", "DTC_NV_SWITCH", "DTC_WAVE"}
+_NOT_SWITCHES = {"DTC_CHECK_LAUNCH", "DTC_LDS", "DTC_OUT_STORE", "DTC_NV_SWITCH", "DTC_WAVE", "DTC_ASSERT",
+                 "DTC_HOST_CHECK"}
 
 
 def _sources():
