@@ -1,0 +1,444 @@
+// Exact-fp32 causal flash attention for gfx950 (dtype: fp32 parity mode) — forward + backward.
+//
+// Reference: model/CausalSelfAttention.py:34-44 computes softmax(Q K^T * hd^-1/2 + mask) V in fp32
+// with the full [B, H, T, T] score tensor materialised (134 MB per layer at the reference size) and
+// an additive -1e9 causal mask (model/GPTModel.py:50-51; exp(-1e9 - max) is exactly 0 in fp32, so an
+// in-kernel predicate is the same function).  Here nothing of size T x T exists: online softmax in
+// the forward (LSE saved), P recomputed in the backward, on v_mfma_f32_32x32x2_f32 (exact f32).
+//
+// The 32x32 accumulator X of an MFMA has its COLUMN on the lane and its ROWS in the 16 registers
+// (row (r&3) + 8(r>>2) + 4(lane>>5)).  So a later product that sums over X's row index takes X as an
+// operand straight from registers, in that same permuted row order (cdna_hip_programming.md §3 "an
+// accumulator tile as the next MFMA's operand").  Each kernel picks its score orientation for that:
+//  * forward and dQ: S^T[key][q] = K Q^T (query on the lane): the per-query softmax statistics are
+//    per-lane scalars (max/sum over the 16 registers + one xor-32 shuffle, no 32-lane reductions),
+//    and O^T = V^T P^T, dQ^T = K^T dS^T sum over the key rows.
+//  * dK/dV: S[q][key] = Q K^T (key on the lane): dV = P^T dO and dK = dS^T Q sum over the q rows.
+// The operand that stays fixed for a wave (its 32 queries, or its 32 keys) lives in registers; the
+// streamed K/V (or Q/dO) tiles are register-staged into double-buffered LDS with a row pitch of
+// hd+4 floats: a ds_read_b128 of 16 rows x 16 B then covers 64 distinct banks, and the 4 floats a lane
+// reads are 4 MFMA k-steps in a permuted d order shared by both operands (sums are order-free).
+// Deterministic: no atomics (separate dK/dV and dQ kernels, each output written by one wave).
+#include "common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int AW = 4;           // waves per block
+constexpr int AT = AW * 64;     // threads
+constexpr int QB = 32 * AW;     // rows (queries or keys) owned by one block
+constexpr int ST = 64;          // streamed rows per LDS stage (2 sub-tiles of 32)
+
+__device__ __forceinline__ int rowmap(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+template <int HD>
+struct AF {
+  static constexpr int LD = HD + 4;      // padded LDS row pitch (floats)
+  static constexpr int NC = HD / 8;      // 8-wide d chunks = 4 permuted MFMA k-steps each
+  static constexpr int DT = HD / 32;     // 32-wide d tiles of an O / dQ / dK / dV accumulator
+  static constexpr int TILE = ST * LD;   // one streamed [ST][HD] tile in LDS
+  static constexpr int CH = ST * HD / 4; // float4 chunks per streamed tile
+  static constexpr int PT = CH / AT;     // per thread
+  static_assert(CH % AT == 0, "");
+
+  // global row t of a [*, row_stride] tensor, columns [col0, col0 + HD)
+  __device__ __forceinline__ static void load(f32x4 (&reg)[PT], const float* base, long row_stride, int t0, int T,
+                                              int tid) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int c = tid + i * AT, row = c / (HD / 4), col = (c % (HD / 4)) * 4;
+      const int t = t0 + row;
+      reg[i] = t < T ? *(const f32x4*)(base + (long)t * row_stride + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ __forceinline__ static void store(const f32x4 (&reg)[PT], float* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int c = tid + i * AT, row = c / (HD / 4), col = (c % (HD / 4)) * 4;
+      *(f32x4*)(lds + row * LD + col) = reg[i];
+    }
+  }
+  // the register-resident operand: row (lane&31) of a wave's 32 rows, d chunk c -> 4 floats of the
+  // lane half's permuted order (d = 8c + 4*half + j)
+  __device__ __forceinline__ static void load_fixed(f32x4 (&reg)[NC], const float* base, long row_stride, int t, int T,
+                                                    int half) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      reg[c] = t < T ? *(const f32x4*)(base + (long)t * row_stride + 8 * c + 4 * half) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // X[i][j] = sum_d L[i][d] R[j][d]: L = 32 LDS rows (sub-tile), R = the register operand
+  // (lds_is_a: L is the MFMA A operand -> X rows = LDS rows, columns = register rows)
+  template <bool LDS_IS_A>
+  __device__ __forceinline__ static f32x16 dot(const float* lds_rows, const f32x4 (&reg)[NC], int l32, int half) {
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const f32x4 v = *(const f32x4*)(lds_rows + l32 * LD + 8 * c + 4 * half);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc = LDS_IS_A ? __builtin_amdgcn_mfma_f32_32x32x2f32(v[j], reg[c][j], acc, 0, 0, 0)
+                       : __builtin_amdgcn_mfma_f32_32x32x2f32(reg[c][j], v[j], acc, 0, 0, 0);
+    }
+    return acc;
+  }
+  // acc[dt][?] += sum over X's rows (permuted: register s <-> row rowmap(s, half)) of
+  //   X_IS_A:  X^T[i][s] * L[s][dt*32 + j]   (output rows = X's columns, columns = d)
+  //   else:    L[s][dt*32 + i] * X[s][j]     (output rows = d, columns = X's columns)
+  template <bool X_IS_A>
+  __device__ __forceinline__ static void acc_rows(f32x16 (&acc)[DT], const f32x16& X, const float* lds_rows, int l32,
+                                                  int half) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float* row = lds_rows + rowmap(s, half) * LD + l32;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        acc[dt] = X_IS_A ? __builtin_amdgcn_mfma_f32_32x32x2f32(X[s], row[dt * 32], acc[dt], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_32x32x2f32(row[dt * 32], X[s], acc[dt], 0, 0, 0);
+    }
+  }
+};
+
+struct AttnFArgs {
+  const float* qkv;  // [B][T][3][H][HD]
+  const float* o;    // [B][T][H][HD]
+  const float* dout; // [B][T][H][HD]
+  const float* lse;  // [B][H][T]
+  const float* delta;// [B][H][T]
+  float* out;        // fwd: o; dq kernel: dqkv; dkdv kernel: dqkv
+  float* lse_out;    // fwd
+  int B, T, H;
+  float scale;
+};
+
+// -------------------------------------------------------------------------------- forward
+template <int HD>
+__global__ void __launch_bounds__(AT, 2) attn_f32_fwd_kernel(AttnFArgs a) {
+  using F = AF<HD>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * F::TILE];  // [buf][K | V]
+  const int nqb = (a.T + QB - 1) / QB;
+  const int bh = blockIdx.x / nqb, qb = nqb - 1 - blockIdx.x % nqb;  // longest (last) query blocks first
+  const int b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const long rs = 3L * a.H * HD;  // qkv row stride
+  const float* qg = a.qkv + (long)b * a.T * rs + (long)h * HD;
+  const float* kg = qg + (long)a.H * HD;
+  const float* vg = kg + (long)a.H * HD;
+  const int q0 = qb * QB, qw = q0 + 32 * wave, q = qw + l32;
+
+  f32x4 qreg[F::NC];
+  F::load_fixed(qreg, qg, rs, q, a.T, half);
+  f32x16 oacc[F::DT];
+#pragma unroll
+  for (int dt = 0; dt < F::DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[dt][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int nstage = min((a.T + ST - 1) / ST, (q0 + QB + ST - 1) / ST);  // key stages up to the last query
+  f32x4 rk[F::PT], rv[F::PT];
+  F::load(rk, kg, rs, 0, a.T, tid);
+  F::load(rv, vg, rs, 0, a.T, tid);
+  F::store(rk, smem, tid);
+  F::store(rv, smem + F::TILE, tid);
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    const float* sK = smem + (st & 1) * 2 * F::TILE;
+    const float* sV = sK + F::TILE;
+    const bool more = st + 1 < nstage;
+    if (more) {
+      F::load(rk, kg, rs, (st + 1) * ST, a.T, tid);
+      F::load(rv, vg, rs, (st + 1) * ST, a.T, tid);
+    }
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = st * ST + sub * 32;
+      if (kb > qw + 31) continue;  // wave-uniform: the whole sub-tile is above this wave's diagonal
+      f32x16 s = F::template dot<true>(sK + sub * 32 * F::LD, qreg, l32, half);  // S^T[key][q]
+      float mloc = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = s[r] * a.scale;
+        if (kb + rowmap(r, half) > q) v = -INFINITY;
+        s[r] = v;
+        mloc = fmaxf(mloc, v);
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run, mloc);
+      const float alpha = expf(m_run - m_new);
+      float lsum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = expf(s[r] - m_new);
+        s[r] = p;
+        lsum += p;
+      }
+      lsum += __shfl_xor(lsum, 32, 64);
+      l_run = l_run * alpha + lsum;
+      m_run = m_new;
+#pragma unroll
+      for (int dt = 0; dt < F::DT; ++dt) oacc[dt] *= alpha;
+      F::template acc_rows<false>(oacc, s, sV + sub * 32 * F::LD, l32, half);  // O^T[d][q] += V^T P^T
+    }
+    if (more) {
+      float* nK = smem + ((st + 1) & 1) * 2 * F::TILE;
+      F::store(rk, nK, tid);
+      F::store(rv, nK + F::TILE, tid);
+    }
+    __syncthreads();
+  }
+  if (q < a.T) {
+    const float inv = 1.f / l_run;
+    float* og = a.out + ((long)(b * a.T + q) * a.H + h) * HD;
+#pragma unroll
+    for (int dt = 0; dt < F::DT; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg)
+        *(f32x4*)(og + dt * 32 + 8 * rg + 4 * half) =
+            f32x4{oacc[dt][4 * rg] * inv, oacc[dt][4 * rg + 1] * inv, oacc[dt][4 * rg + 2] * inv, oacc[dt][4 * rg + 3] * inv};
+    if (half == 0) a.lse_out[(long)bh * a.T + q] = m_run + logf(l_run);
+  }
+}
+
+// -------------------------------------------------------------------------------- backward
+// delta[b][h][t] = sum_d dO[b][t][h][d] * O[b][t][h][d]   (one wave per (b, t), lanes over h*HD)
+__global__ void __launch_bounds__(256) attn_f32_delta_kernel(const float* __restrict__ o, const float* __restrict__ dout,
+                                                             float* __restrict__ delta, int B, int T, int H, int HD) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= (long)B * T) return;
+  const int b = (int)(row / T), t = (int)(row % T);
+  const float* op = o + row * H * HD;
+  const float* dp = dout + row * H * HD;
+  for (int h = 0; h < H; ++h) {
+    float s = 0.f;
+    for (int d = lane; d < HD; d += 64) s += op[h * HD + d] * dp[h * HD + d];
+    s = warp_sum(s);
+    if (lane == 0) delta[((long)b * H + h) * T + t] = s;
+  }
+}
+
+// dK, dV for a block of QB keys (wave w owns keys k0 + 32w ..), streaming Q / dO stages from the
+// diagonal down.  Orientation S[q][key]: key on the lane, 16 query rows in registers.
+template <int HD>
+__global__ void __launch_bounds__(AT, 2) attn_f32_dkdv_kernel(AttnFArgs a) {
+  using F = AF<HD>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (2 * F::TILE + 2 * ST)];  // [buf][Q | dO | lse | delta]
+  constexpr int BUF = 2 * F::TILE + 2 * ST;
+  const int nkb = (a.T + QB - 1) / QB;
+  const int bh = blockIdx.x / nkb, kbk = blockIdx.x % nkb;  // first key blocks have the most queries
+  const int b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const long rs = 3L * a.H * HD, ors = (long)a.H * HD;
+  const float* qg = a.qkv + (long)b * a.T * rs + (long)h * HD;
+  const float* kg = qg + (long)a.H * HD;
+  const float* vg = kg + (long)a.H * HD;
+  const float* dog = a.dout + (long)b * a.T * ors + (long)h * HD;
+  const float* lseg = a.lse + (long)bh * a.T;
+  const float* dlg = a.delta + (long)bh * a.T;
+  const int k0 = kbk * QB, kw = k0 + 32 * wave, key = kw + l32;
+
+  f32x4 kreg[F::NC], vreg[F::NC];
+  F::load_fixed(kreg, kg, rs, key, a.T, half);
+  F::load_fixed(vreg, vg, rs, key, a.T, half);
+  f32x16 dk[F::DT], dv[F::DT];
+#pragma unroll
+  for (int dt = 0; dt < F::DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[dt][r] = dv[dt][r] = 0.f;
+
+  const int st0 = k0 / ST, nst = (a.T + ST - 1) / ST;
+  f32x4 rq[F::PT], rd[F::PT];
+  float rl = 0.f, rdl = 0.f;  // lse / delta of stage row tid (tid < ST)
+  auto ld_stage = [&](int s) {
+    F::load(rq, qg, rs, s * ST, a.T, tid);
+    F::load(rd, dog, ors, s * ST, a.T, tid);
+    if (tid < ST) {
+      const int t = s * ST + tid;
+      rl = t < a.T ? lseg[t] : 0.f;
+      rdl = t < a.T ? dlg[t] : 0.f;
+    }
+  };
+  auto st_stage = [&](float* buf) {
+    F::store(rq, buf, tid);
+    F::store(rd, buf + F::TILE, tid);
+    if (tid < ST) {
+      buf[2 * F::TILE + tid] = rl;
+      buf[2 * F::TILE + ST + tid] = rdl;
+    }
+  };
+  ld_stage(st0);
+  st_stage(smem);
+  __syncthreads();
+  for (int s = st0; s < nst; ++s) {
+    const float* sQ = smem + ((s - st0) & 1) * BUF;
+    const float* sD = sQ + F::TILE;
+    const float* sL = sQ + 2 * F::TILE;
+    const float* sDl = sL + ST;
+    const bool more = s + 1 < nst;
+    if (more) ld_stage(s + 1);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qs = s * ST + sub * 32;
+      if (qs + 31 < kw) continue;  // wave-uniform: every query of the sub-tile precedes this wave's keys
+      const float* Qr = sQ + sub * 32 * F::LD;
+      const float* Dr = sD + sub * 32 * F::LD;
+      f32x16 p = F::template dot<true>(Qr, kreg, l32, half);   // S[q][key]
+      f32x16 dp = F::template dot<true>(Dr, vreg, l32, half);  // dP[q][key] = dO V^T
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = sub * 32 + rowmap(r, half), qa = s * ST + qi;
+        float pv = expf(p[r] * a.scale - sL[qi]);
+        if (key > qa || qa >= a.T) pv = 0.f;
+        p[r] = pv;
+        dp[r] = pv * (dp[r] - sDl[qi]);  // dS
+      }
+      F::template acc_rows<true>(dv, p, Dr, l32, half);   // dV[key][d] += P^T dO
+      F::template acc_rows<true>(dk, dp, Qr, l32, half);  // dK[key][d] += dS^T Q  (x scale at the end)
+    }
+    if (more) st_stage(smem + ((s + 1 - st0) & 1) * BUF);
+    __syncthreads();
+  }
+  // D layout: rows = keys (registers), columns = d (lanes): each store is 2 x 128 B of one row
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int t = kw + rowmap(r, half);
+    if (t >= a.T) continue;
+    float* dkp = a.out + ((long)(b * a.T + t) * 3 + 1) * a.H * HD + (long)h * HD;
+    float* dvp = dkp + (long)a.H * HD;
+#pragma unroll
+    for (int dt = 0; dt < F::DT; ++dt) {
+      dkp[dt * 32 + l32] = dk[dt][r] * a.scale;
+      dvp[dt * 32 + l32] = dv[dt][r];
+    }
+  }
+}
+
+// dQ for a block of QB queries, streaming K / V stages up to the diagonal.  Orientation S^T[key][q].
+template <int HD>
+__global__ void __launch_bounds__(AT, 2) attn_f32_dq_kernel(AttnFArgs a) {
+  using F = AF<HD>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * F::TILE];  // [buf][K | V]
+  const int nqb = (a.T + QB - 1) / QB;
+  const int bh = blockIdx.x / nqb, qb = nqb - 1 - blockIdx.x % nqb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const long rs = 3L * a.H * HD, ors = (long)a.H * HD;
+  const float* qg = a.qkv + (long)b * a.T * rs + (long)h * HD;
+  const float* kg = qg + (long)a.H * HD;
+  const float* vg = kg + (long)a.H * HD;
+  const int q0 = qb * QB, qw = q0 + 32 * wave, q = qw + l32;
+
+  f32x4 qreg[F::NC], doreg[F::NC];
+  F::load_fixed(qreg, qg, rs, q, a.T, half);
+  F::load_fixed(doreg, a.dout + (long)b * a.T * ors + (long)h * HD, ors, q, a.T, half);
+  const float lse_q = q < a.T ? a.lse[(long)bh * a.T + q] : 0.f;
+  const float dl_q = q < a.T ? a.delta[(long)bh * a.T + q] : 0.f;
+  f32x16 dq[F::DT];
+#pragma unroll
+  for (int dt = 0; dt < F::DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+
+  const int nstage = min((a.T + ST - 1) / ST, (q0 + QB + ST - 1) / ST);  // key stages up to the last query
+  f32x4 rk[F::PT], rv[F::PT];
+  F::load(rk, kg, rs, 0, a.T, tid);
+  F::load(rv, vg, rs, 0, a.T, tid);
+  F::store(rk, smem, tid);
+  F::store(rv, smem + F::TILE, tid);
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    const float* sK = smem + (st & 1) * 2 * F::TILE;
+    const float* sV = sK + F::TILE;
+    const bool more = st + 1 < nstage;
+    if (more) {
+      F::load(rk, kg, rs, (st + 1) * ST, a.T, tid);
+      F::load(rv, vg, rs, (st + 1) * ST, a.T, tid);
+    }
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = st * ST + sub * 32;
+      if (kb > qw + 31) continue;
+      const float* Kr = sK + sub * 32 * F::LD;
+      f32x16 p = F::template dot<true>(Kr, qreg, l32, half);                     // S^T[key][q]
+      f32x16 dp = F::template dot<true>(sV + sub * 32 * F::LD, doreg, l32, half);  // dP^T = V dO^T
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = expf(p[r] * a.scale - lse_q);
+        if (kb + rowmap(r, half) > q) pv = 0.f;
+        dp[r] = pv * (dp[r] - dl_q);  // dS^T
+      }
+      F::template acc_rows<false>(dq, dp, Kr, l32, half);  // dQ^T[d][q] += K^T dS^T
+    }
+    if (more) {
+      float* nK = smem + ((st + 1) & 1) * 2 * F::TILE;
+      F::store(rk, nK, tid);
+      F::store(rv, nK + F::TILE, tid);
+    }
+    __syncthreads();
+  }
+  if (q < a.T) {
+    float* dqp = a.out + ((long)(b * a.T + q) * 3) * a.H * HD + (long)h * HD;
+#pragma unroll
+    for (int dt = 0; dt < F::DT; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg)
+        *(f32x4*)(dqp + dt * 32 + 8 * rg + 4 * half) =
+            f32x4{dq[dt][4 * rg] * a.scale, dq[dt][4 * rg + 1] * a.scale, dq[dt][4 * rg + 2] * a.scale,
+                  dq[dt][4 * rg + 3] * a.scale};
+  }
+}
+
+template <int HD>
+int launch_fwd(const AttnFArgs& a, hipStream_t st) {
+  const int blocks = a.B * a.H * ((a.T + QB - 1) / QB);
+  hipLaunchKernelGGL(attn_f32_fwd_kernel<HD>, dim3(blocks), dim3(AT), 0, st, a);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int HD>
+int launch_bwd(const AttnFArgs& a, hipStream_t st) {
+  const int blocks = a.B * a.H * ((a.T + QB - 1) / QB);
+  hipLaunchKernelGGL(attn_f32_dkdv_kernel<HD>, dim3(blocks), dim3(AT), 0, st, a);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(attn_f32_dq_kernel<HD>, dim3(blocks), dim3(AT), 0, st, a);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dtc_attn_f32_fwd(const float* qkv, float* o, float* lse, int B, int T, int H, int HD, float scale, hipStream_t st) {
+  DTC_HOST_CHECK(B > 0 && T > 0 && H > 0);
+  DTC_HOST_CHECK(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)o & 15) == 0);
+  AttnFArgs a{};
+  a.qkv = qkv; a.out = o; a.lse_out = lse; a.B = B; a.T = T; a.H = H; a.scale = scale;
+  if (HD == 32) return launch_fwd<32>(a, st);
+  if (HD == 64) return launch_fwd<64>(a, st);
+  return 4101;
+}
+
+long dtc_attn_f32_bwd_workspace_bytes(int B, int T, int H, int HD) { (void)HD; return (long)B * H * T * 4; }
+
+// dqkv [B][T][3][H][HD] fp32 (every element written)
+int dtc_attn_f32_bwd(const float* qkv, const float* o, const float* lse, const float* dout, float* dqkv, int B, int T,
+                     int H, int HD, float scale, float* ws, long ws_bytes, hipStream_t st) {
+  DTC_HOST_CHECK(B > 0 && T > 0 && H > 0);
+  if (ws_bytes < dtc_attn_f32_bwd_workspace_bytes(B, T, H, HD)) return 4102;
+  hipLaunchKernelGGL(attn_f32_delta_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, st, o, dout, ws, B, T,
+                     H, HD);
+  DTC_CHECK_LAUNCH();
+  AttnFArgs a{};
+  a.qkv = qkv; a.o = o; a.dout = dout; a.lse = lse; a.delta = ws; a.out = dqkv;
+  a.B = B; a.T = T; a.H = H; a.scale = scale;
+  if (HD == 32) return launch_bwd<32>(a, st);
+  if (HD == 64) return launch_bwd<64>(a, st);
+  return 4101;
+}
+
+}  // extern "C"

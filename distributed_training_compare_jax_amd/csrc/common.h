@@ -158,11 +158,13 @@ __device__ __forceinline__ float gelu_tanh_grad_f(float u) {
 __device__ __forceinline__ float ce_row_c(float lse, float scale) {
   return __builtin_amdgcn_logf(scale) - lse * 1.4426950408889634f;  // v_log_f32 is log2
 }
-__device__ __forceinline__ void ce_grad8(const bf16x8& l8, int v0, float cr, int lab, int n_valid, float scale,
-                                         float (&g)[8]) {
+// fp32 logits version (the fp32 parity path's lm_head backward); the bf16 one below converts and
+// calls it, so both give the same bits for the same logit values.
+__device__ __forceinline__ void ce_grad8f(const float (&l)[8], int v0, float cr, int lab, int n_valid, float scale,
+                                          float (&g)[8]) {
   constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) g[e] = __builtin_amdgcn_exp2f(fmaf((float)l8[e], L2E, cr));
+  for (int e = 0; e < 8; ++e) g[e] = __builtin_amdgcn_exp2f(fmaf(l[e], L2E, cr));
   // the label's chunk / a chunk past n_valid: rare, so a WAVE-uniform branch around the fix-up
   // (a lane-level if gets predicated into compares + selects on every element)
   const bool fix = (unsigned)(lab - v0) < 8u || v0 + 8 > n_valid;
@@ -175,6 +177,13 @@ __device__ __forceinline__ void ce_grad8(const bf16x8& l8, int v0, float cr, int
       }
     }
   }
+}
+__device__ __forceinline__ void ce_grad8(const bf16x8& l8, int v0, float cr, int lab, int n_valid, float scale,
+                                         float (&g)[8]) {
+  float l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) l[e] = (float)l8[e];
+  ce_grad8f(l, v0, cr, lab, n_valid, scale, g);
 }
 
 // Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5 "XCD swizzle must

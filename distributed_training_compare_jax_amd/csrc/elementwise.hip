@@ -299,6 +299,35 @@ __global__ void __launch_bounds__(256) ce_bwd_colsum_kernel(bf16* __restrict__ l
   *(f32x4*)(out + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
 }
 
+// fp32 logits (dtype: fp32 parity mode): dlogits in place + fp32 column partials, same structure
+__global__ void __launch_bounds__(256) ce_bwd_colsum_f32_kernel(float* __restrict__ logits, long ld,
+                                                               const float* __restrict__ lse,
+                                                               const int* __restrict__ labels, int M, int V,
+                                                               int vstart, int n_valid, float scale,
+                                                               float* __restrict__ colpart) {
+  const int n = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (n >= V) return;
+  const int m0 = blockIdx.y * CE_ROWS, m1 = min(M, m0 + CE_ROWS);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+  for (int m = m0; m < m1; ++m) {
+    float* p = logits + (long)m * ld + n;
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+    const float l[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    float g[8];
+    ce_grad8f(l, n, ce_row_c(lse[m], scale), labels[m] - vstart, n_valid, scale, g);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) cs[r] += g[r];
+    *(f32x4*)p = f32x4{g[0], g[1], g[2], g[3]};
+    *(f32x4*)(p + 4) = f32x4{g[4], g[5], g[6], g[7]};
+  }
+  if (colpart) {
+    float* out = colpart + (long)blockIdx.y * V + n;
+    *(f32x4*)out = f32x4{cs[0], cs[1], cs[2], cs[3]};
+    *(f32x4*)(out + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+  }
+}
+
 // ---------------------------------------------------------------- optimizer
 constexpr int SS_BLOCKS = 1024;
 
@@ -572,6 +601,17 @@ int dtc_ce_bwd(bf16* logits, long ld, const float* lse, const int* labels, int M
   long n = (long)M * (V / 8);
   hipLaunchKernelGGL(ce_bwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, logits, ld, lse, labels, M, V, vstart,
                      n_valid, scale);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// fp32 logits: colpart (optional) [ceil(M/CE_ROWS)][V]
+int dtc_ce_bwd_f32(float* logits, long ld, const float* lse, const int* labels, int M, int V, int vstart, int n_valid,
+                   float scale, float* colpart, hipStream_t st) {
+  if (V % 8 || ld % 4) return 3003;
+  dim3 grid((V / 8 + 255) / 256, (M + CE_ROWS - 1) / CE_ROWS);
+  hipLaunchKernelGGL(ce_bwd_colsum_f32_kernel, grid, dim3(256), 0, st, logits, ld, lse, labels, M, V, vstart, n_valid,
+                     scale, colpart);
   DTC_CHECK_LAUNCH();
   return 0;
 }

@@ -136,6 +136,14 @@ def _declare(lib):
         "dtc_ce_dgrad": ([vp, l, vp, vp, i, i, f, vp, l, vp, l, vp, vp, i, i, i, vp, l, vp], i),
         "dtc_ce_dgrad_workspace_bytes": ([i, i, i], l),
         "dtc_ce_dgrad_colpart_rows": ([i], i),
+        # exact-fp32 parity path (csrc/gemm_f32.hip, csrc/attention_f32.hip)
+        "dtc_gemm_f32": ([ctypes.POINTER(GemmArgs), vp], i),
+        "dtc_gemm_f32_workspace_bytes": ([i, i, i, i], l),
+        "dtc_lmhead_nparts_f32": ([i, i, i], i),
+        "dtc_attn_f32_fwd": ([vp, vp, vp, i, i, i, i, f, vp], i),
+        "dtc_attn_f32_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, vp, l, vp], i),
+        "dtc_attn_f32_bwd_workspace_bytes": ([i, i, i, i], l),
+        "dtc_ce_bwd_f32": ([vp, l, vp, vp, i, i, i, i, f, vp, vp], i),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -164,13 +172,12 @@ def lib():
 
 
 def library_path(t: torch.Tensor) -> bool:
-    """True when an op runs its torch implementation: CPU tensors (the fp32 oracle / gloo path) and
-    the GPU exact-fp32 parity mode (``TrainConfig.dtype: fp32``), whose GEMM-shaped ops
-    (Dense layers, attention scores, lm_head) run as fp32 library GEMMs (rocBLAS via torch; MI355X
-    has no reduced-precision fp32 MFMA, so they are exact) — every bf16 tensor takes the HIP
-    kernels.  LayerNorm, embedding/dropout, cross-entropy combine, reductions and AdamW run their
-    HIP kernels in both GPU precisions."""
-    return (not t.is_cuda) or t.dtype == torch.float32
+    """True when an op runs its pure-torch implementation: CPU tensors only (the fp32 oracle and
+    the gloo plumbing path).  Every GPU tensor takes a HIP kernel of ``_dtc_kernels.so`` in BOTH
+    precisions: bf16 (MFMA bf16, the default) and the exact-fp32 parity mode
+    (``TrainConfig.dtype: fp32``: ``csrc/gemm_f32.hip`` / ``csrc/attention_f32.hip`` on
+    ``v_mfma_f32_32x32x2_f32``) — no rocBLAS / hipBLASLt / torch matmul on the GPU path."""
+    return not t.is_cuda
 
 
 def stream_ptr(device=None) -> int:

@@ -6,6 +6,8 @@ score tensor materialised.  Here the mask is an in-kernel predicate (``-1e9`` th
 is exactly 0 in fp32, so the semantics are identical) and the scores never leave the chip:
 ``csrc/attention.hip`` is a flash-style kernel (online softmax, LSE saved for backward,
 P recomputed in backward) on ``mfma_f32_16x16x32_bf16`` with head_dim = 32 = one MFMA K.
+fp32 tensors (the exact-fp32 parity mode) run ``csrc/attention_f32.hip``: the same algorithm on
+``v_mfma_f32_32x32x2_f32`` (exact f32), again with no ``[B,H,T,T]`` tensor anywhere.
 
 Layout: the fused QKV GEMM writes ``qkv[B, T, 3, H, hd]`` (bf16); attention reads Q/K/V
 in place with strides and writes ``o[B, T, H, hd]`` which is directly the out_proj input.
@@ -36,11 +38,15 @@ def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None, flags:
         p = torch.exp(s - lse[..., None])
         o = torch.einsum("bhts,bshd->bthd", p, v).reshape(B, T, n_heads * hd)
         return o.to(qkv.dtype), lse
-    assert qkv.dtype == torch.bfloat16 and qkv.is_contiguous()
+    assert qkv.dtype in (torch.bfloat16, torch.float32) and qkv.is_contiguous()
     if hd != 32 and hd != 64:
         raise NotImplementedError(f"attention kernel supports head_dim 32/64, got {hd}")
-    o = torch.empty(B, T, n_heads * hd, dtype=torch.bfloat16, device=qkv.device)
+    o = torch.empty(B, T, n_heads * hd, dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty(B, n_heads, T, dtype=torch.float32, device=qkv.device)
+    if qkv.dtype == torch.float32:
+        N.check(N.lib().dtc_attn_f32_fwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, T, n_heads, hd, scale,
+                                         N.stream_ptr(qkv.device)), "dtc_attn_f32_fwd")
+        return o, lse
     N.check(N.lib().dtc_attn_fwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, T, n_heads, hd, int(flags), scale,
                                  N.stream_ptr(qkv.device)), "dtc_attn_fwd")
     return o, lse
@@ -70,6 +76,13 @@ def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Te
     assert do.is_contiguous() and o.is_contiguous()
     dqkv = torch.empty_like(qkv)
     L = N.lib()
+    if qkv.dtype == torch.float32:
+        assert do.dtype == torch.float32 and o.dtype == torch.float32
+        ws = _workspace(qkv.device, int(L.dtc_attn_f32_bwd_workspace_bytes(B, T, n_heads, hd)))
+        N.check(L.dtc_attn_f32_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), B, T,
+                                   n_heads, hd, scale, ws.data_ptr(), ws.numel(), N.stream_ptr(qkv.device)),
+                "dtc_attn_f32_bwd")
+        return dqkv
     ws = _workspace(qkv.device, int(L.dtc_attn_bwd_workspace_bytes(B, T, n_heads, hd)))
     N.check(L.dtc_attn_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), int(flags),
                            B, T, n_heads, hd, int(flags), scale, ws.data_ptr(), ws.numel(), N.stream_ptr(qkv.device)),

@@ -15,7 +15,10 @@ in ``csrc/gemm.hip`` (bf16 in, fp32 accumulate) with fused epilogues:
 * ``wgrad``          dW = β·dW + dYᵀ·X                    (fp32, written straight into the flat grad buffer)
 * ``colsum``         db = β·db + Σ_rows dY                (bias grads)
 
-CPU tensors take the pure-torch fp32 path below (the oracle / gloo path).
+fp32 GPU tensors (the exact-fp32 parity mode, ``dtype: fp32`` — the reference's precision) run the
+same ops on ``csrc/gemm_f32.hip`` (``v_mfma_f32_32x32x2_f32``, exact f32 products and fp32
+accumulation, same layouts and epilogues).  CPU tensors take the pure-torch fp32 path below (the
+oracle / gloo path).
 """
 
 from __future__ import annotations
@@ -85,7 +88,10 @@ def reserve_workspace(device, nbytes: int, role: str = "main"):
 
 def _gemm_native(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, **kw):
     args = _gemm_args(layout, M, N_, K, a, lda, b, ldb, c, ldc, **kw)
-    N.check(N.lib().dtc_gemm(args, N.stream_ptr(c.device)), "dtc_gemm")
+    if a.dtype == torch.float32:
+        N.check(N.lib().dtc_gemm_f32(args, N.stream_ptr(c.device)), "dtc_gemm_f32")
+    else:
+        N.check(N.lib().dtc_gemm(args, N.stream_ptr(c.device)), "dtc_gemm")
 
 
 def _gemm_args(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c, ldc: int, *,
@@ -97,7 +103,10 @@ def _gemm_args(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c
     if workspace is not None:
         ws = workspace.view(torch.uint8) if workspace.dtype != torch.uint8 else workspace
     else:
-        ws_need = int(L.dtc_gemm_workspace_bytes(layout, M, N_, K))
+        if a.dtype == torch.float32:
+            ws_need = int(L.dtc_gemm_f32_workspace_bytes(layout, M, N_, K))
+        else:
+            ws_need = int(L.dtc_gemm_workspace_bytes(layout, M, N_, K))
         ws = _workspace(c.device, ws_need) if ws_need > 0 else None
     args = N.GemmArgs(
         layout=layout, M=M, N=N_, K=K,
@@ -114,8 +123,8 @@ def _gemm_args(layout: int, M: int, N_: int, K: int, a, lda: int, b, ldb: int, c
 def _check2d(t: torch.Tensor, name: str):
     if t.dim() != 2 or t.stride(1) != 1:
         raise ValueError(f"{name}: expected a row-major 2-D tensor, got shape {tuple(t.shape)} strides {t.stride()}")
-    if t.is_cuda and t.dtype not in (torch.bfloat16,):
-        raise TypeError(f"{name}: GPU GEMM operands are bf16, got {t.dtype}")
+    if t.is_cuda and t.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError(f"{name}: GPU GEMM operands are bf16 (MFMA bf16) or fp32 (exact fp32 MFMA), got {t.dtype}")
 
 
 def _f32(t):
@@ -178,7 +187,7 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]):
             u = u + bias.float()
         return gelu_tanh_grad(u).to(x.dtype), gelu_tanh(u).to(x.dtype)
     _check2d(x, "x"); _check2d(w, "w")
-    u = torch.empty(M, Nn, dtype=torch.bfloat16, device=x.device)
+    u = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
     g = torch.empty_like(u)
     _gemm_native(0, M, Nn, K, x, x.stride(0), w, w.stride(0), u, Nn, epi=N.EPI_GELU, bias=bias, aux_out=g)
     return u, g
@@ -206,7 +215,7 @@ def matmul_nn_dgelu(dy: torch.Tensor, w: torch.Tensor, u: torch.Tensor) -> torch
     if N.library_path(dy):
         return ((_f32(dy) @ _f32(w)) * _f32(u)).to(u.dtype)
     _check2d(dy, "dy"); _check2d(w, "w")
-    du = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    du = torch.empty(M, K, dtype=u.dtype, device=dy.device)
     _gemm_native(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), du, K, epi=N.EPI_DGELU, aux=u, ldaux=K)
     return du
 
@@ -219,7 +228,7 @@ def matmul_nt_dgelu(dy: torch.Tensor, wt: torch.Tensor, u: torch.Tensor) -> torc
     if N.library_path(dy):
         return ((_f32(dy) @ _f32(wt).t()) * _f32(u)).to(u.dtype)
     _check2d(dy, "dy"); _check2d(wt, "wt")
-    du = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
+    du = torch.empty(M, K, dtype=u.dtype, device=dy.device)
     _gemm_native(0, M, K, dy.shape[1], dy, dy.stride(0), wt, wt.stride(0), du, K, epi=N.EPI_DGELU, aux=u, ldaux=K)
     return du
 
@@ -246,6 +255,11 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
         return dw
     _check2d(dy, "dy"); _check2d(x, "x")
     assert dw.dtype == torch.float32 and dw.is_contiguous()
+    if dy.dtype == torch.float32:  # exact-fp32 kernel: split-K + its own fixed-order reduce
+        _gemm_native(2, Nn, K, M, dy, dy.stride(0), x, x.stride(0), dw, K, beta=beta)
+        if db is not None:
+            colsum(dy, db, beta, red=red)
+        return dw
     if red is not None:
         L = N.lib()
         split = int(L.dtc_gemm_wgrad_split(Nn, K, M, 1 if db is not None else 0))
@@ -284,7 +298,7 @@ def linear_backward(dy: torch.Tensor, w: torch.Tensor, x: torch.Tensor, dw: torc
     read the same dY, the weight gradient's blocks fill the CUs the dgrad's last wave leaves
     idle, one dependent kernel boundary less); otherwise two calls.  ``wt``: the transposed weight
     ``[in, out]`` (``FlatParams.wt``) — the dgrad then runs as an NT GEMM (both operands K-major)."""
-    if N.library_path(dy) or red is None or not (_PAIR and pair):
+    if N.library_path(dy) or red is None or not (_PAIR and pair) or dy.dtype == torch.float32:
         if wt is not None and not N.library_path(dy):
             dx = matmul_nt_dgelu(dy, wt, dgelu_u) if dgelu_u is not None else linear(dy, wt, out_dtype=out_dtype)
         else:

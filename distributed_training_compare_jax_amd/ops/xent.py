@@ -43,8 +43,9 @@ def lmhead_logits_partials(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, la
         rs = torch.stack([mx, se], -1)
         return logits.to(h.dtype), (rs if combine else rs.unsqueeze(0)), lab
     L = N.lib()
-    P = int(L.dtc_lmhead_nparts(M, Vl, D))
-    logits = torch.empty(M, Vl, dtype=torch.bfloat16, device=h.device)
+    f32 = h.dtype == torch.float32  # exact-fp32 parity mode: fp32 logits (csrc/gemm_f32.hip)
+    P = int(L.dtc_lmhead_nparts_f32(M, Vl, D) if f32 else L.dtc_lmhead_nparts(M, Vl, D))
+    logits = torch.empty(M, Vl, dtype=h.dtype, device=h.device)
     part = torch.empty(P, M, 2, dtype=torch.float32, device=h.device)  # part-major (coalesced epilogue writes)
     # a single shard (combine=False) holds every row's label: the epilogue writes all of lab
     lab = (torch.zeros if combine else torch.empty)(M, dtype=torch.float32, device=h.device)
@@ -111,8 +112,9 @@ def ce_backward_inplace(logits: torch.Tensor, lse: torch.Tensor, labels: torch.T
     if colpart:
         R = (M + int(L.dtc_ce_colsum_rows()) - 1) // int(L.dtc_ce_colsum_rows())
         cp = torch.empty(R, Vl, dtype=torch.float32, device=logits.device)
-    N.check(L.dtc_ce_bwd(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), M, Vl, vocab_start,
-                         n_valid, grad_scale, N.ptr(cp), N.stream_ptr(logits.device)), "dtc_ce_bwd")
+    fn = L.dtc_ce_bwd_f32 if logits.dtype == torch.float32 else L.dtc_ce_bwd
+    N.check(fn(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), M, Vl, vocab_start,
+               n_valid, grad_scale, N.ptr(cp), N.stream_ptr(logits.device)), "dtc_ce_bwd")
     return (logits, cp) if colpart else logits
 
 

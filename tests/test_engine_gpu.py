@@ -137,9 +137,10 @@ def test_deferred_optimizer_matches_immediate(cuda, monkeypatch):
 
 
 def test_fp32_mode_matches_oracle(cuda):
-    """dtype: fp32 on the GPU (the reference's precision): exact-fp32 library GEMMs + HIP kernels for
-    LayerNorm / embedding / CE combine / reductions — loss and grads match the fp32 autograd oracle
-    to fp32 reassociation, far tighter than the bf16 path."""
+    """dtype: fp32 on the GPU (the reference's precision): every GEMM, the attention and the CE on our
+    exact-fp32 MFMA kernels (csrc/gemm_f32.hip, csrc/attention_f32.hip) + the HIP LayerNorm / embedding /
+    reduction / AdamW kernels — loss and grads match the fp32 autograd oracle to fp32 reassociation, far
+    tighter than the bf16 path."""
     eng, mc = _engine(cuda, use_graph=False, preset="tiny", dropout=0.1, dtype="fp32")
     assert eng.act_dtype == torch.float32
     b = next(get_batch_iterator(4, mc.max_seq_len + 1, vocab=999))
