@@ -19,6 +19,8 @@
 // hd+4 floats: a ds_read_b128 of 16 rows x 16 B then covers 64 distinct banks, and the 4 floats a lane
 // reads are 4 MFMA k-steps in a permuted d order shared by both operands (sums are order-free).
 // Deterministic: no atomics (separate dK/dV and dQ kernels, each output written by one wave).
+// Softmax runs in the log2 domain (scores pre-multiplied by scale*log2(e), v_exp_f32): ~1 ulp per
+// exponential, i.e. ~1e-6 relative on P at the score ranges here (tests: 1e-5 of the float64 result).
 #include "common.h"
 
 namespace {
@@ -29,6 +31,9 @@ constexpr int AW = 4;           // waves per block
 constexpr int AT = AW * 64;     // threads
 constexpr int QB = 32 * AW;     // rows (queries or keys) owned by one block
 constexpr int ST = 64;          // streamed rows per LDS stage (2 sub-tiles of 32)
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ int rowmap(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
@@ -136,6 +141,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_fwd_kernel(AttnFArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[dt][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
+  const float sc2 = a.scale * LOG2E;
 
   const int nstage = min((a.T + ST - 1) / ST, (q0 + QB + ST - 1) / ST);  // key stages up to the last query
   f32x4 rk[F::PT], rv[F::PT];
@@ -160,18 +166,18 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_fwd_kernel(AttnFArgs a) {
       float mloc = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float v = s[r] * a.scale;
+        float v = s[r] * sc2;
         if (kb + rowmap(r, half) > q) v = -INFINITY;
         s[r] = v;
         mloc = fmaxf(mloc, v);
       }
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_run, mloc);
-      const float alpha = expf(m_run - m_new);
+      const float m_new = fmaxf(m_run, mloc);  // log2 units
+      const float alpha = ex2(m_run - m_new);
       float lsum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = expf(s[r] - m_new);
+        const float p = ex2(s[r] - m_new);
         s[r] = p;
         lsum += p;
       }
@@ -198,7 +204,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_fwd_kernel(AttnFArgs a) {
       for (int rg = 0; rg < 4; ++rg)
         *(f32x4*)(og + dt * 32 + 8 * rg + 4 * half) =
             f32x4{oacc[dt][4 * rg] * inv, oacc[dt][4 * rg + 1] * inv, oacc[dt][4 * rg + 2] * inv, oacc[dt][4 * rg + 3] * inv};
-    if (half == 0) a.lse_out[(long)bh * a.T + q] = m_run + logf(l_run);
+    if (half == 0) a.lse_out[(long)bh * a.T + q] = (m_run + __builtin_amdgcn_logf(l_run)) * LN2;  // natural log
   }
 }
 
@@ -239,6 +245,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_dkdv_kernel(AttnFArgs a) {
   const float* lseg = a.lse + (long)bh * a.T;
   const float* dlg = a.delta + (long)bh * a.T;
   const int k0 = kbk * QB, kw = k0 + 32 * wave, key = kw + l32;
+  const float sc2 = a.scale * LOG2E;
 
   f32x4 kreg[F::NC], vreg[F::NC];
   F::load_fixed(kreg, kg, rs, key, a.T, half);
@@ -257,7 +264,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_dkdv_kernel(AttnFArgs a) {
     F::load(rd, dog, ors, s * ST, a.T, tid);
     if (tid < ST) {
       const int t = s * ST + tid;
-      rl = t < a.T ? lseg[t] : 0.f;
+      rl = t < a.T ? lseg[t] * LOG2E : 0.f;
       rdl = t < a.T ? dlg[t] : 0.f;
     }
   };
@@ -290,7 +297,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_dkdv_kernel(AttnFArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = sub * 32 + rowmap(r, half), qa = s * ST + qi;
-        float pv = expf(p[r] * a.scale - sL[qi]);
+        float pv = ex2(fmaf(p[r], sc2, -sL[qi]));
         if (key > qa || qa >= a.T) pv = 0.f;
         p[r] = pv;
         dp[r] = pv * (dp[r] - sDl[qi]);  // dS
@@ -334,7 +341,8 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_dq_kernel(AttnFArgs a) {
   f32x4 qreg[F::NC], doreg[F::NC];
   F::load_fixed(qreg, qg, rs, q, a.T, half);
   F::load_fixed(doreg, a.dout + (long)b * a.T * ors + (long)h * HD, ors, q, a.T, half);
-  const float lse_q = q < a.T ? a.lse[(long)bh * a.T + q] : 0.f;
+  const float lse_q = q < a.T ? a.lse[(long)bh * a.T + q] * LOG2E : 0.f;
+  const float sc2 = a.scale * LOG2E;
   const float dl_q = q < a.T ? a.delta[(long)bh * a.T + q] : 0.f;
   f32x16 dq[F::DT];
 #pragma unroll
@@ -366,7 +374,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_dq_kernel(AttnFArgs a) {
       f32x16 dp = F::template dot<true>(sV + sub * 32 * F::LD, doreg, l32, half);  // dP^T = V dO^T
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float pv = expf(p[r] * a.scale - lse_q);
+        float pv = ex2(fmaf(p[r], sc2, -lse_q));
         if (kb + rowmap(r, half) > q) pv = 0.f;
         dp[r] = pv * (dp[r] - dl_q);  // dS^T
       }

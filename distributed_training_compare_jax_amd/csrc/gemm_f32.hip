@@ -25,7 +25,7 @@
 //  * Register-staged, double-buffered LDS (the loads of k-tile t+1 are in flight under the MFMAs
 //    of tile t, written after them, one barrier per 16-deep k-tile = 8 MFMA k-steps per barrier).
 //  * Buffer-resource loads: rows past M/N read 0 by the hardware range check (ragged edges are
-//    branch-free); K must be a multiple of 16 (host-checked; every model dimension is).
+//    branch-free); a ragged last k-tile is zero-filled by a select (K % 4 == 0, host-checked).
 //  * Accumulator layout (32x32 C/D map: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)) puts n on the
 //    lane: each store instruction writes two 128-B row segments; bias is one load per lane.
 //  * Split-K (fp32 slabs + fixed-order reduce) for the long-K / small-MN shapes (weight gradients,
@@ -39,32 +39,46 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int NTF = 256;  // threads per block
-constexpr int BKF = 16;   // k per LDS stage
+constexpr int BKF = 16;   // K granularity (every plan's k-tile is a multiple)
 
-template <int R, bool KMAJ>
+// k per LDS stage: the MFMAs between two barriers are (BK/2) * TM * TN per wave; 16 for the 128x128
+// tile (32 MFMAs = 2048 cycles per barrier), 32 for the smaller tiles so they get as many
+template <int TM, int TN>
+constexpr int bk_of() { return TM * TN >= 4 ? 16 : 32; }
+
+template <int R, bool KMAJ, int BK>
 struct FTile {
-  // LDS image [BKF][LD] floats: element (k, r) at k*LD + r
-  static constexpr int LD = KMAJ ? R + 2 : R + 4;
-  static constexpr int ELEMS = BKF * LD;
-  static constexpr int CHUNKS = R * BKF / 4;  // float4 chunks per tile
+  // LDS image [BK][LD] floats: element (k, r) at k*LD + r.  K-major tiles are written transposed,
+  // 4 ds_write_b32 per float4: a half-wave covers 32/(BK/4) rows x BK/4 k-quads, bank
+  // (4*kq*LD + j*LD + row) % 32, distinct over the 32 lanes when 4*LD = 32/(BK/4) (mod 32): LD = R+2
+  // for BK 16, R+1 for BK 32.  M/N-major tiles are written as float4 (16-B aligned rows: R+4).
+  static constexpr int LD = KMAJ ? (BK == 16 ? R + 2 : R + 1) : R + 4;
+  static constexpr int ELEMS = BK * LD;
+  static constexpr int CHUNKS = R * BK / 4;  // float4 chunks per tile
   static constexpr int PT = CHUNKS / NTF;
   static_assert(CHUNKS % NTF == 0, "tile too small for 256 threads");
 
   // rs: resource whose base is the operand's first row of this tile (KMAJ: row r0; else k-row k0)
+  // k indices >= klim (the split's end, in the resource's k coordinates) read as 0: a K that is not
+  // a multiple of BK (any K % 4 == 0 works) and split boundaries inside a k-tile
   __device__ __forceinline__ static void load(f32x4 (&reg)[PT], __amdgpu_buffer_rsrc_t rs, long ld, int kofs, int rofs,
-                                              int tid) {
+                                              int klim, int tid) {
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int c = tid + i * NTF;
       long off;
+      bool ok;
       if (KMAJ) {
-        const int row = c >> 2, kq = c & 3;
+        const int row = c / (BK / 4), kq = c % (BK / 4);
         off = ((long)row * ld + kofs + 4 * kq) * 4;
+        ok = kofs + 4 * kq < klim;
       } else {
         const int krow = c / (R / 4), col = (c % (R / 4)) * 4;
         off = ((long)(kofs + krow) * ld + rofs + col) * 4;
+        ok = kofs + krow < klim;
       }
-      reg[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+      const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+      reg[i] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   __device__ __forceinline__ static void store(const f32x4 (&reg)[PT], float* lds, int tid) {
@@ -72,7 +86,7 @@ struct FTile {
     for (int i = 0; i < PT; ++i) {
       const int c = tid + i * NTF;
       if (KMAJ) {
-        const int row = c >> 2, kq = c & 3;
+        const int row = c / (BK / 4), kq = c % (BK / 4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) lds[(4 * kq + j) * LD + row] = reg[i][j];
       } else {
@@ -111,9 +125,9 @@ __device__ __forceinline__ float exp_f32(float x) { return expf(x); }
 
 template <int TM, int TN, bool AK, bool BKM, int EPI>
 __global__ void __launch_bounds__(NTF, 2) gemm_f32_kernel(GemmF g) {
-  constexpr int BM = 64 * TM, BN = 64 * TN;
-  using TA = FTile<BM, AK>;
-  using TB = FTile<BN, BKM>;
+  constexpr int BM = 64 * TM, BN = 64 * TN, BK = bk_of<TM, TN>();
+  using TA = FTile<BM, AK, BK>;
+  using TB = FTile<BN, BKM, BK>;
   constexpr int BUF = TA::ELEMS + TB::ELEMS;
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
 
@@ -125,16 +139,18 @@ __global__ void __launch_bounds__(NTF, 2) gemm_f32_kernel(GemmF g) {
   const int tm_idx = tile % g.tiles_m, tn_idx = tile / g.tiles_m;  // M-tiles fastest: blocks of one
   const int m0 = tm_idx * BM, n0 = tn_idx * BN;                    // XCD share the B (weight) panel
   const int kbeg = z * g.kps;
-  const int nk = min(g.kps, g.K - kbeg) / BKF;
+  const int klen = min(g.kps, g.K - kbeg);
+  const int nk = (klen + BK - 1) / BK;  // a ragged last k-tile is zero-filled by the loads
 
   // resources: K-major operands start at the tile's first row, M/N-major at the split's first k-row
   const long a_base = AK ? (long)m0 * g.lda : (long)kbeg * g.lda;
   const long b_base = BKM ? (long)n0 * g.ldb : (long)kbeg * g.ldb;
   const __amdgpu_buffer_rsrc_t rsA = rsrc_from(g.A + a_base, g.a_elems - a_base);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_from(g.B + b_base, g.b_elems - b_base);
-  // k offset inside the resource: K-major -> kbeg + t*BKF (column), M/N-major -> t*BKF (row)
-  auto kofs = [&](int t) { return t * BKF; };
+  // k offset inside the resource: K-major -> kbeg + t*BK (column), M/N-major -> t*BK (row)
+  auto kofs = [&](int t) { return t * BK; };
   const int ak0 = AK ? kbeg : 0, bk0 = BKM ? kbeg : 0;
+  const int alim = ak0 + klen, blim = bk0 + klen;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -146,8 +162,8 @@ __global__ void __launch_bounds__(NTF, 2) gemm_f32_kernel(GemmF g) {
 
   f32x4 ra[TA::PT], rb[TB::PT];
   if (nk > 0) {
-    TA::load(ra, rsA, g.lda, ak0 + kofs(0), m0, tid);
-    TB::load(rb, rsB, g.ldb, bk0 + kofs(0), n0, tid);
+    TA::load(ra, rsA, g.lda, ak0 + kofs(0), m0, alim, tid);
+    TB::load(rb, rsB, g.ldb, bk0 + kofs(0), n0, blim, tid);
     TA::store(ra, smem, tid);
     TB::store(rb, smem + TA::ELEMS, tid);
   }
@@ -158,11 +174,11 @@ __global__ void __launch_bounds__(NTF, 2) gemm_f32_kernel(GemmF g) {
     const float* sB = sA + TA::ELEMS;
     const bool more = t + 1 < nk;
     if (more) {
-      TA::load(ra, rsA, g.lda, ak0 + kofs(t + 1), m0, tid);
-      TB::load(rb, rsB, g.ldb, bk0 + kofs(t + 1), n0, tid);
+      TA::load(ra, rsA, g.lda, ak0 + kofs(t + 1), m0, alim, tid);
+      TB::load(rb, rsB, g.ldb, bk0 + kofs(t + 1), n0, blim, tid);
     }
 #pragma unroll
-    for (int kk = 0; kk < BKF / 2; ++kk) {
+    for (int kk = 0; kk < BK / 2; ++kk) {
       const int k = 2 * kk + half;
       float fa[TM], fb[TN];
 #pragma unroll
@@ -291,7 +307,8 @@ struct PlanF {
 };
 
 // Tile / split-K choice: the biggest tile that still gives >= 2 blocks per CU (512), then smaller
-// tiles, then split-K over the largest tile for long-K problems that cannot fill the chip.
+// tiles, then split-K over the largest tile for long-K problems that cannot fill the chip.  Every
+// split's k range is a multiple of the variant's BK (a K that is not falls back to the BK-16 tile).
 PlanF plan_f32(int M, int N, int K) {
   static const int cands[3][2] = {{2, 2}, {2, 1}, {1, 1}};
   const int target = 512;
@@ -299,15 +316,15 @@ PlanF plan_f32(int M, int N, int K) {
     const int tm = (M + 64 * c[0] - 1) / (64 * c[0]), tn = (N + 64 * c[1] - 1) / (64 * c[1]);
     if ((long)tm * tn >= target) return PlanF{c[0], c[1], 1, K, tm, tn};
   }
-  // split-K: 128x128 if K is long, else 64x64; slices of >= 256 k (multiples of BKF)
-  const bool big = K >= 4096;
-  const int ct = big ? 2 : 1;
+  // split-K: 128x128 if K is long, else 64x64; slices of >= 256 k
+  const int ct = K >= 4096 ? 2 : 1;
+  const int bk = ct == 2 ? 16 : 32;
   const int tm = (M + 64 * ct - 1) / (64 * ct), tn = (N + 64 * ct - 1) / (64 * ct);
   const long tiles = (long)tm * tn;
   int split = (int)std::max<long>(1, (target + tiles - 1) / tiles);
   split = std::min(split, std::max(1, K / 256));
   int kps = (K + split - 1) / split;
-  kps = (kps + BKF - 1) / BKF * BKF;
+  kps = (kps + bk - 1) / bk * bk;
   split = (K + kps - 1) / kps;
   return PlanF{ct, ct, split, kps, tm, tn};
 }
@@ -359,7 +376,8 @@ int dtc_lmhead_nparts_f32(int M, int N, int K) {
 int dtc_gemm_f32(const GemmArgs* a, hipStream_t st) {
   DTC_HOST_CHECK(a->layout >= 0 && a->layout <= 2);
   DTC_HOST_CHECK(a->c_f32 == 1);
-  DTC_HOST_CHECK(a->K % BKF == 0 && a->M > 0 && a->N > 0);
+  DTC_HOST_CHECK(a->K > 0 && a->M > 0 && a->N > 0);
+  DTC_HOST_CHECK(a->layout == 2 || a->K % 4 == 0);  // float4 loads along k of a K-major operand
   DTC_HOST_CHECK(a->lda % 4 == 0 && a->ldb % 4 == 0);
   DTC_HOST_CHECK(((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0);
   const bool AK = a->layout != 2, BKM = a->layout == 0;
@@ -385,8 +403,8 @@ int dtc_gemm_f32(const GemmArgs* a, hipStream_t st) {
   }
   if (p.split > 1 && (long)p.split * a->M * a->N * 4 > a->ws_bytes) return 1101;  // workspace too small
   g.tiles_m = p.tiles_m; g.tiles_n = p.tiles_n; g.split = p.split; g.kps = p.kps;
-  DTC_HOST_CHECK(AK ? fits(128L * a->lda) : fits((long)(p.kps + BKF) * a->lda));
-  DTC_HOST_CHECK(BKM ? fits(128L * a->ldb) : fits((long)(p.kps + BKF) * a->ldb));
+  DTC_HOST_CHECK(AK ? fits(128L * a->lda) : fits((long)(p.kps + 32) * a->lda));
+  DTC_HOST_CHECK(BKM ? fits(128L * a->ldb) : fits((long)(p.kps + 32) * a->ldb));
   g.slab = (float*)a->workspace;
   if (a->epi == EPI_LMHEAD && a->layout != 0) return (int)hipErrorInvalidValue;
   int rc;

@@ -22,6 +22,7 @@ import os
 import pandas as pd
 
 CLK, SIMDS = 2.4e9, 1024
+SIMDS_FLOP = 1024  # bf16 16x16x32: 1024 FLOP per MFMA-busy cycle per SIMD
 
 
 def load(d):
@@ -43,10 +44,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tag", default="step", help="pmc_<tag>{1,2,3} directories (scripts/pmc_step.sh PMC_TAG)")
+    ap.add_argument("--fp32", action="store_true",
+                    help="exact-fp32 step: MFMA busy cycles are v_mfma_f32_32x32x2_f32 (64 FLOP/cycle/SIMD, 157 TF peak)")
+    ap.add_argument("--title", default="Whole-step hardware counters (rocprofv3 --pmc, 3 passes, one step of bench.py)")
     a = ap.parse_args()
+    flop_cyc = 64 if a.fp32 else SIMDS_FLOP
     frames = []
     for i in (1, 2, 3):
-        s = last_step(load(os.path.join(a.root, f"pmc_step{i}")))
+        s = last_step(load(os.path.join(a.root, f"pmc_{a.tag}{i}")))
         s = s.assign(order=s.Dispatch_Id.rank(method="dense").astype(int))
         frames.append(s)
     # the three passes run the same dispatch sequence: align them by position within the step
@@ -71,15 +77,17 @@ def main():
                                  ldsa=("SQ_ACTIVE_INST_LDS", "sum"))
     g = g.sort_values("dur_us", ascending=False)
     tot = g.dur_us.sum()
-    lines = [f"# Whole-step hardware counters (rocprofv3 --pmc, 3 passes, one step of bench.py)", "",
+    lines = [f"# {a.title}", "",
              f"{int(g.calls.sum())} dispatches, {tot:.0f} us summed dispatch time under PMC; step MFMA FLOPs "
-             f"{g.mfma.sum() * SIMDS / 1e12:.3f} TFLOP, HBM traffic {(2 * g.fetch.sum() + g.write.sum()) * 1024 / 1e9:.2f} GB.", "",
+             f"{g.mfma.sum() * flop_cyc / 1e12:.3f} TFLOP, HBM traffic {(2 * g.fetch.sum() + g.write.sum()) * 1024 / 1e9:.2f} GB.",
+             "", "MFMA util = MFMA-busy fraction of all SIMD cycles" + (
+                 " (exact-fp32 MFMA: 100 % = 157 TF/s)" if a.fp32 else " (bf16: 100 % = 2.5 PF/s dense)"), "",
              "| kernel | calls | us | % | MFMA util | MFMA TF/s | HBM GB/s | SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS |",
              "|---|---|---|---|---|---|---|---|"]
     for n, r in g.iterrows():
         s = r.dur_us * 1e-6
         util = r.mfma / (s * CLK * SIMDS) if s > 0 else 0
-        tf = r.mfma * SIMDS / s / 1e12 if s > 0 else 0
+        tf = r.mfma * flop_cyc / s / 1e12 if s > 0 else 0
         bw = (2 * r.fetch + r.write) * 1024 / s / 1e9 if s > 0 else 0
         lc = f"{r.ldsc / r.ldsa:.3f}" if r.ldsa > 0 else "-"
         lines.append(f"| `{n}` | {int(r.calls)} | {r.dur_us:.1f} | {100 * r.dur_us / tot:.1f} | "
