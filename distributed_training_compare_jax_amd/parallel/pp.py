@@ -3,15 +3,26 @@
 Reference PP (``train/create_train_step.py:55-195``): GPipe fill/drain expressed as a
 ``lax.scan`` over ``M+S-1`` clocks where EVERY stage runs ``lax.cond``-gated work on every
 clock and ``ppermute`` shifts activations, labels and a valid flag each clock (also on
-bubble clocks); backward is autodiff of the scan.  Here the schedule is a host-side
-static program:
+bubble clocks); backward is autodiff of the scan.  Here each stage runs a host-side static
+PROGRAM (:func:`pp_program`) of compute items and communication entries:
 
 * only valid (stage, microbatch) work exists — no bubble-clock compute or traffic;
 * labels never travel (every rank reads its own rows; reference ppermutes them, ``:165``);
-* activations travel as fp32 ``[mb·T, D]`` (the residual stream) with
-  ``isend``/``irecv``; the receiver waits right before the consuming segment;
-* ``gpipe`` = reference order (all forwards, then all backwards), ``1f1b`` = PipeDream-flush
-  order (activation memory bounded by S microbatches instead of M).
+* activations travel as fp32 ``[mb·T, D]`` (the residual stream), gradients likewise;
+* ``gpipe`` = reference order (all forwards, then all backwards) with the receive of the next
+  microbatch posted BEFORE the current one computes (the transfer runs under the compute);
+* ``1f1b`` = PipeDream-flush order (activation memory bounded by S microbatches instead of M), with
+  Megatron's paired exchanges: in the steady state the send of a forward output and the receive of
+  a backward gradient — both with the next stage — are ONE grouped RCCL call
+  (``batch_isend_irecv``), and likewise send-gradient/receive-activation with the previous stage.
+
+Why the pairing matters on RCCL: all p2p traffic between two ranks runs, in issue order, on that
+pair's communicator stream, and a send completes only against the matching receive.  Two stages
+that each issue "send to you" before "receive from you" therefore wait on each other forever (a
+buffered backend such as gloo hides this).  A grouped call is one kernel that makes progress on
+both directions at once.  :func:`simulate` replays the programs of all stages under exactly these
+semantics (per-pair ordered queues, rendezvous matching, groups atomic) and is run by the CPU tests
+for every S / M / schedule the engine accepts — no-deadlock and message order by construction.
 
 Loss/gradient scaling is exact: each microbatch's CE is scaled by ``1/(mb·T·M)`` so the
 sum over microbatches is the full-batch mean (reference: ``psum(loss_sum / M)``, ``:187``).
@@ -19,7 +30,7 @@ sum over microbatches is the full-batch mean (reference: ``psum(loss_sum / M)``,
 
 from __future__ import annotations
 
-from typing import Dict, List
+from typing import Dict, List, Tuple
 
 import torch
 import torch.distributed as dist
@@ -27,27 +38,16 @@ import torch.distributed as dist
 from ..ops.optim import cast_to_bf16, fill_
 from .dist import staged_p2p
 
-
-class _HostSend:
-    """isend of a device tensor through a host copy (gloo backend); ``wait()`` like a Work."""
-
-    def __init__(self, t, dst):
-        self.host = t.detach().to("cpu")
-        self.work = dist.isend(self.host, dst)
-
-    def wait(self):
-        self.work.wait()
-        self.host = None
-
-
-def _host_recv(buf, src):
-    host = torch.empty(buf.shape, dtype=buf.dtype)
-    dist.recv(host, src)
-    buf.copy_(host)
+# ------------------------------------------------------------------------------ static programs
+# items: ("F", i) / ("B", i)                         compute of microbatch i
+#        ("post", name, peer, sends, recvs)          one (grouped) p2p call with stage s+peer;
+#                                                    sends/recvs: tuples of tags ("f"|"b", i)
+#        ("wait", names)                              the compute stream waits for these entries
+# tag ("f", i): activation of microbatch i, stage s -> s+1; ("b", i): its gradient, s+1 -> s.
 
 
 def _schedule(kind: str, S: int, s: int, M: int) -> List[tuple]:
-    """List of ('F', mb) / ('B', mb) for stage s of S."""
+    """Compute order ('F', mb) / ('B', mb) for stage s of S."""
     if kind == "gpipe" or S == 1:
         return [("F", i) for i in range(M)] + [("B", i) for i in reversed(range(M))]
     if kind != "1f1b":
@@ -66,6 +66,160 @@ def _schedule(kind: str, S: int, s: int, M: int) -> List[tuple]:
     return ops
 
 
+def pp_program(kind: str, S: int, s: int, M: int) -> List[tuple]:
+    first, last = s == 0, s == S - 1
+    prog: List[tuple] = []
+    sends: List[str] = []
+
+    def post(name, peer, snd=(), rcv=()):
+        prog.append(("post", name, peer, tuple(snd), tuple(rcv)))
+        return name
+
+    def send_f(i):
+        if not last:
+            sends.append(post(f"sf{i}", +1, snd=[("f", i)]))
+
+    def send_b(i):
+        if not first:
+            sends.append(post(f"sb{i}", -1, snd=[("b", i)]))
+
+    if kind == "gpipe" or S == 1:
+        # all forwards, then all backwards (reverse microbatch order); the receive of the next
+        # microbatch of the same phase is posted before the current one computes
+        for phase in ("F", "B"):
+            mbs = list(range(M)) if phase == "F" else list(reversed(range(M)))
+            has = (not first) if phase == "F" else (not last)
+            d, peer = ("f", -1) if phase == "F" else ("b", +1)
+            if has:
+                post(f"r{d}{mbs[0]}", peer, rcv=[(d, mbs[0])])
+            for n, i in enumerate(mbs):
+                if has:
+                    prog.append(("wait", (f"r{d}{i}",)))
+                    if n + 1 < len(mbs):
+                        post(f"r{d}{mbs[n + 1]}", peer, rcv=[(d, mbs[n + 1])])
+                prog.append((phase, i))
+                send_f(i) if phase == "F" else send_b(i)
+        if sends:
+            prog.append(("wait", tuple(sends)))
+        return prog
+
+    if kind != "1f1b":
+        raise ValueError(f"unknown pp_schedule {kind}")
+    warm = min(S - s - 1, M)
+
+    def recv_f(i):
+        if not first:
+            prog.append(("wait", (post(f"rf{i}", -1, rcv=[("f", i)]),)))
+
+    def recv_b(i):
+        if not last:
+            prog.append(("wait", (post(f"rb{i}", +1, rcv=[("b", i)]),)))
+
+    for i in range(warm):
+        recv_f(i)
+        prog.append(("F", i))
+        send_f(i)
+    rem = M - warm
+    if rem > 0:
+        recv_f(warm)
+    for j in range(rem):
+        i = warm + j
+        prog.append(("F", i))
+        if not last:  # send_forward + recv_backward with the next stage: one grouped call
+            n = post(f"xf{i}b{j}", +1, snd=[("f", i)], rcv=[("b", j)])
+            prog.append(("wait", (n,)))
+        prog.append(("B", j))
+        if j == rem - 1:
+            send_b(j)
+        elif not first:  # send_backward + recv_forward with the previous stage
+            n = post(f"xb{j}f{i + 1}", -1, snd=[("b", j)], rcv=[("f", i + 1)])
+            prog.append(("wait", (n,)))
+    for j in range(rem, M):
+        recv_b(j)
+        prog.append(("B", j))
+        send_b(j)
+    if sends:
+        prog.append(("wait", tuple(sends)))
+    return prog
+
+
+def simulate(kind: str, S: int, M: int) -> Dict[str, int]:
+    """Run every stage's :func:`pp_program` under RCCL p2p semantics and return counters.
+
+    Model: each stage executes its items in order on one compute stream; a ``post`` enqueues its
+    entry on the (stage, peer) pair queue once every earlier compute item of the stage is done
+    (the comm stream waits on the compute stream); the heads of the two queues of a pair complete
+    TOGETHER when both are posted and complementary (sends of one == receives of the other, as
+    sets: a grouped call); a ``wait`` blocks the stage until its entries completed.  Raises
+    RuntimeError on a deadlock or on a head pair that does not match (wrong message order)."""
+    progs = [pp_program(kind, S, s, M) for s in range(S)]
+    pc = [0] * S
+    queues: Dict[Tuple[int, int], List[tuple]] = {}
+    done = set()
+    counts = {"posts": 0, "waits": 0, "compute": 0}
+    while True:
+        progressed = False
+        for s in range(S):
+            while pc[s] < len(progs[s]):
+                it = progs[s][pc[s]]
+                if it[0] == "post":
+                    _, name, peer, snd, rcv = it
+                    queues.setdefault((s, s + peer), []).append((name, frozenset(snd), frozenset(rcv)))
+                    counts["posts"] += 1
+                elif it[0] == "wait":
+                    if not all((s, n) in done for n in it[1]):
+                        break
+                    counts["waits"] += 1
+                else:
+                    counts["compute"] += 1
+                pc[s] += 1
+                progressed = True
+        for (a, b), qa in list(queues.items()):
+            qb = queues.get((b, a), [])
+            while qa and qb:
+                na, sa, ra = qa[0]
+                nb, sb, rb = qb[0]
+                if sa != rb or ra != sb:
+                    # two sends (or two receives) at the heads of a pair wait on each other forever
+                    what = "deadlock (head-of-line)" if (sa and sb and not (ra or rb)) or (ra and rb and not (
+                        sa or sb)) else "message order mismatch"
+                    raise RuntimeError(f"{kind} S={S} M={M}: {what}: stage {a} entry {na} sends {sorted(sa)} "
+                                       f"receives {sorted(ra)}, stage {b} entry {nb} sends {sorted(sb)} "
+                                       f"receives {sorted(rb)}")
+                qa.pop(0)
+                qb.pop(0)
+                done.add((a, na))
+                done.add((b, nb))
+                progressed = True
+        if all(pc[s] == len(progs[s]) for s in range(S)):
+            left = {k: v for k, v in queues.items() if v}
+            if left:
+                raise RuntimeError(f"{kind} S={S} M={M}: unmatched entries at the end: {left}")
+            return counts
+        if not progressed:
+            stuck = {s: progs[s][pc[s]] for s in range(S) if pc[s] < len(progs[s])}
+            raise RuntimeError(f"{kind} S={S} M={M}: deadlock, stages blocked at {stuck}")
+
+
+# ------------------------------------------------------------------------------ executor
+class _HostSend:
+    """isend of a device tensor through a host copy (gloo backend); ``wait()`` like a Work."""
+
+    def __init__(self, t, dst):
+        self.host = t.detach().to("cpu")
+        self.work = dist.isend(self.host, dst)
+
+    def wait(self):
+        self.work.wait()
+        self.host = None
+
+
+def _host_recv(buf, src):
+    host = torch.empty(buf.shape, dtype=buf.dtype)
+    dist.recv(host, src)
+    buf.copy_(host)
+
+
 def run_pipeline(eng) -> None:
     m = eng.mesh
     st = eng.stage
@@ -75,57 +229,95 @@ def run_pipeline(eng) -> None:
     first, last = s == 0, s == S - 1
     step = eng.opt.step_t
     ctxs: Dict[int, Dict] = {i: {} for i in range(M)}
-    outs: Dict[int, torch.Tensor] = {}
     grad_scale = 1.0 / (rows * T * M * m.dp)
     loss_scale = 1.0 / (rows * T * M)
-    order = _schedule(eng.tcfg.pp_schedule, S, s, M)
     n_bwd_done = 0
-    sends = []
     if not last:
         fill_(eng.loss, 0.0)
-
     staged = staged_p2p() and eng.device.type == "cuda"
+    outs: Dict[int, torch.Tensor] = {}  # forward outputs (sent to the next stage)
 
-    def isend(t, dst, tag):
-        name = f"send_{tag}"
-        if staged:  # gloo carries host tensors only: stage through pinned host memory
-            prog.comm(lambda: _HostSend(t, dst), name=name)
-        else:
-            prog.comm(lambda: dist.isend(t, dst), name=name)
-        sends.append(name)
+    def tensor_of(tag, sending):
+        d, i = tag
+        if d == "f":
+            return outs[i] if sending else eng.recv_x[i]
+        return dx_out[i] if sending else eng.recv_dx[i]
 
-    def recv(buf, src, tag):
-        name = f"recv_{tag}"
-        if staged:
-            prog.comm(lambda: _host_recv(buf, src), name=None)
-            return
-        prog.comm(lambda: dist.irecv(buf, src), name=name)
-        prog.wait(name)
+    def issue(peer, snd, rcv):
+        """One grouped p2p call; snd / rcv are tensors (resolved when the program runs, so a replayed
+        hipGraph step moves the same buffers)."""
+        rank = m.pp_next if peer > 0 else m.pp_prev
+        if staged:  # gloo carries host tensors only: host-staged sends, blocking host receives
+            works = [_HostSend(t, rank) for t in snd]
+            for t in rcv:
+                _host_recv(t, rank)
+            return works
+        ops = [dist.P2POp(dist.isend, t, rank) for t in snd]
+        ops += [dist.P2POp(dist.irecv, t, rank) for t in rcv]
+        return dist.batch_isend_irecv(ops)
 
-    for kind, i in order:
+    def run_comm(run):
+        """Every p2p item between two compute items in ONE collective call (one graph cut): posts
+        whose wait is in the same run are waited right away, the others are parked by name."""
+        waited_here = {n for it in run if it[0] == "wait" for n in it[1]}
+        steps = []
+        for it in run:
+            if it[0] == "post":
+                _, name, peer, snd, rcv = it
+                steps.append(("post", name, peer, [tensor_of(t, True) for t in snd],
+                              [tensor_of(t, False) for t in rcv]))
+            else:
+                steps.append(it)
+        local = {}
+
+        def fn():
+            for st_ in steps:
+                if st_[0] == "post":
+                    _, name, peer, snd, rcv = st_
+                    works = issue(peer, snd, rcv)
+                    if name in waited_here:
+                        local[name] = works
+                    else:
+                        prog._handles[name] = works
+                else:
+                    for n in st_[1]:
+                        if n in local:
+                            for w in local.pop(n):
+                                w.wait()
+                        else:
+                            prog._wait(n)
+
+        prog.comm(fn)
+
+    items = pp_program(eng.tcfg.pp_schedule, S, s, M)
+    dx_out: Dict[int, torch.Tensor] = {}
+    k = 0
+    while k < len(items):
+        if items[k][0] in ("post", "wait"):
+            j = k
+            while j < len(items) and items[j][0] in ("post", "wait"):
+                j += 1
+            run_comm(items[k:j])
+            k = j
+            continue
+        kind, i = items[k]
         ids = eng.ids[i * rows:(i + 1) * rows]
         labels = eng.labels[i * rows:(i + 1) * rows]
         row0 = eng.row0 + i * rows
         ctx = ctxs[i]
         if kind == "F":
-            if first:
-                h = st.embed_forward(ids, step, row0, ctx)
-            else:
-                recv(eng.recv_x[i], m.pp_prev, f"f{i}")
-                h = eng.recv_x[i]
+            h = st.embed_forward(ids, step, row0, ctx) if first else eng.recv_x[i]
             h = st.stage_forward(h, rows, ctx)
             if last:
                 st.head_forward(h, labels, loss_scale, ctx, loss_out=eng.loss, accumulate=(i > 0))
             else:
                 outs[i] = h
-                isend(h, m.pp_next, f"f{i}")
         else:
             beta = 0.0 if n_bwd_done == 0 else 1.0
             n_bwd_done += 1
             if last:
                 dx, dx_c = st.head_backward(ctx, grad_scale, beta)
             else:
-                recv(eng.recv_dx[i], m.pp_next, f"b{i}")
                 dx = eng.recv_dx[i]
                 dx_c = eng.recv_dx_c[i]
                 if dx_c is not dx:
@@ -134,7 +326,5 @@ def run_pipeline(eng) -> None:
             if first:
                 st.embed_backward(ctx, dx, step, beta)
             else:
-                isend(dx, m.pp_prev, f"b{i}")
-            outs.pop(i, None)
-    for name in sends:
-        prog.wait(name)
+                dx_out[i] = dx
+        k += 1

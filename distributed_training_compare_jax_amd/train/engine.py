@@ -303,7 +303,7 @@ class Engine:
         if dp > 1:
             # the loss is final here: its DP mean goes out now, under the whole backward, instead of
             # as an exposed collective at the end of the step (joined before the optimizer)
-            self._loss_allreduce(name="loss_dp")
+            self._loss_allreduce(name="loss_dp")  # (pp == 1 here)
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
         bk, opt = self.buckets, self.opt
         side = st.red if st.red is not None else st.side.defer  # where grad-norm chunks are queued
@@ -356,21 +356,33 @@ class Engine:
         self._finish_optimizer()
         return self.loss
 
-    def _loss_allreduce(self, name: Optional[str] = None):
-        """Sum the loss over the DP (and PP) groups.  With ``name`` (DP only) the all-reduce is
-        asynchronous: :meth:`StepProgram.wait` joins it later."""
+    def _loss_allreduce(self, name: Optional[str] = None, pp: bool = False):
+        """Sum the loss over the DP group (and the PP group with ``pp``: only the last stage holds
+        it).  With ``name`` the all-reduces are asynchronous: :meth:`StepProgram.wait` joins them
+        later (the loss is read by the host only, nothing in the step consumes it)."""
         m = self.mesh
         groups = []
         if m.dp > 1:
             groups.append(m.dp_group)
-        if m.pp > 1 and name is None:
+        if m.pp > 1 and pp:
             groups.append(m.pp_group)
-        for g in groups:
-            t = self.loss
-            if name is not None:
-                self.program.comm(lambda g=g, t=t: dist.all_reduce(t, group=g, async_op=True), name=name)
-            else:
-                self.program.comm(lambda g=g, t=t: dist.all_reduce(t, group=g))
+        if not groups:
+            return []
+        t = self.loss
+        if name is None:
+            for g in groups:
+                self.program.comm(lambda g=g: dist.all_reduce(t, group=g))
+            return []
+        # one collective item (one graph cut): with both groups the pp sum must land before the dp
+        # sum reads the tensor (separate communicators / streams), so the first is joined to the
+        # issuing stream and only the last stays asynchronous
+        def fn():
+            for g in groups[:-1]:
+                dist.all_reduce(t, group=g, async_op=True).wait()
+            return dist.all_reduce(t, group=groups[-1], async_op=True)
+
+        self.program.comm(fn, name=name)
+        return [name]
 
     def _step_fn_pp(self):
         from ..parallel.pp import run_pipeline
@@ -378,9 +390,12 @@ class Engine:
         run_pipeline(self)
         self.stage.side.join()
         self.buckets.ready_all()
+        # the loss sum overlaps the bucket all-reduces and the optimizer; joined at the very end
+        waits = self._loss_allreduce(name="loss_pp", pp=True)
         self.buckets.wait_all()
-        self._loss_allreduce()
         self.opt.step()
+        for n in waits:
+            self.program.wait(n)
         return self.loss
 
     def _step_fn(self):

@@ -55,9 +55,13 @@ def _spawn_target(args):
 @click.option("--output_dir", default=None, help="override train_config.output_dir")
 @click.option("--profile", is_flag=True, default=False,
               help="roctx ranges + device step times + Chrome trace in <output_dir>/trace/")
+@click.option("--dtype", type=click.Choice(["bf16", "fp32"]), default=None,
+              help="compute precision (default bf16; fp32 = the reference's precision on the exact-fp32 kernels)")
 def main(train_config_path: str, model_config_path: str, optim_config_path: str, nproc, steps, device, log_every,
-         warmup_steps, output_dir, profile):
+         warmup_steps, output_dir, profile, dtype):
     overrides = {}
+    if dtype is not None:
+        overrides["dtype"] = dtype
     if output_dir is not None:
         overrides["output_dir"] = output_dir
     if profile:

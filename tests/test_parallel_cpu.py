@@ -84,6 +84,8 @@ def single():
     ("pp", 2, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("dp", 4, {"tp": 2}),
     ("pp", 4, {"dp": 2, "pp_microbatches": 2, "pp_clip": "global"}),
+    ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
+    ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "gpipe"}),
 ])
 def test_layout_matches_single_process(single, parallel, world, kw):
     res = _run(parallel, world, **kw)

@@ -1,0 +1,65 @@
+"""Pipeline programs (parallel/pp.py) under RCCL point-to-point semantics, without any GPU.
+
+RCCL runs all traffic between two ranks, in issue order, on that pair's communicator stream, and a
+send completes only against the matching receive; a buffered backend (gloo, which the CPU layout
+tests use) hides ordering bugs that would hang on the real node.  ``pp.simulate`` replays the
+static programs of all S stages with per-pair ordered queues, rendezvous matching and grouped calls
+as atomic units, and fails on a deadlock or on a message-order mismatch.
+"""
+
+import pytest
+
+from distributed_training_compare_jax_amd.parallel import pp as PP
+
+
+@pytest.mark.parametrize("kind", ["gpipe", "1f1b"])
+@pytest.mark.parametrize("S", [1, 2, 3, 4, 8])
+def test_programs_never_deadlock(kind, S):
+    for M in range(1, 17):
+        c = PP.simulate(kind, S, M)
+        assert c["compute"] == 2 * M * S  # every stage: one forward and one backward per microbatch
+
+
+def test_simulator_catches_the_ungrouped_1f1b_order(monkeypatch):
+    """The round-2 executor's order (send, then an ungrouped receive from the same peer) deadlocks
+    under blocking semantics as soon as S >= 2 and M >= 2: the simulator must see it."""
+    def naive(kind, S, s, M):
+        prog, sends = [], []
+        for k, i in PP._schedule(kind, S, s, M):
+            if k == "F":
+                if s > 0:
+                    prog += [("post", f"rf{i}", -1, (), (("f", i),)), ("wait", (f"rf{i}",))]
+                prog.append(("F", i))
+                if s < S - 1:
+                    prog.append(("post", f"sf{i}", +1, (("f", i),), ()))
+                    sends.append(f"sf{i}")
+            else:
+                if s < S - 1:
+                    prog += [("post", f"rb{i}", +1, (), (("b", i),)), ("wait", (f"rb{i}",))]
+                prog.append(("B", i))
+                if s > 0:
+                    prog.append(("post", f"sb{i}", -1, (("b", i),), ()))
+                    sends.append(f"sb{i}")
+        return prog + ([("wait", tuple(sends))] if sends else [])
+
+    monkeypatch.setattr(PP, "pp_program", naive)
+    PP.simulate("gpipe", 4, 4)  # GPipe's phases never cross on a pair: fine even ungrouped
+    with pytest.raises(RuntimeError, match="deadlock"):
+        PP.simulate("1f1b", 2, 2)
+
+
+@pytest.mark.parametrize("kind", ["gpipe", "1f1b"])
+def test_comm_cuts_per_microbatch(kind):
+    """Every run of p2p items between two compute items is ONE collective call (one graph cut in a
+    replayed step): at most one per compute item + 1, i.e. ~2 per microbatch per stage (round 2:
+    recv = post + wait, send = post, each its own cut -> ~6 per microbatch)."""
+    S, M = 4, 8
+    for s in range(S):
+        prog = PP.pp_program(kind, S, s, M)
+        runs, prev_comm = 0, False
+        for it in prog:
+            is_comm = it[0] in ("post", "wait")
+            if is_comm and not prev_comm:
+                runs += 1
+            prev_comm = is_comm
+        assert runs <= 2 * M + 1, (s, runs)
