@@ -169,6 +169,13 @@ int dtc_p2p_open(const char* handle, void** ptr) {
 }
 
 int dtc_p2p_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// Topology checks at P2P init (parallel/p2p.py): the PCI bus id identifies a GPU across processes
+// (device ordinals depend on each process's visible set); can-access-peer says whether a kernel on
+// `dev` can load `peer`'s memory directly (xGMI).
+int dtc_device_pci_bus_id(int dev, char* buf, int len) { return (int)hipDeviceGetPCIBusId(buf, len, dev); }
+int dtc_device_count(int* n) { return (int)hipGetDeviceCount(n); }
+int dtc_can_access_peer(int dev, int peer, int* ok) { return (int)hipDeviceCanAccessPeer(ok, dev, peer); }
 int dtc_p2p_free(void* ptr) { return (int)hipFree(ptr); }
 
 // out = sum over ranks of x (fp32, n % 4 == 0, n*4 <= half_bytes).  x and out may alias.

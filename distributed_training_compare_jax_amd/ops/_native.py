@@ -112,6 +112,9 @@ def _declare(lib):
         "dtc_p2p_alloc": ([l, vp, vp], i),
         "dtc_p2p_open": ([vp, vp], i),
         "dtc_p2p_close": ([vp], i),
+        "dtc_device_pci_bus_id": ([i, ctypes.c_char_p, i], i),
+        "dtc_device_count": ([ctypes.POINTER(c_int)], i),
+        "dtc_can_access_peer": ([i, i, ctypes.POINTER(c_int)], i),
         "dtc_p2p_free": ([vp], i),
         "dtc_p2p_allreduce": ([vp, vp, l, vp, i, i, l, vp, vp, vp], i),
         "dtc_embed_sort_bits": ([i], i),

@@ -26,6 +26,42 @@ import torch.distributed as dist
 from ..ops import _native as N
 
 
+def _pci_bus_id(L, dev: int) -> str:
+    buf = ctypes.create_string_buffer(64)
+    N.check(L.dtc_device_pci_bus_id(dev, buf, 64), "hipDeviceGetPCIBusId")
+    return buf.value.decode().lower()
+
+
+def check_peer_access(L, rank: int, dev: int, peers) -> dict:
+    """``peers``: [(rank, pci bus id)] of the group.  Every peer GPU must be reachable by direct
+    loads from this one (hipDeviceCanAccessPeer over xGMI); raises naming the rank and peer
+    otherwise — the P2P all-reduce never silently switches paths.  Peers on this same GPU (the
+    one-GPU multi-process tests) need no peer access.  Returns {peer rank: "self" | "xgmi" |
+    "not-visible"} (a peer GPU outside this process's visible set cannot be queried; its IPC
+    mapping below still has to succeed)."""
+    mine = _pci_bus_id(L, dev)
+    n = ctypes.c_int(0)
+    N.check(L.dtc_device_count(ctypes.byref(n)), "hipGetDeviceCount")
+    ordinal = {_pci_bus_id(L, d): d for d in range(n.value)}
+    out = {}
+    for p, bus in peers:
+        if p == rank:
+            continue
+        if bus == mine:
+            out[p] = "self"
+            continue
+        if bus not in ordinal:
+            out[p] = "not-visible"
+            continue
+        ok = ctypes.c_int(0)
+        N.check(L.dtc_can_access_peer(dev, ordinal[bus], ctypes.byref(ok)), "hipDeviceCanAccessPeer")
+        if not ok.value:
+            raise RuntimeError(f"P2P all-reduce: rank {rank} (GPU {dev}, {mine}) cannot access rank {p}'s GPU "
+                               f"({bus}) directly; use tp_comm: rccl")
+        out[p] = "xgmi"
+    return out
+
+
 class P2PAllReduce:
     def __init__(self, group, rank: int, world: int, device, max_bytes: int):
         assert 1 <= world <= 8, "P2P all-reduce supports up to 8 ranks (one xGMI hive)"
@@ -39,18 +75,23 @@ class P2PAllReduce:
         with torch.cuda.device(self.device):
             N.check(L.dtc_p2p_alloc(total, ctypes.addressof(ptr), ctypes.addressof(handle)), "dtc_p2p_alloc")
         self._own = ptr.value
-        handles = [None] * world
-        dist.all_gather_object(handles, bytes(handle.raw), group=group)
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        info = [None] * world
+        dist.all_gather_object(info, (bytes(handle.raw), _pci_bus_id(L, dev)), group=group)
+        self.peer_paths = check_peer_access(L, rank, dev, [(p, bus) for p, (_, bus) in enumerate(info)])
         bases = []
         self._opened = []
         with torch.cuda.device(self.device):
-            for p, h in enumerate(handles):
+            for p, (h, bus) in enumerate(info):
                 if p == rank:
                     bases.append(self._own)
                     continue
                 q = ctypes.c_void_p()
                 hb = ctypes.create_string_buffer(h, 64)
-                N.check(L.dtc_p2p_open(ctypes.addressof(hb), ctypes.addressof(q)), "dtc_p2p_open")
+                rc = L.dtc_p2p_open(ctypes.addressof(hb), ctypes.addressof(q))
+                if rc != 0:
+                    raise RuntimeError(f"P2P all-reduce: rank {rank} could not map rank {p}'s buffer (GPU {bus}): "
+                                       f"hipIpcOpenMemHandle error {rc}")
                 bases.append(q.value)
                 self._opened.append(q.value)
         self._bases = (ctypes.c_void_p * 8)(*(bases + [None] * (8 - world)))
