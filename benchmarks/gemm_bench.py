@@ -2,7 +2,7 @@
 other hot kernels, in TFLOP/s / TB/s.  torch.matmul (hipBLASLt) is timed on the same bf16 operands
 as a yardstick only — it is never used by the training path.
 
-    python benchmarks/gemm_bench.py [--reps 50] [--json out.json]
+    python benchmarks/gemm_bench.py [--reps 50] [--json out.json] [--model ref|gpt2-small|gpt2-medium]
 """
 import argparse
 import json
@@ -33,9 +33,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--model", default="ref")
     a = ap.parse_args()
     dev = torch.device("cuda")
-    M, D, F, V = 4096, 512, 2048, 50304
+    from distributed_training_compare_jax_amd.config.schema import model_config_from_preset
+
+    mc = model_config_from_preset(a.model)
+    M, D, F, V = 8 * mc.max_seq_len, mc.d_model, mc.d_ff, mc.padded_vocab
+    H, T = mc.n_heads, mc.max_seq_len
     r = lambda *s: (torch.randn(*s, device=dev) * 0.5).to(torch.bfloat16)  # noqa: E731
     rows = []
 
@@ -78,12 +83,12 @@ def main():
     # lm_head forward without the CE epilogue (isolates the epilogue cost)
     x, w = r(M, D), r(V, D) * 0.05
     rec(f"fwd  lm_head plain-epilogue [{M}x{V}x{D}]", timeit(lambda: G.linear(x, w, None), a.reps), 2 * M * V * D)
-    qkv = r(8, 512, 3 * D)
-    o, lse = A.attn_fwd(qkv, 16)
-    fl = A.attn_flops(8, 512, 16, 32)
-    rec("attn fwd  B8 T512 H16 hd32", timeit(lambda: A.attn_fwd(qkv, 16), a.reps), fl)
-    do = r(8, 512, D)
-    rec("attn bwd  B8 T512 H16 hd32", timeit(lambda: A.attn_bwd(qkv, o, lse, do, 16), a.reps), 2.5 * fl)
+    qkv = r(8, T, 3 * D)
+    o, lse = A.attn_fwd(qkv, H)
+    fl = A.attn_flops(8, T, H, D // H)
+    rec(f"attn fwd  B8 T{T} H{H} hd{D // H}", timeit(lambda: A.attn_fwd(qkv, H), a.reps), fl)
+    do = r(8, T, D)
+    rec(f"attn bwd  B8 T{T} H{H} hd{D // H}", timeit(lambda: A.attn_bwd(qkv, o, lse, do, H), a.reps), 2.5 * fl)
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(rows, fh, indent=1)

@@ -1260,7 +1260,8 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
   const int kbeg = z * a.kps;
   const int nk = min(a.kps, a.K - kbeg) / 64;
   // the dlogits stores + column sums of k-step kt go to n-tile kt % 2 (the two n-tiles share them)
-  const int nown = min(a.tiles_n, 2);
+  // no dlogits output (the weight gradient recomputes them, ce_wgrad256_kernel): nothing to own
+  const int nown = a.dlogits ? min(a.tiles_n, 2) : 0;
   auto owns = [&](int kt) { return tn_idx < nown && kt % nown == tn_idx; };
 
   // staging coordinates: rows q*64 + srow (q = 0..3), 16-B chunk schunk of the 64-wide k-step,
@@ -1373,6 +1374,144 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
       const int m = m0 + wm * 128 + j * 16 + (lane & 15);
       const int n = n0 + wn * 64 + i * 16 + g4;
       if (m < a.M && n < a.N) *(f32x4*)(sl + (long)m * a.N + n) = acc[i][j];
+    }
+}
+
+// ============================================================================================
+// lm_head WEIGHT gradient with the cross-entropy backward fused into its A operand:
+//   dW[v][d] = beta*dW[v][d] + sum_t dlogits[t][v] * h[t][d]      (TN: both operands token-major)
+//   db[v]    = beta*db[v]    + sum_t dlogits[t][v]                 (fp32, summed before any rounding)
+// dlogits is never stored: each block recomputes its [64 tokens][256 vocab] slice of it from the bf16
+// logits on the way into the LDS image (ce_grad8, the same bits ce_dgrad256 / ce_bwd produce), so
+// the lm_head backward reads the logits twice (dgrad, wgrad) and writes nothing of size tokens x
+// vocab (round 2 wrote and re-read 412 / 824 MB of dlogits per step).  The A image is the MN-major
+// [64 k][256 m] layout of dma_tile<false> (16-B chunk c of k-row r at c ^ mn_swz(r)), so the MFMA
+// fragment reads are the verified big_frag<false> ones; h (B) still streams by LDS DMA.  Each
+// thread stages the SAME 8 vocab columns for every k-row (columns tid % 32), so the bias gradient is
+// 8 register sums per thread + one fixed-order LDS combine at the end (n-tile 0 blocks write it).
+struct CeWgradArgs {
+  const bf16* logits; long ldl;   // [tokens][V] bf16 (A, m = vocab, k = token)
+  const float* lse; const int* labels; int vocab_start, n_valid; float scale;
+  const bf16* h; long ldh;        // [tokens][D] bf16 (B, n = d, k = token)
+  float* dw; long lddw;           // [V][D] fp32
+  float* db;                      // [V] fp32 (or null)
+  float beta;
+  int M, N, K, tiles_m, tiles_n, gm;  // M = V, N = D, K = tokens
+};
+
+__global__ void __launch_bounds__(NT2, 1) ce_wgrad256_kernel(CeWgradArgs a) {
+  constexpr int TM = 8, TN = 4;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = a.tiles_m * a.tiles_n;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int grp = tile / (a.gm * a.tiles_n), in_g = tile % (a.gm * a.tiles_n);
+  const int gm_eff = min(a.gm, a.tiles_m - grp * a.gm);
+  const int tm_idx = grp * a.gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
+  const int nk = a.K / 64;
+
+  // staging: 8 vocab columns v0 = m0 + 8*cc of k-rows kr0 + 16q (q = 0..3) of each 64-token k-step
+  const int cc = tid & 31, kr0 = tid >> 5;
+  const int v0 = m0 + cc * 8;
+  const int vload = min(v0, a.M - 8);  // ragged vocab edge: clamped (those columns are never stored)
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  u32x4 R[4];
+  float cr[4];
+  int lab[4];
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int t = k0 + kr0 + 16 * q;
+      R[q] = *(const u32x4*)(a.logits + (long)t * a.ldl + vload);
+      cr[q] = a.lse[t];
+      lab[q] = a.labels[t];
+    }
+  };
+  auto put_a = [&](bf16* img) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float g[8];
+      ce_grad8(__builtin_bit_cast(bf16x8, R[q]), v0, ce_row_c(cr[q], a.scale), lab[q] - a.vocab_start, a.n_valid,
+               a.scale, g);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += g[e];
+        o[e] = f2bf(g[e]);
+      }
+      const int kr = kr0 + 16 * q;
+      *(bf16x8*)(img + kr * 256 + ((cc ^ mn_swz(kr)) << 3)) = o;
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  dma_tile<false>(a.h, a.ldh, n0, a.N, 0, smem + IMG, wave, lane);
+  if (nk > 0) {
+    load_a(0);
+    put_a(smem);
+  }
+  if (nk > 1) load_a(64);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16* sA = smem + (kt & 1) * 2 * IMG;
+    const bf16* sB = sA + IMG;
+    bf16* nA = smem + ((kt + 1) & 1) * 2 * IMG;
+    const bool more = kt + 1 < nk, more2 = kt + 2 < nk;
+    if (more) {
+      dma_tile<false>(a.h, a.ldh, n0, a.N, (kt + 1) * 64, nA + IMG, wave, lane);
+      put_a(nA);
+    }
+    if (more2) load_a((kt + 2) * 64);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = big_frag<false>(sA, wm * 8 + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = big_frag<false>(sB, wn * 4 + i, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    // the k+2 loads (12 ops, issued after this k-step's DMA) may stay in flight across the barrier
+    if (more2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // bias gradient: the 16 threads of column group cc combine in a fixed order (n-tile 0 writes)
+  if (a.db && tn_idx == 0) {
+    float* red = (float*)smem;  // the main-loop buffers are free after the last barrier
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[kr0 * 256 + cc * 8 + e] = cs[e];
+    __syncthreads();
+    if (tid < 256 && m0 + tid < a.M) {
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += red[r * 256 + tid];
+      float* d = a.db + m0 + tid;
+      *d = (a.beta != 0.f ? a.beta * *d : 0.f) + s;
+    }
+  }
+  Epi e{};
+  e.M = a.M; e.N = a.N; e.C = a.dw; e.ldc = a.lddw; e.alpha = 1.f; e.beta = a.beta;
+  const int g4 = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+      const int n = n0 + wn * 64 + i * 16 + g4;
+      if (m < a.M && n < a.N) epilogue_store<EPI_STORE, true>(e, m, n, acc[i][j]);
     }
 }
 
@@ -2171,6 +2310,26 @@ int dtc_ce_dgrad(const bf16* logits, long ldl, const float* lse, const int* labe
   const long MN = (long)M * N;
   hipLaunchKernelGGL(splitk_reduce, dim3((int)((MN / 4 + 255) / 256)), dim3(256), 0, st, (const float*)ws, split, MN,
                      dx, (long)N, N, 0.f);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// lm_head weight + bias gradient from the logits (ce_wgrad256_kernel): dw [V][D] fp32 (ldw), db [V] fp32
+// (optional), both = beta*old + new.  Token count K % 64 == 0, D % 8 == 0, V % 8 == 0.
+int dtc_ce_wgrad(const bf16* logits, long ldl, const float* lse, const int* labels, int vocab_start, int n_valid,
+                 float scale, const bf16* h, long ldh, float* dw, long lddw, float* db, float beta, int V, int D,
+                 int tokens, hipStream_t st) {
+  if (tokens % 64 || D % 8 || V % 8 || ldl % 8 || ldh % 8 || lddw % 4 || V < 8) return 1310;
+  CeWgradArgs a;
+  a.logits = logits; a.ldl = ldl; a.lse = lse; a.labels = labels; a.vocab_start = vocab_start; a.n_valid = n_valid;
+  a.scale = scale; a.h = h; a.ldh = ldh; a.dw = dw; a.lddw = lddw; a.db = db; a.beta = beta;
+  a.M = V; a.N = D; a.K = tokens;
+  a.tiles_m = (V + BIG - 1) / BIG;
+  a.tiles_n = (D + BIG - 1) / BIG;
+  const int ntiles = a.tiles_m * a.tiles_n;
+  a.gm = a.tiles_m;
+  if (a.tiles_n <= 16) a.gm = std::max(1, std::min(a.tiles_m, (ntiles / 8 + a.tiles_n - 1) / a.tiles_n));
+  hipLaunchKernelGGL(ce_wgrad256_kernel, dim3(ntiles), dim3(NT2), 0, st, a);
   DTC_CHECK_LAUNCH();
   return 0;
 }

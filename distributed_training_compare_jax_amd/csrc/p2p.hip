@@ -37,10 +37,12 @@ struct PeerTable {
 
 __device__ __forceinline__ uint64_t wall_clock() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
+// inc: 1 per barrier of the two-shot call (2 barriers), 2 for the one-shot call's single barrier, so
+// every call advances the epoch by 2 and the buffer half stays (epoch >> 1) & 1 at the call's start
 __global__ void p2p_barrier_kernel(PeerTable t, int rank, int world, uint32_t* __restrict__ epoch,
-                                   int* __restrict__ err) {
+                                   int* __restrict__ err, int inc) {
   const int p = threadIdx.x;
-  const uint32_t e = epoch[0] + 1;
+  const uint32_t e = epoch[0] + inc;
   __threadfence_system();  // this rank's prior writes (its buffer half) before the signal
   if (p < world && p != rank) {
     uint32_t* peer_flag = (uint32_t*)t.base[p] + rank;
@@ -88,6 +90,21 @@ __global__ void p2p_all_gather_kernel(PeerTable t, int world, long n4, long half
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const int q = (int)(i / chunk);
     out[i] = ((const f32x4*)(t.base[q] + off))[i];
+  }
+}
+
+// one-shot (small messages): after the single barrier every rank sums ALL ranks' halves itself, in
+// rank order (identical result on every rank); (W-1) n bytes over xGMI instead of 2 (W-1)/W n, but
+// one barrier and two fewer launches: the latency path for the CE row statistics, label logits and
+// the grad-norm scalar
+__global__ void p2p_oneshot_kernel(PeerTable t, int world, long n4, long half_bytes, f32x4* __restrict__ out,
+                                   const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 2) >> 1) & 1;
+  const long off = FLAG_BYTES + h * half_bytes;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    f32x4 s = ((const f32x4*)(t.base[0] + off))[i];
+    for (int p = 1; p < world; ++p) s += ((const f32x4*)(t.base[p] + off))[i];
+    out[i] = s;
   }
 }
 
@@ -179,22 +196,33 @@ int dtc_can_access_peer(int dev, int peer, int* ok) { return (int)hipDeviceCanAc
 int dtc_p2p_free(void* ptr) { return (int)hipFree(ptr); }
 
 // out = sum over ranks of x (fp32, n % 4 == 0, n*4 <= half_bytes).  x and out may alias.
+// mode: 0 auto (one-shot up to P2P_ONESHOT_BYTES), 1 two-shot, 2 one-shot.
+constexpr long P2P_ONESHOT_BYTES = 512 * 1024;
 int dtc_p2p_allreduce(const float* x, float* out, long n, void* const* bases, int rank, int world, long half_bytes,
-                      uint32_t* epoch, int* err, hipStream_t st) {
+                      uint32_t* epoch, int* err, int mode, hipStream_t st) {
   if (world < 1 || world > P2P_MAX || n % 4 || n * 4 > half_bytes) return 4001;
   PeerTable t;
   for (int p = 0; p < P2P_MAX; ++p) t.base[p] = (unsigned char*)(p < world ? bases[p] : nullptr);
   const long n4 = n / 4;
   const int blocks = (int)std::min(1024L, std::max(1L, (n4 + 255) / 256));
+  const bool one = mode == 2 || (mode == 0 && n * 4 <= P2P_ONESHOT_BYTES);
   hipLaunchKernelGGL(p2p_stage_kernel, dim3(blocks), dim3(256), 0, st, (const f32x4*)x, t, rank, n4, half_bytes, epoch);
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err);
+  if (one) {
+    hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 2);
+    DTC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(p2p_oneshot_kernel, dim3(blocks), dim3(256), 0, st, t, world, n4, half_bytes, (f32x4*)out,
+                       epoch);
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 1);
   DTC_CHECK_LAUNCH();
   const int rs_blocks = (int)std::min(1024L, std::max(1L, (n4 / world + 255) / 256));
   hipLaunchKernelGGL(p2p_reduce_scatter_kernel, dim3(rs_blocks), dim3(256), 0, st, t, rank, world, n4, half_bytes,
                      epoch);
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err);
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 1);
   DTC_CHECK_LAUNCH();
   hipLaunchKernelGGL(p2p_all_gather_kernel, dim3(blocks), dim3(256), 0, st, t, world, n4, half_bytes, (f32x4*)out,
                      epoch);

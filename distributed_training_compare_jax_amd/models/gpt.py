@@ -45,6 +45,12 @@ _LMHEAD_WGRAD_MAIN = _os.environ.get("DTC_LMHEAD_WGRAD", "side") == "main"
 # this layer's dgrad GEMMs; 0 = one fork per layer after its dgrad chain
 _SIDE_INTERLEAVE = _os.environ.get("DTC_SIDE_INTERLEAVE", "0") == "1"  # measured: 1 is slower
 _CE_FUSED = _os.environ.get("DTC_CE_FUSED", "1") == "1"  # ops/xent.py ce_dgrad_fused
+# lm_head weight/bias gradients recomputing dlogits from the logits (ops/xent.py ce_wgrad_fused): no
+# tokens x vocab dlogits tensor is written or read (-1.6 GB of HBM traffic per GPT-2 small step) and
+# the bias gradient is summed from fp32 values.  Off by default: the recompute (a second exp pass,
+# register-staged instead of DMA-staged operand) measured 14.57 vs 14.48 ms (GPT-2 small) and 4.73 vs
+# 4.70 ms (reference model), profiles/r3_ab_ce_wgrad.log
+_CE_WGRAD = _os.environ.get("DTC_CE_WGRAD", "0") == "1"
 
 
 class NoComm:
@@ -402,24 +408,34 @@ class GPTStage:
         f = self.flat
         x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
         wt = f.wt("lm_head.w")  # transposed mirror: NT split-K dgrad, both operands K-major
-        if wt is not None and _CE_FUSED and logits.is_cuda:
-            # CE backward fused into the dgrad's operand staging (no separate 824 MB dlogits pass)
-            dyf, dlogits, colp = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt)
-        else:
-            # one pass: dlogits in place + column partials of it (the bias gradient's input)
-            dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale,
-                                                  colpart=True)
-            # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
-            # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
-            dyf = (G.linear_resid(dlogits, wt, None, None) if wt is not None
-                   else G.matmul_nn(dlogits, f.w("lm_head.w")))
         red = self.red
-        wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
-                                                G.colsum(cp, f.g("lm_head.b"), beta, red=red))
+        if wt is not None and _CE_FUSED and logits.is_cuda and _CE_WGRAD and lab.shape[0] % 64 == 0:
+            # dx from the fused CE + dgrad kernel; dW / db from the fused CE + weight-gradient kernel:
+            # the logits are read twice, no dlogits anywhere
+            dyf, dlogits, _ = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt,
+                                               want_dlogits=False)
+            wg = lambda lg=logits, ls=lse, lb=lab, y=yf: X.ce_wgrad_fused(
+                lg, ls, lb, self.v_start, self.v_valid, grad_scale, y, f.g("lm_head.w"), f.g("lm_head.b"), beta)
+            keep = (logits, lse, lab, yf)
+        else:
+            if wt is not None and _CE_FUSED and logits.is_cuda:
+                # CE backward fused into the dgrad's operand staging (no separate dlogits pass)
+                dyf, dlogits, colp = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt)
+            else:
+                # one pass: dlogits in place + column partials of it (the bias gradient's input)
+                dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale,
+                                                      colpart=True)
+                # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
+                # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
+                dyf = (G.linear_resid(dlogits, wt, None, None) if wt is not None
+                       else G.matmul_nn(dlogits, f.w("lm_head.w")))
+            wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
+                                                    G.colsum(cp, f.g("lm_head.b"), beta, red=red))
+            keep = (dlogits, yf, colp)
         if _LMHEAD_WGRAD_MAIN:
             wg()
         else:
-            self.side.defer(wg, dlogits, yf, colp)
+            self.side.defer(wg, *keep)
         del logits, dlogits
         self.tp.all_reduce_(dyf)
         last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None

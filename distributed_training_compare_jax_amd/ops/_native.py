@@ -116,7 +116,7 @@ def _declare(lib):
         "dtc_device_count": ([ctypes.POINTER(c_int)], i),
         "dtc_can_access_peer": ([i, i, ctypes.POINTER(c_int)], i),
         "dtc_p2p_free": ([vp], i),
-        "dtc_p2p_allreduce": ([vp, vp, l, vp, i, i, l, vp, vp, vp], i),
+        "dtc_p2p_allreduce": ([vp, vp, l, vp, i, i, l, vp, vp, i, vp], i),
         "dtc_embed_sort_bits": ([i], i),
         "dtc_embed_sort": ([vp, i, i, vp, vp], i),
         "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),
@@ -139,6 +139,7 @@ def _declare(lib):
         "dtc_ce_dgrad": ([vp, l, vp, vp, i, i, f, vp, l, vp, l, vp, vp, i, i, i, vp, l, vp], i),
         "dtc_ce_dgrad_workspace_bytes": ([i, i, i], l),
         "dtc_ce_dgrad_colpart_rows": ([i], i),
+        "dtc_ce_wgrad": ([vp, l, vp, vp, i, i, f, vp, l, vp, l, vp, f, i, i, i, vp], i),
         # exact-fp32 parity path (csrc/gemm_f32.hip, csrc/attention_f32.hip)
         "dtc_gemm_f32": ([ctypes.POINTER(GemmArgs), vp], i),
         "dtc_gemm_f32_workspace_bytes": ([i, i, i, i], l),

@@ -14,6 +14,10 @@ bitwise identical.  RCCL remains the path for anything else (scalars, non-fp32, 
 Handles are exchanged once over the process group (``all_gather_object``), so the same code runs
 on a real node (RCCL group) and in the one-GPU multi-process tests (gloo group, all ranks on one
 device — IPC within a device works the same way).
+
+Small messages (the vocab-parallel CE row statistics and label logits, the grad-norm scalar) take a
+one-shot variant (one barrier; every rank sums all peers' buffers itself), so a TP step issues no
+RCCL call at all: :class:`parallel.tp.TPComm` gathers by summing zero-padded slots.
 """
 
 from __future__ import annotations
@@ -106,9 +110,12 @@ class P2PAllReduce:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
                 and t.numel() * 4 <= self.half)
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce_(self, t: torch.Tensor, mode: int = 0) -> torch.Tensor:
+        """In-place sum over the group.  mode 0: one-shot (one barrier, every rank reads every peer)
+        up to 512 KB, two-shot (reduce-scatter + all-gather, 2 (W-1)/W of the bytes per rank) above;
+        1 / 2 force two-shot / one-shot."""
         N.check(N.lib().dtc_p2p_allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._bases_ptr, self.rank, self.world,
-                                          self.half, self.epoch.data_ptr(), self.err.data_ptr(),
+                                          self.half, self.epoch.data_ptr(), self.err.data_ptr(), int(mode),
                                           N.stream_ptr(t.device)), "dtc_p2p_allreduce")
         return t
 

@@ -33,14 +33,36 @@ class TPComm:
             return t
         if self.p2p is not None and self.p2p.supports(t):
             return self.p2p.all_reduce_(t)
+        if self.p2p is not None and t.dtype == torch.float32 and t.numel() < 4 and t.is_contiguous():
+            # a scalar (the grad-norm partial): through a zero-padded 4-float buffer, in-graph
+            from ..ops.optim import fill_
+
+            if not hasattr(self, "_pad4"):
+                self._pad4 = torch.zeros(4, dtype=torch.float32, device=t.device)
+            fill_(self._pad4, 0.0)
+            self._pad4[:t.numel()].copy_(t.view(-1))
+            self.p2p.all_reduce_(self._pad4)
+            t.view(-1).copy_(self._pad4[:t.numel()])
+            return t
         g = self.group
         self.program.comm(lambda: dist.all_reduce(t, group=g))
         return t
 
     def all_gather_stack(self, t: torch.Tensor) -> torch.Tensor:
-        """[...] → [size, ...] (shard-major)."""
+        """[...] → [size, ...] (shard-major).  With the P2P path: every rank writes its slot of a
+        zeroed [size, ...] buffer and the buffer is summed (x + 0 = x exactly, so it IS the gather),
+        in-graph, no RCCL call."""
         if self.size == 1:
             return t.unsqueeze(0)
+        if self.p2p is not None and t.dtype == torch.float32 and (t.numel() * self.size) % 4 == 0 \
+                and t.numel() * self.size * 4 <= self.p2p.half:
+            from ..ops.optim import fill_
+
+            out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            fill_(out, 0.0)
+            out[self.rank].copy_(t)
+            self.p2p.all_reduce_(out.view(-1))
+            return out
         out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         outs = list(out.unbind(0))
         g = self.group

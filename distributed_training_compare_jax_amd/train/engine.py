@@ -113,6 +113,8 @@ class Engine:
             self.opt = FusedAdamW(self.flat, opt_cfg, self.program, tp, m.tp_group, m.pp_group,
                                   pp_global_clip=(train_cfg.pp_clip == "global"))
         self.opt.reducer = self.stage.red
+        if not self.zero:
+            self.opt.tp_comm = self.tp_comm
         if pp == 1 and not self.zero:
             # incremental Σg²: with dp == 1 each layer's grads are final when its backward ends
             # (norm chunk per layer, reduced on the side stream); with dp > 1 only the locally

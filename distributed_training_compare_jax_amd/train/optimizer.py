@@ -55,6 +55,7 @@ class FusedAdamW:
         self.chunks = []  # incremental-norm chunks: [segments, lo, hi, partial view, reducer tasks]
         self._done = []
         self.reducer = None  # GradReducer of the model stage (single-stream GPU backward)
+        self.tp_comm = None  # parallel.tp.TPComm: the TP norm partial through its P2P path when it has one
 
     # -- incremental global norm ------------------------------------------------------
     def set_chunks(self, cuts, elems_per_block: int = 16384):
@@ -123,9 +124,12 @@ class FusedAdamW:
                 red.flush_all()  # grads must be final
             O.sumsq_segments(f.grads, self.segments, self.sumsq, step=self.step_t)
         if self.tp_size > 1:
-            g = self.tp_group
-            s = self.sumsq
-            self.program.comm(lambda: dist.all_reduce(s, group=g))
+            if self.tp_comm is not None and self.tp_comm.p2p is not None:
+                self.tp_comm.all_reduce_(self.sumsq)  # in-graph one-shot (no graph cut)
+            else:
+                g = self.tp_group
+                s = self.sumsq
+                self.program.comm(lambda: dist.all_reduce(s, group=g))
         if self.pp_group is not None:
             g = self.pp_group
             s = self.sumsq
