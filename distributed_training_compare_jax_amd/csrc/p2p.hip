@@ -196,8 +196,15 @@ int dtc_can_access_peer(int dev, int peer, int* ok) { return (int)hipDeviceCanAc
 int dtc_p2p_free(void* ptr) { return (int)hipFree(ptr); }
 
 // out = sum over ranks of x (fp32, n % 4 == 0, n*4 <= half_bytes).  x and out may alias.
-// mode: 0 auto (one-shot up to P2P_ONESHOT_BYTES), 1 two-shot, 2 one-shot.
+// mode: 0 auto, 1 two-shot, 2 one-shot.  Per link, one-shot moves n bytes (each rank reads every peer
+// once over that peer's link) and two-shot 2n/W, for one barrier fewer: at W = 2 the bytes are equal
+// and one-shot always wins; at W = 4 / 8 it wins up to ~1 MB / 512 KB (a barrier round trip is a few
+// us, a link ~150 GB/s).  Measured with 2 ranks on one device (benchmarks/p2p_bench.py): one-shot
+// 6.5 / 7.5 / 11.9 / 16.9 us vs two-shot 11.2 (512 KB) / 12.3 / 18.5 / 22.8 us at 64 KB / 1 / 4 / 8 MB.
 constexpr long P2P_ONESHOT_BYTES = 512 * 1024;
+inline bool oneshot_auto(long bytes, int world) {
+  return world <= 2 || bytes <= P2P_ONESHOT_BYTES * (world <= 4 ? 2 : 1);
+}
 int dtc_p2p_allreduce(const float* x, float* out, long n, void* const* bases, int rank, int world, long half_bytes,
                       uint32_t* epoch, int* err, int mode, hipStream_t st) {
   if (world < 1 || world > P2P_MAX || n % 4 || n * 4 > half_bytes) return 4001;
@@ -205,7 +212,7 @@ int dtc_p2p_allreduce(const float* x, float* out, long n, void* const* bases, in
   for (int p = 0; p < P2P_MAX; ++p) t.base[p] = (unsigned char*)(p < world ? bases[p] : nullptr);
   const long n4 = n / 4;
   const int blocks = (int)std::min(1024L, std::max(1L, (n4 + 255) / 256));
-  const bool one = mode == 2 || (mode == 0 && n * 4 <= P2P_ONESHOT_BYTES);
+  const bool one = mode == 2 || (mode == 0 && oneshot_auto(n * 4, world));
   hipLaunchKernelGGL(p2p_stage_kernel, dim3(blocks), dim3(256), 0, st, (const f32x4*)x, t, rank, n4, half_bytes, epoch);
   DTC_CHECK_LAUNCH();
   if (one) {

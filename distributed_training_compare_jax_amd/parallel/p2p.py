@@ -111,9 +111,9 @@ class P2PAllReduce:
                 and t.numel() * 4 <= self.half)
 
     def all_reduce_(self, t: torch.Tensor, mode: int = 0) -> torch.Tensor:
-        """In-place sum over the group.  mode 0: one-shot (one barrier, every rank reads every peer)
-        up to 512 KB, two-shot (reduce-scatter + all-gather, 2 (W-1)/W of the bytes per rank) above;
-        1 / 2 force two-shot / one-shot."""
+        """In-place sum over the group.  mode 0: one-shot (one barrier, every rank reads every peer) at
+        W = 2 and for small messages (<= 1 MB at W <= 4, 512 KB at W = 8), else two-shot (reduce-scatter
+        + all-gather, 2 (W-1)/W of the bytes per rank); 1 / 2 force two-shot / one-shot."""
         N.check(N.lib().dtc_p2p_allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._bases_ptr, self.rank, self.world,
                                           self.half, self.epoch.data_ptr(), self.err.data_ptr(), int(mode),
                                           N.stream_ptr(t.device)), "dtc_p2p_allreduce")
