@@ -2078,7 +2078,11 @@ int big_split(int layout, int M, int N, int K) {
   static const int min_tiles = [] { const char* v = getenv("DTC_BIG_MIN_TILES"); return v ? atoi(v) : 512; }();
   const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
   if (layout == 2) return (t >= 256 && K >= 1024) ? 1 : 0;
-  if (K < 16384) return t >= min_tiles ? 1 : 0;   // ordinary K: whole tiles
+  // ordinary K: whole tiles, when there are enough of them, or when the last round of 256^2 tiles is
+  // nearly empty anyway (GPT-2 small qkv forward: 288 tiles = 1.125 rounds, 54.7 -> 47.7 us;
+  // fc1's 384 = 1.5 rounds stays on the 128^2 kernel: 76 vs 85 us, profiles/r3_gemm_bench_gpt2s*.log)
+  static const int tail_ok = [] { const char* v = getenv("DTC_BIG_TAIL"); return v ? atoi(v) : 64; }();
+  if (K < 16384) return (t >= min_tiles || (layout == 0 && t >= 256 && t % 256 <= tail_ok)) ? 1 : 0;
   if (t > 256) return 0;                           // dgrad through the vocab (NN, or NT on W^T): split-K
   int split = (int)std::max(1L, 256 / t);
   while (split > 1 && (K / 64) / split < 8) --split;
@@ -2196,7 +2200,8 @@ WPlan dmaw_plan(int layout, int M, int N, int K, int epi, bool f32, bool has_col
     else if ((mode & 4) && epi == EPI_STORE && f32 && K <= 4096 && tiles(128, 64) >= 192 && tiles(128, 64) <= 512)
       w.cfg = W_128x64;
   } else if (layout == 2 && epi == EPI_STORE && f32 && !has_colsum && tiles(128, 128) <= 256 &&
-             (all || tiles(128, 128) < 32)) {
+             (all || tiles(128, 128) <= 48)) {
+    // (<= 48 tiles: also GPT-2's [768 x 768] out_proj weight gradient, 53.4 -> 38.3 us)
     // weight gradient (K = tokens): split-K towards 256 blocks of >= 8 k-steps
     const int nk = K / 64;
     const int cfg = tiles(128, 128) >= 32 ? W_128x128 : W_64x128;
