@@ -34,11 +34,36 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+# HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), in
+# order: two streams on one queue execute as one.  A multi-rank step has more streams than that (the
+# step stream, the side stream, every communicator's RCCL stream, gloo's copy streams) and kernels
+# that wait on OTHER processes (RCCL's, the P2P all-reduce barrier): a barrier queued ahead of an
+# unrelated collective on a shared queue blocks that collective, and across ranks this closes a
+# cycle.  Measured: dp2 x tp2 with the P2P all-reduce on one GPU timed out at the default 4 queues
+# and passes at 16 (profiles/r3_hw_queues.log).  So every multi-rank GPU process gets >= 16 queues.
+MIN_HW_QUEUES = 16
+
+
+def _ensure_hw_queues():
+    cur = os.environ.get("GPU_MAX_HW_QUEUES")
+    if cur is not None and cur.isdigit() and int(cur) >= MIN_HW_QUEUES:
+        return
+    if torch.cuda.is_initialized():
+        import warnings
+
+        warnings.warn(f"HIP was initialised before init_distributed: GPU_MAX_HW_QUEUES={cur} stays in effect "
+                      f"(multi-rank steps want >= {MIN_HW_QUEUES}; set it in the launcher's environment)")
+        return
+    os.environ["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
+
+
 def init_distributed(device: str = "auto", timeout_s: float = 600.0) -> DistInfo:
     """Initialise (or reuse) the default process group from the environment."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world > 1 and device != "cpu":
+        _ensure_hw_queues()  # before the first HIP call of this process
     use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
     if use_cuda:
         ndev = torch.cuda.device_count()

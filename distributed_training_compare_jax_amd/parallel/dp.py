@@ -20,6 +20,7 @@ from typing import List, Tuple
 import torch.distributed as dist
 
 from .buffers import FlatParams
+from .program import csig
 
 
 class GradBuckets:
@@ -111,7 +112,8 @@ class GradBuckets:
         a, b = self.buckets[i]
         view = self.flat.grads[a:b]
         g = self.group
-        self.program.comm(lambda: dist.all_reduce(view, group=g, async_op=True), name=f"dp_bucket{i}")
+        self.program.comm(lambda: dist.all_reduce(view, group=g, async_op=True), name=f"dp_bucket{i}",
+                          sig=csig("all_reduce", g, view))
         self.issued[i] = True
 
     def wait_all(self):

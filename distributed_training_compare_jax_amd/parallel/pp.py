@@ -37,6 +37,7 @@ import torch.distributed as dist
 
 from ..ops.optim import cast_to_bf16, fill_
 from .dist import staged_p2p
+from .program import psig
 
 # ------------------------------------------------------------------------------ static programs
 # items: ("F", i) / ("B", i)                         compute of microbatch i
@@ -287,7 +288,13 @@ def run_pipeline(eng) -> None:
                         else:
                             prog._wait(n)
 
-        prog.comm(fn)
+        sig = []
+        for st_ in steps:
+            if st_[0] == "post":
+                _, _, peer, snd, rcv = st_
+                rank = m.pp_next if peer > 0 else m.pp_prev
+                sig += [x for t in snd for x in psig("send", rank, t)] + [x for t in rcv for x in psig("recv", rank, t)]
+        prog.comm(fn, sig=sig)
 
     items = pp_program(eng.tcfg.pp_schedule, S, s, M)
     dx_out: Dict[int, torch.Tensor] = {}

@@ -11,9 +11,16 @@ same stream order, which
 * keeps PP send/recv and TP all-reduces on the well-trodden eager RCCL path.
 
 ``record(step_fn)`` runs ``step_fn`` once with capture on; every ``comm(fn)`` call the
-step makes cuts the current graph, runs the collective for real (on whatever stale data
-the buffers hold — the recording pass computes nothing) and opens the next graph.
-``replay()`` then issues [graph, comm, graph, comm, ...] with one host call each.  With
+step makes cuts the current graph, stores ``fn`` WITHOUT running it (the recording pass
+computes nothing, so a collective there would only move stale bytes and add a step of RCCL
+traffic that the replays do not have) and opens the next graph.
+``replay()`` then issues [graph, comm, graph, comm, ...] with one host call each.
+
+Every collective also carries a signature (op, group ranks, tensor shapes/dtypes; for p2p the
+peer and direction).  The first eager step and the recorded step gather every rank's list and
+:func:`check_collective_sequences` proves that each group's members issue the same sequence and
+that each send has the matching receive, in order — a mismatch (the classic hang of a rank-dependent
+branch, or a PP schedule whose two sides disagree) raises on every rank instead of deadlocking.  With
 ``mode="eager"`` the same step code just executes (CPU/gloo path, first warmup steps).
 All segments share one memory pool and are replayed in capture order, so activations
 produced in one segment and consumed in a later one stay valid.
@@ -25,6 +32,71 @@ import time
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import torch
+
+
+_RANKS: Dict[int, Tuple[int, ...]] = {}
+
+
+def _group_ranks(group) -> Tuple[int, ...]:
+    import torch.distributed as dist
+
+    if not dist.is_initialized():  # nothing to check against (unit tests drive the code single-process)
+        return ()
+    key = id(group)
+    if key not in _RANKS:
+        g = group if group is not None else dist.group.WORLD
+        _RANKS[key] = tuple(dist.get_process_group_ranks(g))
+    return _RANKS[key]
+
+
+def _meta(t) -> Tuple:
+    return tuple(t.shape), str(t.dtype).replace("torch.", "")
+
+
+def csig(op: str, group, *tensors) -> List[Tuple]:
+    """Signature of one collective on ``group`` (the tensors that define its message size)."""
+    return [("coll", op, _group_ranks(group), tuple(_meta(t) for t in tensors))]
+
+
+def psig(direction: str, peer: int, t) -> List[Tuple]:
+    """Signature of one point-to-point transfer (``direction`` = "send" | "recv", ``peer`` = global rank)."""
+    return [(direction, int(peer), _meta(t))]
+
+
+def check_collective_sequences(per_rank: List[List[Tuple]]) -> Optional[str]:
+    """``per_rank[r]`` = rank r's collective signatures in issue order.  Returns None when every
+    group's members issue identical sequences and every send (a -> b) sequence equals b's receive
+    (from a) sequence, else a message naming the first disagreement."""
+    colls: Dict[Tuple[int, ...], Dict[int, List]] = {}
+    p2p: Dict[Tuple[int, int], Tuple[List, List]] = {}
+    for r, seq in enumerate(per_rank):
+        for e in seq:
+            if e[0] == "coll":
+                _, op, ranks, meta = e
+                ranks = tuple(ranks)
+                if r not in ranks:
+                    return f"rank {r} issued {op} on group {ranks}, of which it is not a member"
+                colls.setdefault(ranks, {}).setdefault(r, []).append((op, tuple(meta)))
+            else:
+                d, peer, meta = e
+                key = (r, peer) if d == "send" else (peer, r)
+                p2p.setdefault(key, ([], []))[0 if d == "send" else 1].append(tuple(meta))
+    for ranks, by in sorted(colls.items()):
+        ref = by.get(ranks[0], [])
+        for r in ranks[1:]:
+            seq = by.get(r, [])
+            if seq != ref:
+                k = next((i for i, (a, b) in enumerate(zip(ref, seq)) if a != b), min(len(ref), len(seq)))
+                a = ref[k] if k < len(ref) else "nothing"
+                b = seq[k] if k < len(seq) else "nothing"
+                return (f"group {ranks}: collective #{k} is {a} on rank {ranks[0]} but {b} on rank {r} "
+                        f"({len(ref)} vs {len(seq)} collectives per step)")
+    for (a, b), (snd, rcv) in sorted(p2p.items()):
+        if snd != rcv:
+            k = next((i for i, (x, y) in enumerate(zip(snd, rcv)) if x != y), min(len(snd), len(rcv)))
+            return (f"p2p {a} -> {b}: transfer #{k} sends {snd[k] if k < len(snd) else 'nothing'} but "
+                    f"receives {rcv[k] if k < len(rcv) else 'nothing'} ({len(snd)} sends, {len(rcv)} receives)")
+    return None
 
 
 class StepProgram:
@@ -48,6 +120,8 @@ class StepProgram:
         self.time_comms = False
         self.step_comms = 0
         self._ev: List[List[Any]] = []  # per step (FIFO): [(start, end) event pairs | host ms floats]
+        # collective signatures of the step being collected (None = not collecting)
+        self.sigs: Optional[List[Tuple]] = None
 
     def begin_step(self):
         self.step_comms = 0
@@ -87,18 +161,18 @@ class StepProgram:
         return ms
 
     # -------------------------------------------------------------- step-code API
-    def comm(self, fn: Callable[[], Any], name: Optional[str] = None):
-        """Issue a collective.  ``fn`` may return an async Work handle, retrievable by ``wait(name)``."""
+    def comm(self, fn: Callable[[], Any], name: Optional[str] = None, sig: Optional[List[Tuple]] = None):
+        """Issue a collective.  ``fn`` may return an async Work handle, retrievable by ``wait(name)``;
+        ``sig`` (:func:`csig` / :func:`psig` entries) describes what it moves, for the cross-rank check."""
         for h in self.before_comm:
             h()
+        if self.sigs is not None and sig:
+            self.sigs.extend(sig)
         if self.recording:
             self._cut()
             self.items.append(("comm", fn, name))
-            res = fn()
-            if name is not None:
-                self._handles[name] = res
             self._begin()
-            return res
+            return None
         res = self._timed(fn)
         if name is not None:
             self._handles[name] = res
@@ -114,6 +188,23 @@ class StepProgram:
             self._begin()
         else:
             self._timed(lambda: self._wait(name))
+
+    # -------------------------------------------------------------- cross-rank sequence check
+    def collect(self):
+        self.sigs = []
+
+    def verify(self, what: str = "step"):
+        """Gather every rank's collected signatures and raise on any disagreement (all ranks raise)."""
+        import torch.distributed as dist
+
+        mine, self.sigs = self.sigs or [], None
+        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
+            return
+        allv: List[Any] = [None] * dist.get_world_size()
+        dist.all_gather_object(allv, mine)
+        err = check_collective_sequences(allv)
+        if err is not None:
+            raise RuntimeError(f"ranks disagree on the collectives of the {what}: {err}")
 
     def _wait(self, name):
         h = self._handles.pop(name, None)

@@ -16,6 +16,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from .program import csig
+
 
 class TPComm:
     """``p2p`` (optional :class:`parallel.p2p.P2PAllReduce`) takes the fp32 activation
@@ -45,7 +47,7 @@ class TPComm:
             t.view(-1).copy_(self._pad4[:t.numel()])
             return t
         g = self.group
-        self.program.comm(lambda: dist.all_reduce(t, group=g))
+        self.program.comm(lambda: dist.all_reduce(t, group=g), sig=csig("all_reduce", g, t))
         return t
 
     def all_gather_stack(self, t: torch.Tensor) -> torch.Tensor:
@@ -66,5 +68,5 @@ class TPComm:
         out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         outs = list(out.unbind(0))
         g = self.group
-        self.program.comm(lambda: dist.all_gather(outs, t, group=g))
+        self.program.comm(lambda: dist.all_gather(outs, t, group=g), sig=csig("all_gather", g, t))
         return out

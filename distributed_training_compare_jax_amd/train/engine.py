@@ -27,7 +27,7 @@ from ..parallel.buffers import FlatParams
 from ..parallel.dist import DistInfo
 from ..parallel.dp import GradBuckets
 from ..parallel.mesh import Mesh, build_mesh, resolve_degrees, split_layers
-from ..parallel.program import StepProgram
+from ..parallel.program import StepProgram, csig
 from ..parallel.tp import TPComm
 from .optimizer import FusedAdamW, ShardedAdamW
 
@@ -341,7 +341,8 @@ class Engine:
             # the embedding-output gradients go out the moment the first layer's dgrad produces them,
             # under that layer's remaining weight-gradient work
             def dx_hook(d, out=self.dh_all, g=self.mesh.dp_group):
-                self.program.comm(lambda: dist.all_gather_into_tensor(out, d, group=g))
+                self.program.comm(lambda: dist.all_gather_into_tensor(out, d, group=g),
+                                  sig=csig("all_gather", g, d))
         dx, dx_c = st.stage_backward(ctx, dx, dx_c, 0.0, hook=hook, dx_hook=dx_hook)
         if self.embed_gather:
             bk.ready_all()
@@ -373,7 +374,7 @@ class Engine:
         t = self.loss
         if name is None:
             for g in groups:
-                self.program.comm(lambda g=g: dist.all_reduce(t, group=g))
+                self.program.comm(lambda g=g: dist.all_reduce(t, group=g), sig=csig("all_reduce", g, t))
             return []
         # one collective item (one graph cut): with both groups the pp sum must land before the dp
         # sum reads the tensor (separate communicators / streams), so the first is joined to the
@@ -383,7 +384,7 @@ class Engine:
                 dist.all_reduce(t, group=g, async_op=True).wait()
             return dist.all_reduce(t, group=groups[-1], async_op=True)
 
-        self.program.comm(fn, name=name)
+        self.program.comm(fn, name=name, sig=[x for g in groups for x in csig("all_reduce", g, t)])
         return [name]
 
     def _step_fn_pp(self):
@@ -408,6 +409,9 @@ class Engine:
         """Enqueue one full training step on the static inputs; returns the (device) loss."""
         p = self.program
         p.begin_step()
+        check = self.steps_done == 0 or (p.use_graph and not p.recorded)
+        if check:
+            p.collect()  # the first eager step and the recorded step prove the ranks agree
         if not p.use_graph:
             self._step_fn()
         elif not p.recorded:
@@ -415,9 +419,12 @@ class Engine:
                 self._step_fn()  # eager first step: lazy RCCL init, workspace sizing
             else:
                 p.record(self._step_fn)
+                p.verify("recorded step")
                 p.replay()
         else:
             p.replay()
+        if check and p.sigs is not None:
+            p.verify("first step")
         self.steps_done += 1
         return self.loss
 

@@ -20,6 +20,7 @@ from ..config.schema import OptimConfig
 from ..ops import optim as O
 from ..ops.reduce import GradReducer
 from ..parallel.buffers import FlatParams
+from ..parallel.program import csig
 
 
 def merge_segments(segs, total: int):
@@ -129,11 +130,11 @@ class FusedAdamW:
             else:
                 g = self.tp_group
                 s = self.sumsq
-                self.program.comm(lambda: dist.all_reduce(s, group=g))
+                self.program.comm(lambda: dist.all_reduce(s, group=g), sig=csig("all_reduce", g, s))
         if self.pp_group is not None:
             g = self.pp_group
             s = self.sumsq
-            self.program.comm(lambda: dist.all_reduce(s, group=g))
+            self.program.comm(lambda: dist.all_reduce(s, group=g), sig=csig("all_reduce", g, s))
 
     def update_range(self, lo: int, hi: int, enable=None, max_blocks: int = 0):
         """Clip + AdamW over flat[lo:hi] (4-aligned) with the norm/step of the last :meth:`norm`
@@ -211,22 +212,25 @@ class ShardedAdamW:
         g, p = f.grads, f.params
         lo, hi, n = self.lo, self.hi, self.n_rs
         if n and self._emulate:
-            self.program.comm(lambda: dist.all_reduce(g[:n], group=grp))
+            self.program.comm(lambda: dist.all_reduce(g[:n], group=grp), sig=csig("all_reduce", grp, g[:n]))
         elif n:
-            self.program.comm(lambda: dist.reduce_scatter_tensor(g[lo:hi], g[:n], group=grp))
+            self.program.comm(lambda: dist.reduce_scatter_tensor(g[lo:hi], g[:n], group=grp),
+                              sig=csig("reduce_scatter", grp, g[:n]))
         if self.n_tail:
-            self.program.comm(lambda: dist.all_reduce(g[n:], group=grp))
+            self.program.comm(lambda: dist.all_reduce(g[n:], group=grp), sig=csig("all_reduce", grp, g[n:]))
         O.sumsq_segments(g, self.segments, self.sumsq, step=self.step_t)
         s = self.sumsq
-        self.program.comm(lambda: dist.all_reduce(s, group=grp))
+        self.program.comm(lambda: dist.all_reduce(s, group=grp), sig=csig("all_reduce", grp, s))
         self._adamw(lo, hi, 0)
         self._adamw(n, f.numel, self.S)
         if n and self._emulate:
             S = self.S
             self.program.comm(lambda: dist.all_gather([p[i * S:(i + 1) * S] for i in range(self.dp)],
-                                                      p[lo:hi].clone(), group=grp))
+                                                      p[lo:hi].clone(), group=grp),
+                              sig=csig("all_gather", grp, p[lo:hi]))
         elif n:
-            self.program.comm(lambda: dist.all_gather_into_tensor(p[:n], p[lo:hi], group=grp))
+            self.program.comm(lambda: dist.all_gather_into_tensor(p[:n], p[lo:hi], group=grp),
+                              sig=csig("all_gather", grp, p[lo:hi]))
         f.refresh_mirror()
 
     def grad_norm(self) -> float:

@@ -12,7 +12,7 @@ class _Prog:
     def __init__(self):
         self.issued = []
 
-    def comm(self, fn, name=None):
+    def comm(self, fn, name=None, sig=None):
         self.issued.append(name)
 
 
