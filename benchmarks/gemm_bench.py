@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--json", default=None)
     ap.add_argument("--model", default="ref")
+    ap.add_argument("--only", default="", help="comma list: run only ops whose name contains one of these")
+    ap.add_argument("--no-ref", action="store_true", help="skip the hipBLASLt yardstick (clean PMC runs)")
     a = ap.parse_args()
+    only = [x for x in a.only.split(",") if x]
+    want = lambda name: not only or any(o in name for o in only)  # noqa: E731
     dev = torch.device("cuda")
     from distributed_training_compare_jax_amd.config.schema import model_config_from_preset
 
@@ -43,6 +47,12 @@ def main():
     H, T = mc.n_heads, mc.max_seq_len
     r = lambda *s: (torch.randn(*s, device=dev) * 0.5).to(torch.bfloat16)  # noqa: E731
     rows = []
+
+    def tm(name, fn, ref=None):
+        """(us, hipBLASLt us) of `name`, or None when filtered out"""
+        if not want(name):
+            return None
+        return timeit(fn, a.reps), (None if (ref is None or a.no_ref) else timeit(ref, a.reps))
 
     def rec(name, us, flops, ref_us=None):
         tf = flops / us / 1e6
@@ -65,30 +75,48 @@ def main():
             f = lambda: X.lmhead_logits_partials(x, w, b, lab, 0, 50257)  # noqa: E731
         else:
             f = lambda: G.linear(x, w, b)  # noqa: E731
-        rec(f"fwd  {tag} [{M}x{n}x{k}]", timeit(f, a.reps), 2 * M * n * k, timeit(lambda: x @ w.t(), a.reps))
+        nm = f"fwd  {tag} [{M}x{n}x{k}]"
+        t = tm(nm, f, lambda: x @ w.t())
+        if t:
+            rec(nm, t[0], 2 * M * n * k, t[1])
         dy = r(M, n)
         if tag == "fc2":
             u = r(M, k)
             f = lambda: G.matmul_nn_dgelu(dy, w, u)  # noqa: E731
         else:
             f = lambda: G.matmul_nn(dy, w)  # noqa: E731
-        rec(f"dgrad {tag} [{M}x{k}x{n}]", timeit(f, a.reps), 2 * M * n * k, timeit(lambda: dy @ w, a.reps))
+        nm = f"dgrad {tag} [{M}x{k}x{n}]"
+        t = tm(nm, f, lambda: dy @ w)
+        if t:
+            rec(nm, t[0], 2 * M * n * k, t[1])
         dw = torch.zeros(n, k, device=dev)
-        rec(f"wgrad {tag} [{n}x{k}x{M}]", timeit(lambda: G.wgrad(dy, x, dw), a.reps), 2 * M * n * k,
-            timeit(lambda: dy.t() @ x, a.reps))
+        nm = f"wgrad {tag} [{n}x{k}x{M}]"
+        t = tm(nm, lambda: G.wgrad(dy, x, dw), lambda: dy.t() @ x)
+        if t:
+            rec(nm, t[0], 2 * M * n * k, t[1])
         db = torch.zeros(n, device=dev)
-        us = timeit(lambda: G.colsum(dy, db), a.reps)
-        rows.append(dict(op=f"colsum {tag}", us=round(us, 2)))
-        print(f"colsum {tag:31s} {us:9.1f} us", flush=True)
+        t = tm(f"colsum {tag}", lambda: G.colsum(dy, db))
+        if t:
+            rows.append(dict(op=f"colsum {tag}", us=round(t[0], 2)))
+            print(f"colsum {tag:31s} {t[0]:9.1f} us", flush=True)
     # lm_head forward without the CE epilogue (isolates the epilogue cost)
     x, w = r(M, D), r(V, D) * 0.05
-    rec(f"fwd  lm_head plain-epilogue [{M}x{V}x{D}]", timeit(lambda: G.linear(x, w, None), a.reps), 2 * M * V * D)
+    nm = f"fwd  lm_head plain-epilogue [{M}x{V}x{D}]"
+    t = tm(nm, lambda: G.linear(x, w, None))
+    if t:
+        rec(nm, t[0], 2 * M * V * D)
     qkv = r(8, T, 3 * D)
     o, lse = A.attn_fwd(qkv, H)
     fl = A.attn_flops(8, T, H, D // H)
-    rec(f"attn fwd  B8 T{T} H{H} hd{D // H}", timeit(lambda: A.attn_fwd(qkv, H), a.reps), fl)
+    nm = f"attn fwd  B8 T{T} H{H} hd{D // H}"
+    t = tm(nm, lambda: A.attn_fwd(qkv, H))
+    if t:
+        rec(nm, t[0], fl)
     do = r(8, T, D)
-    rec(f"attn bwd  B8 T{T} H{H} hd{D // H}", timeit(lambda: A.attn_bwd(qkv, o, lse, do, H), a.reps), 2.5 * fl)
+    nm = f"attn bwd  B8 T{T} H{H} hd{D // H}"
+    t = tm(nm, lambda: A.attn_bwd(qkv, o, lse, do, H))
+    if t:
+        rec(nm, t[0], 2.5 * fl)
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(rows, fh, indent=1)

@@ -1214,6 +1214,491 @@ gemm256_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B,
 }
 
 // ============================================================================================
+// 256x256 tile, phase-interleaved ("ping-pong") main loop: the same tile, waves and epilogues as
+// gemm256_kernel, with the staging pipeline rebuilt for ~1 block per CU
+// (cdna_hip_programming.md §5 "The 256² 8-phase template", T3-T5):
+//  * each K-step (64 k) is 4 phases; in phase p a wave ds-reads its A fragments of output rows
+//    32p..32p+31 (+ all its B fragments at p = 0), issues 2 LDS-DMA instructions of the pipeline,
+//    raw s_barrier, then 16 MFMAs between s_setprio(1)/(0), raw s_barrier.  The waves of the second
+//    M half (waves 4-7, the other wave of each SIMD) run one barrier behind, so on every SIMD one
+//    wave's MFMAs cover the other's LDS reads and DMA issue.
+//  * operand images are 4 chunks of 64 contiguous rows (m or n) x 64 k: wave group wr reads A chunks
+//    2wr (phases 0-1) and 2wr+1 (phases 2-3), wave column q reads B chunk q.  Contiguous chunks keep
+//    every DMA source run a whole 128-B line for both operand kinds.
+//    K-major chunk: [64 rows][64 k] (128-B rows, 16-B k-piece c of image row r at c ^ ((r>>1)&7),
+//    the gemm256 image); MN-major chunk: [64 k][64 rows] (128-B k-rows, 16-B piece c of k-row r at
+//    c ^ mn8_swz(r)).  Fragment reads of both kinds are bank-conflict-free.
+//  * DMA schedule (2 per thread per phase): p0 A chunks 0,2 of K-step t+1, p1 A chunks 1,3 of t+1,
+//    p2 B chunks 0,1 of t+2, p3 B chunks 2,3 of t+2.  Every region is re-staged >= 2 phases after its
+//    last read (WAR: A chunks 0,2 are last read in phase 1, 1,3 in phase 3, B in phase 0).  Counted
+//    waits (never vmcnt(0) in steady state) at the end of p0 (vmcnt 6: A chunks 1,3 of t landed) and
+//    p2 (vmcnt 4: B and A chunks 0,2 of t+1): each retires data two phases before its first read,
+//    which covers the half-phase stagger of the two wave groups.
+constexpr int P8_CHUNK = 64 * 64;  // elements per operand chunk
+
+__device__ __forceinline__ int mn8_swz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+
+// one LDS-DMA instruction per wave: chunk q (rows 64q..64q+63) of an operand at k-step k0 -> img
+template <bool KMAJ>
+__device__ __forceinline__ void p8_dma(const bf16* __restrict__ X, long ldx, int r0, int rmax, int k0, bf16* img,
+                                       int q, int wave, int lane) {
+  if (KMAJ) {  // 8 image rows x 128 B
+    const int r = wave * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int g = min(r0 + 64 * q + r, rmax - 1);
+    __builtin_amdgcn_global_load_lds((glb_vptr)(X + (long)g * ldx + k0 + c * 8),
+                                     (lds_vptr)(img + q * P8_CHUNK + wave * 512), 16, 0, 0);
+  } else {  // 8 k-rows x 128 B
+    const int kr = wave * 8 + (lane >> 3);
+    const int pc = (lane & 7) ^ mn8_swz(kr);
+    const int col = min(r0 + 64 * q + 8 * pc, rmax - 8);
+    __builtin_amdgcn_global_load_lds((glb_vptr)(X + (long)(k0 + kr) * ldx + col),
+                                     (lds_vptr)(img + q * P8_CHUNK + wave * 512), 16, 0, 0);
+  }
+}
+
+// ds_read_b64_tr_b16 as inline asm: hipcc puts an s_waitcnt vmcnt(0) in front of every builtin
+// transpose read while an LDS-DMA is in flight (it does not for ds_read_b128), which drained the
+// whole DMA pipeline each phase of the MN-major kernels.  The compiler does not count these reads:
+// their consumers sit behind p8_lgkm_wait, which waits lgkmcnt(0) and ties the fragment registers.
+__device__ __forceinline__ s16x4 ds_tr16_asm(const bf16* p) {
+  s16x4 r;
+  const unsigned a = (unsigned)(unsigned long)(DTC_LDS void*)(p);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
+// fragment of 16-row group t (0..15: chunk t>>2, rows 16(t&3)..) at k-chunk kk, natural k order
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 p8_frag(const bf16* img, int t, int kk, int lane) {
+  if (KMAJ) return big_frag<true>(img, t, kk, lane);
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const bf16* base = img + (t >> 2) * P8_CHUNK;
+  const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
+  const int pc = 2 * (t & 3) + (pp >> 1), w = (pp & 1) * 4;
+  const bf16* p0 = base + k0 * 64 + ((pc ^ mn8_swz(k0)) << 3) + w;
+  const bf16* p1 = base + k1 * 64 + ((pc ^ mn8_swz(k1)) << 3) + w;
+  const s16x4 lo = ds_tr16_asm(p0), hi = ds_tr16_asm(p1);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// every LDS read of the phase has landed; the fragments are tied in so no consumer moves above it
+__device__ __forceinline__ void p8_lgkm_wait(bf16x8 (&fa)[2][2], bf16x8 (&fb)[4][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                 "+v"(fb[1][0]), "+v"(fb[1][1]), "+v"(fb[2][0]), "+v"(fb[2][1]), "+v"(fb[3][0]), "+v"(fb[3][1])
+               :
+               : "memory");
+}
+
+#define P8_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(NT2, 1)
+gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+              int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+  constexpr int TM = 8, TN = 4;  // 16x16 fragments per wave: 128 (m) x 64 (n)
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB (the only LDS object)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;  // M half (= wave group), 64-column slice
+  const int ntiles = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, ntiles * split);
+  const int tile = lid % ntiles, z = lid / ntiles;
+  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+  const int gm_eff = min(gm, tiles_m - grp * gm);
+  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
+  const int kbeg = z * k_per_split;
+  const int nk = min(k_per_split, K - kbeg) / 64;
+  DTC_ASSERT(nk >= 1);
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto imgA = [&](int t) { return smem + (t & 1) * 2 * IMG; };
+  auto imgB = [&](int t) { return smem + (t & 1) * 2 * IMG + IMG; };
+  auto dmaA = [&](int t, int q) { p8_dma<AK>(A, lda, m0, M, kbeg + t * 64, imgA(t), q, wave, lane); };
+  auto dmaB = [&](int t, int q) { p8_dma<BKM>(B, ldb, n0, N, kbeg + t * 64, imgB(t), q, wave, lane); };
+
+  EpiPre<TN, TM> pre;  // epilogue operands: loaded ahead of every DMA, retired by the prologue wait
+  if (split == 1 && (EPI == EPI_LMHEAD || EPI == EPI_STORE))
+    epi_prefetch<TN, TM>(e, m0 + wr * 128, n0 + wc * 64, lane, EPI == EPI_LMHEAD, pre);
+  // prologue: B(0), A(0), B(1) in flight; wait for the first two
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dmaB(0, q);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dmaA(0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dmaB(1, q);
+    P8_VMCNT(4);
+  } else {
+    P8_VMCNT(0);
+  }
+  if (EPI == EPI_LMHEAD && split == 1) {  // the bias is the accumulators' starting value
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = pre.bb[i];
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // second wave group: one barrier behind
+
+  bf16x8 fb[TN][2], fa[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const bf16* sA = imgA(t);
+    const bf16* sB = imgB(t);
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      // ---- load slot: fragments of this phase + 2 DMA instructions of the pipeline
+      if (p == 0) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) fb[i][kk] = p8_frag<BKM>(sB, 4 * wc + i, kk, lane);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fa[jj][kk] = p8_frag<AK>(sA, 8 * wr + 2 * p + jj, kk, lane);
+      if (p < 2) {
+        if (more1) { dmaA(t + 1, p); dmaA(t + 1, p + 2); }
+      } else {
+        if (more2) { dmaB(t + 2, 2 * p - 4); dmaB(t + 2, 2 * p - 3); }
+      }
+      __builtin_amdgcn_s_barrier();
+      p8_lgkm_wait(fa, fb);
+      // ---- MFMA slot: output rows 32p..32p+31 of this wave's 128 x all 64 columns, K = 64
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[i][2 * p + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i][kk], fa[jj][kk], acc[i][2 * p + jj], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (p == 0) {
+        if (more1) P8_VMCNT(6); else P8_VMCNT(0);
+      } else if (p == 2) {
+        if (more2) P8_VMCNT(4); else if (more1) P8_VMCNT(2); else P8_VMCNT(0);
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the second group's extra barrier: LDS free after it
+
+  const int g4 = 4 * (lane >> 4);
+  if (split > 1) {  // fp32 slab z; splitk_reduce sums the slabs in a fixed order
+    float* sl = slab + (long)z * M * N;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wr * 128 + j * 16 + (lane & 15);
+        const int n = n0 + wc * 64 + i * 16 + g4;
+        if (m < M && n < N) *(f32x4*)(sl + (long)m * N + n) = acc[i][j];  // N % 4 == 0 (checked by host)
+      }
+    return;
+  }
+  bf16* stage = smem + wave * (128 * 64);
+  if (EPI == EPI_LMHEAD) {
+    lmhead_epilogue<TN, TM, true, true>(acc, e, m0 + wr * 128, n0 + wc * 64, tn_idx * 4 + wc, lane, pre, stage);
+    return;
+  }
+  if (EPI == EPI_STORE && !OUTF32) {
+    f32x4 bb[TN];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wc * 64 + i * 16 + g4;
+      bb[i] = pre.bb[i];
+      if (e.bias && n < N && n + 4 > N)
+        for (int r = 0; r < 4; ++r) bb[i][r] = n + r < N ? e.bias[n + r] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        bf16x4 ob;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ob[r] = f2bf(e.alpha * acc[i][j][r] + bb[i][r]);
+        stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
+      }
+    stage_out<128>(stage, (bf16*)e.C, e.ldc, m0 + wr * 128, n0 + wc * 64, M, N, lane);
+    return;
+  }
+  if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      int m = m0 + wr * 128 + j * 16 + (lane & 15);
+      int n = n0 + wc * 64 + i * 16 + g4;
+      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+    }
+}
+
+// ============================================================================================
+// Stream-K form of gemm8p_kernel for layer-sized GEMMs (a few hundred 256^2 tiles of 12-48 K-steps:
+// whole tiles per block would leave the last round of blocks mostly empty and pay a prologue and an
+// epilogue per tile).  The grid is one block per CU; the ntiles * nk K-steps are cut into equal
+// contiguous ranges of L, one per block, so every CU does the same MFMA work.  A block's range runs
+// through the phase pipeline as ONE K-step stream (the DMA of the next tile's first K-steps is in
+// flight while a tile finishes).  A range cuts at most two tiles; a cut tile's pieces store fp32
+// partials (wave-fragment order, coalesced) and bump the tile's counter; the last arriver sums all
+// pieces IN PIECE ORDER (deterministic) and runs the epilogue (agent-scope release / acquire around
+// the counter: cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2).  No block ever
+// waits for another, so a partly occupied chip cannot deadlock it.
+struct SkPlan {
+  int tiles_m, tiles_n, gm, nk, L, iters;
+  float* part;  // [2 * grid][256 * 256] fp32 piece partials (slot 2c: block c's first piece, 2c+1: its last)
+  int* cnt;     // [tiles] arrival counters, zero between launches (the last arriver resets its tile's)
+};
+
+__device__ __forceinline__ void sk_tile(const SkPlan& s, int T, int& tm, int& tn) {
+  const int grp = T / (s.gm * s.tiles_n), in_g = T % (s.gm * s.tiles_n);
+  const int gm_eff = min(s.gm, s.tiles_m - grp * s.gm);
+  tm = grp * s.gm + in_g % gm_eff;
+  tn = in_g / gm_eff;
+}
+
+// Epilogue of one wave's 128 x 64 from registers (the pipeline owns the LDS).  Its operand loads go
+// out a column of fragments at a time before any is used (see the fixup above); N % 4 == 0.
+template <int EPI, bool OUTF32>
+__device__ __forceinline__ void sk_epilogue(const f32x4 (&acc)[4][8], const Epi& e, int m_w, int n_w, int lane) {
+  constexpr int TN = 4;
+  const int g4 = 4 * (lane >> 4), li = lane & 15;
+  f32x4 bias[TN];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n_w + i * 16 + g4;
+    bias[i] = (e.bias && n < e.N) ? *(const f32x4*)(e.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr bool AUX = EPI == EPI_RESID || EPI == EPI_DGELU || (EPI == EPI_STORE && OUTF32);
+#pragma unroll
+  for (int h = 0; h < 2 * TN; ++h) {
+    const int i = h >> 1, j0 = (h & 1) * 4;
+    const int n = n_w + i * 16 + g4;
+    f32x4 ax[4];
+    if constexpr (AUX) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int m = m_w + (j0 + jj) * 16 + li;
+        ax[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (m < e.M && n < e.N) {
+          if (EPI == EPI_RESID) ax[jj] = *(const f32x4*)((const float*)e.aux + (long)m * e.ldaux + n);
+          if (EPI == EPI_DGELU) {
+            const bf16x4 u = *(const bf16x4*)((const bf16*)e.aux + (long)m * e.ldaux + n);
+            ax[jj] = f32x4{(float)u[0], (float)u[1], (float)u[2], (float)u[3]};
+          }
+          if (EPI == EPI_STORE && OUTF32 && e.beta != 0.f) ax[jj] = *(const f32x4*)((const float*)e.C + (long)m * e.ldc + n);
+        }
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int m = m_w + (j0 + jj) * 16 + li;
+      if (m >= e.M || n >= e.N) continue;
+      f32x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = e.alpha * acc[i][j0 + jj][r] + bias[i][r];
+      if (EPI == EPI_RESID) o += ax[jj];
+      if (EPI == EPI_DGELU) o *= ax[jj];
+      if (EPI == EPI_STORE && OUTF32 && e.beta != 0.f) o += e.beta * ax[jj];
+      if (OUTF32) {
+        *(f32x4*)((float*)e.C + (long)m * e.ldc + n) = o;
+      } else {
+        bf16x4 ob, gb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (EPI == EPI_GELU) {  // C = gelu'(u) (read in the backward only: non-temporal), aux_out = gelu(u)
+            float gv, dgv;
+            gelu_tanh_and_grad_f(o[r], gv, dgv);
+            ob[r] = f2bf(dgv);
+            gb[r] = f2bf(gv);
+          } else {
+            ob[r] = f2bf(o[r]);
+          }
+        }
+        if (EPI == EPI_GELU) {
+          __builtin_nontemporal_store(ob, (bf16x4*)((bf16*)e.C + (long)m * e.ldc + n));
+          *(bf16x4*)((bf16*)e.aux_out + (long)m * e.ldc + n) = gb;
+        } else {
+          *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
+        }
+      }
+    }
+  }
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(NT2, 1)
+gemm_sk_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, SkPlan s, Epi e) {
+  constexpr int TM = 8, TN = 4;
+  // pipeline buffers + one word (the counter broadcast): a single LDS object (§5 trap 4a)
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG + 8];
+  int* bcast = (int*)(smem + 4 * IMG);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int G = gridDim.x;
+  const int c = xcd_remap(blockIdx.x, G);  // logical block: each XCD runs a contiguous stretch of the stream
+  const int it0 = c * s.L, it1 = min(s.iters, it0 + s.L);
+  if (it0 >= it1) return;
+  const int n_it = it1 - it0;
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto imgA = [&](int j) { return smem + (j & 1) * 2 * IMG; };
+  auto imgB = [&](int j) { return smem + (j & 1) * 2 * IMG + IMG; };
+  // Running (tile, k-step) coordinates, advanced once per step (no divisions in the phases): the
+  // A stream runs one step ahead (step j+1), the B stream two (step j+2), `cur` is step j.
+  struct Pos { int T, k, base; };  // base: the tile's first row (A) / column (B)
+  auto tile_of = [&](int T, bool rows) { int tm, tn; sk_tile(s, T, tm, tn); return (rows ? tm : tn) * BIG; };
+  auto advance = [&](Pos& q, bool rows) {
+    if (++q.k == s.nk) { q.k = 0; ++q.T; if (q.T * s.nk < s.iters) q.base = tile_of(q.T, rows); }
+  };
+  Pos cur{it0 / s.nk, it0 % s.nk, 0};
+  Pos pa = cur, pb = cur;
+  pa.base = tile_of(pa.T, true);
+  pb.base = tile_of(pb.T, false);
+  auto dmaA = [&](const Pos& q, int j, int c4) { p8_dma<AK>(A, lda, q.base, M, q.k * 64, imgA(j), c4, wave, lane); };
+  auto dmaB = [&](const Pos& q, int j, int c4) { p8_dma<BKM>(B, ldb, q.base, N, q.k * 64, imgB(j), c4, wave, lane); };
+
+  // prologue: B(0), A(0), B(1); afterwards pa = step 1, pb = step 2
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dmaB(pb, 0, q);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dmaA(pa, 0, q);
+  advance(pa, true);
+  advance(pb, false);
+  if (n_it > 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dmaB(pb, 1, q);
+    advance(pb, false);
+    P8_VMCNT(4);
+  } else {
+    P8_VMCNT(0);
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  // piece partials: write-through (sc1) 16-B stores and sc1 loads, so no L2 writeback / invalidate
+  // fence is needed around the counter (§6 Guideline 16 R1); slot = 256 KB, wave-fragment order
+  const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc((void*)s.part, (short)0, 0x7fffffff, 0x00020000);
+  constexpr int SC1 = 16;
+
+  bf16x8 fb[TN][2], fa[2][2];
+  for (int j = 0; j < n_it; ++j) {
+    const bf16* sA = imgA(j);
+    const bf16* sB = imgB(j);
+    const bool more1 = j + 1 < n_it, more2 = j + 2 < n_it;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p == 0) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) fb[i][kk] = p8_frag<BKM>(sB, 4 * wc + i, kk, lane);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fa[jj][kk] = p8_frag<AK>(sA, 8 * wr + 2 * p + jj, kk, lane);
+      if (p < 2) {
+        if (more1) { dmaA(pa, j + 1, p); dmaA(pa, j + 1, p + 2); }
+      } else {
+        if (more2) { dmaB(pb, j + 2, 2 * p - 4); dmaB(pb, j + 2, 2 * p - 3); }
+      }
+      __builtin_amdgcn_s_barrier();
+      p8_lgkm_wait(fa, fb);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[i][2 * p + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i][kk], fa[jj][kk], acc[i][2 * p + jj], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (p == 0) {
+        if (more1) P8_VMCNT(6); else P8_VMCNT(0);
+      } else if (p == 2) {
+        if (more2) P8_VMCNT(4); else if (more1) P8_VMCNT(2); else P8_VMCNT(0);
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    const int T = cur.T, k = cur.k;
+    advance(pa, true);
+    advance(pb, false);
+    if (++cur.k == s.nk) { cur.k = 0; ++cur.T; }
+    if (k != s.nk - 1 && j != n_it - 1) continue;  // not the end of a piece
+    // ---------------- piece end: realign the two wave groups (block-wide barriers from here on)
+    if (wr == 0) __builtin_amdgcn_s_barrier();
+    int tm, tn;
+    sk_tile(s, T, tm, tn);
+    const int m_w = tm * BIG + wr * 128, n_w = tn * BIG + wc * 64;
+    const int k_first = j >= k ? 0 : k - j;  // this piece covers the tile's k-steps [k_first, k]
+    bool emit = true;
+    if (k_first != 0 || k != s.nk - 1) {
+      // a cut tile: pieces are the blocks c_lo..c_hi covering its K-steps
+      const int c_lo = (T * s.nk) / s.L, c_hi = ((T + 1) * s.nk - 1) / s.L;
+      const int np = c_hi - c_lo + 1;
+      // byte offset of block cb's slot for this tile (slot 2cb: cb's first piece, 2cb+1: its last)
+      auto slot = [&](int cb) { return (2 * cb + ((cb * s.L) / s.nk == T ? 0 : 1)) * (65536 * 4) + wave * (TN * TM * 1024); };
+      const int mine = slot(c);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TM; ++jj)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][jj]), rsP,
+                                                 mine + ((i * TM + jj) * 64 + lane) * 16, 0, SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) *bcast = __hip_atomic_fetch_add(s.cnt + T, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      emit = *bcast == np - 1;
+      if (emit) {  // last arriver: acc = sum of every piece in piece order (its own read back too:
+                   // no per-element register-or-load select, §5 trap 4c)
+        if (tid == 0) __hip_atomic_store(s.cnt + T, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int pi = 0; pi < np; ++pi) {
+          const int src = slot(c_lo + pi);
+#pragma unroll
+          for (int h = 0; h < 2 * TN; ++h) {  // 4 loads out before any use: one round trip per batch
+            const int i = h >> 1, j0 = (h & 1) * 4;
+            f32x4 v[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              v[jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, src + ((i * TM + j0 + jj) * 64 + lane) * 16, 0, SC1));
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) acc[i][j0 + jj] = pi == 0 ? v[jj] : acc[i][j0 + jj] + v[jj];
+          }
+        }
+      }
+    }
+    if (emit) sk_epilogue<EPI, OUTF32>(acc, e, m_w, n_w, lane);
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int jj = 0; jj < TM; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (j + 1 < n_it && wr == 1) __builtin_amdgcn_s_barrier();  // re-stagger for the next piece
+  }
+}
+
+// ============================================================================================
 // lm_head backward with the cross-entropy backward fused into the dgrad's A operand.
 //   dlogits[t][v] = (exp(logit[t][v] - lse[t]) - [v == label[t]]) * scale   (pad columns 0)
 //   dX[t][:]      = sum_v dlogits[t][v] * W[v][:]    (NT split-K on W^T, as the unfused dgrad)
@@ -2091,6 +2576,78 @@ int big_split(int layout, int M, int N, int K) {
 
 inline int big_kps(int K, int split) { return ((K / 64 + split - 1) / split) * 64; }
 
+// ---- stream-K (gemm_sk_kernel): one workspace per device (piece partials + tile counters), allocated
+// on first use OUTSIDE graph capture.  Only forwards and dgrads take this path, which never run on two
+// streams at once (the optional side stream carries weight gradients), so one workspace suffices.
+struct SkWs { int dev; float* part; int* cnt; };
+constexpr int SK_MAX_DEV = 16, SK_MAX_TILES = 1 << 16;
+static SkWs g_skws[SK_MAX_DEV];
+static int g_nskws = 0;
+
+static int sk_cus() {
+  static const int n = [] {
+    int d = 0, v = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) v = 0;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+static const SkWs* sk_ws(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  for (int i = 0; i < g_nskws; ++i) if (g_skws[i].dev == dev) return &g_skws[i];
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (g_nskws == SK_MAX_DEV) return nullptr;
+  SkWs w{dev, nullptr, nullptr};
+  if (hipMalloc(&w.part, (size_t)2 * sk_cus() * 65536 * sizeof(float)) != hipSuccess) return nullptr;
+  if (hipMalloc(&w.cnt, SK_MAX_TILES * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemset(w.cnt, 0, SK_MAX_TILES * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+  g_skws[g_nskws++] = w;
+  return &g_skws[g_nskws - 1];
+}
+
+// DTC_GEMM_SK: bit mask of the layouts (1 fwd, 2 dgrad) whose layer-sized GEMMs run stream-K.  A
+// problem qualifies when its 256^2 tiles would leave the chip unevenly loaded as whole tiles.
+static int g_sk_mask = [] { const char* v = getenv("DTC_GEMM_SK"); return v ? atoi(v) : 0; }();
+static int sk_mask() { return g_sk_mask; }
+static bool sk_wanted(int layout, int M, int N, int K) {
+  if (!(sk_mask() & (1 << layout)) || K % 64 || N % 4 || M < 256 || N < 256) return false;
+  if (layout != 0 && N % 8) return false;
+  const long tiles = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
+  if (tiles > SK_MAX_TILES) return false;
+  const long iters = tiles * (K / 64);
+  return iters >= 2L * sk_cus();  // at least 2 K-steps per CU
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_sk(const GemmArgs& a, hipStream_t st) {
+  const SkWs* ws = sk_ws(st);
+  if (!ws) return -1;  // no workspace (first use under capture): caller takes the tiled path
+  Epi e{};
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
+  SkPlan p{};
+  p.tiles_m = (a.M + BIG - 1) / BIG;
+  p.tiles_n = (a.N + BIG - 1) / BIG;
+  p.nk = a.K / 64;
+  const long iters = (long)p.tiles_m * p.tiles_n * p.nk;
+  const int G0 = sk_cus();
+  p.L = (int)((iters + G0 - 1) / G0);
+  p.iters = (int)iters;
+  const int G = (int)((iters + p.L - 1) / p.L);
+  // an XCD's 1/8 of the stream: groups of gm M-tiles sweep the N-tiles within it
+  const long per_xcd = std::max(1L, (iters / 8) / p.nk);
+  p.gm = (int)std::max(1L, std::min((long)p.tiles_m, per_xcd / std::max(1, p.tiles_n)));
+  p.part = ws->part;
+  p.cnt = ws->cnt;
+  hipLaunchKernelGGL((gemm_sk_kernel<AK, BKM, EPI, OUTF32>), dim3(G), dim3(NT2), 0, st, (const bf16*)a.A, a.lda,
+                     (const bf16*)a.B, a.ldb, a.M, a.N, p, e);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
 template <bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   Epi e{};
@@ -2101,13 +2658,26 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   const int tiles_m = (a.M + BIG - 1) / BIG, tiles_n = (a.N + BIG - 1) / BIG;
   e.nparts = tiles_n * 4;
   const int ntiles = tiles_m * tiles_n;
+  // tile order: groups of gm M-tiles sweep all N-tiles.  With few N-tiles a group is sized to the
+  // ~32 blocks an XCD runs at once, so the N-tiles sharing an A panel run together on one L2 (a group
+  // spanning a whole XCD run -- 74 tiles of the lm_head weight gradient -- left 2 of its 3 N-tiles
+  // re-fetching their A panel from HBM: 2x FETCH_SIZE, profiles/r3_gemm8p.md)
   int gm = tiles_m;
-  if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles * split / 8 + tiles_n - 1) / tiles_n));
+  if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, 32 / tiles_n));
   const int kps = big_kps(a.K, split);
   if (split > 1 && (a.ws_bytes < (long)split * a.M * a.N * 4 || a.N % 4)) return 1005;
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
-                     (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
-                     (float*)a.workspace, e);
+  // DTC_GEMM8P: 2 = the phase-interleaved main loop (gemm8p_kernel) for every layout, 1 = only with a
+  // K-major A operand, 0 = gemm256_kernel.  GPT-2 small lm_head: forward 793 -> 770 us, vocab-K dgrad
+  // 852 -> 636 us, weight gradient 843 -> 679 us (profiles/r3_gemm8p.md).
+  static const int p8 = [] { const char* v = getenv("DTC_GEMM8P"); return v ? atoi(v) : 2; }();
+  if (p8 == 2 || (p8 == 1 && AK))
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
+                       (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
+                       (float*)a.workspace, e);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
+                       (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
+                       (float*)a.workspace, e);
   DTC_CHECK_LAUNCH();
   if (split > 1 && !a.defer_reduce) {
     long MN = (long)a.M * a.N;
@@ -2269,6 +2839,7 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   if (a1->M <= 0 || a1->N <= 0 || a2->M <= 0 || a2->N <= 0) return 1100;
   if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
   if (big_split(a1->layout, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
+  if (sk_wanted(a1->layout, a1->M, a1->N, a1->K) && a1->colsum == nullptr) return 1100;  // stream-K dgrad: own launch
   if (dmaw_plan(a1->layout, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
       dmaw_plan(2, a2->M, a2->N, a2->K, a2->epi, a2->c_f32 != 0, a2->colsum != nullptr).cfg != W_NONE)
     return 1100;  // the 8-wave kernels run these as two launches
@@ -2401,12 +2972,32 @@ long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   return split > 1 ? (long)split * M * N * 4 : 0;
 }
 
+// stream-K layout mask (DTC_GEMM_SK at load time); returns the previous mask (tests / A/B)
+int dtc_gemm_set_sk(int mask) {
+  const int old = g_sk_mask;
+  g_sk_mask = mask;
+  return old;
+}
+
 int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->K % 32 != 0) return 1001;               // K must be a multiple of 32 (BK = 64, or 32)
   if (a->lda % 8 || a->ldb % 8 || a->ldc % 4) return 1002;  // 16-B row alignment
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
+  if (a->layout <= 1 && !a->colsum && sk_wanted(a->layout, a->M, a->N, a->K)) {
+    int r = -2;
+    if (a->layout == 0) {
+      if (epi == EPI_STORE) r = f32 ? launch_sk<true, true, EPI_STORE, true>(*a, st) : launch_sk<true, true, EPI_STORE, false>(*a, st);
+      else if (epi == EPI_GELU && !f32) r = launch_sk<true, true, EPI_GELU, false>(*a, st);
+      else if (epi == EPI_RESID && f32) r = launch_sk<true, true, EPI_RESID, true>(*a, st);
+      else if (epi == EPI_DGELU && !f32) r = launch_sk<true, true, EPI_DGELU, false>(*a, st);
+    } else {
+      if (epi == EPI_STORE) r = f32 ? launch_sk<true, false, EPI_STORE, true>(*a, st) : launch_sk<true, false, EPI_STORE, false>(*a, st);
+      else if (epi == EPI_DGELU && !f32) r = launch_sk<true, false, EPI_DGELU, false>(*a, st);
+    }
+    if (r >= 0) return r;
+  }
   if (a->layout <= 2 && !(a->layout == 2 && a->bias)) {
     const WPlan w = dmaw_plan(a->layout, a->M, a->N, a->K, epi, f32, a->colsum != nullptr);
     if (w.cfg != W_NONE) {

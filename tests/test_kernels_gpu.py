@@ -34,7 +34,7 @@ def _close(a, b, rtol, name=""):
 
 
 GEMM_SHAPES = [(4096, 1536, 512), (4096, 512, 512), (4096, 2048, 512), (4096, 512, 2048), (256, 384, 128), (512, 768, 96),
-               (200, 136, 64), (4096, 50304, 512), (2000, 33000, 128)]
+               (200, 136, 64), (4096, 50304, 512), (2000, 33000, 128), (8192, 2304, 768)]
 
 
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
