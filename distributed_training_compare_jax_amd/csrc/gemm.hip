@@ -1715,8 +1715,9 @@ __device__ __forceinline__ bf16x8 ce_colsum_frag(const bf16* img, int r0, int vt
   const int row = r0 + 4 * g + q;  // rows r0 + {4g+q} and +16: every row of r0..r0+31 once
   const int ch = 2 * vt + (pp >> 1);
   const bf16* p0 = img + row * 64 + ((ch ^ ((row >> 1) & 7)) << 3) + (pp & 1) * 4;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0 + 16 * 64));
+  // asm reads (ds_tr16_asm): the builtin made hipcc drain the in-flight W^T DMA before every column-sum
+  // k-step; the caller waits lgkmcnt(0) with the fragments tied in
+  const s16x4 lo = ds_tr16_asm(p0), hi = ds_tr16_asm(p0 + 16 * 64);
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
@@ -1823,8 +1824,12 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
     const bool cs_own = owns(kt);
     if (cs_own) {  // column sums of this k-step's dlogits tile: 4 MFMAs per wave
       f32x4 cs = {0.f, 0.f, 0.f, 0.f};
+      bf16x8 cf[4];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) cs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, ce_colsum_frag(sA, cs_half * 128 + 32 * s4, cs_vt, lane), cs, 0, 0, 0);
+      for (int s4 = 0; s4 < 4; ++s4) cf[s4] = ce_colsum_frag(sA, cs_half * 128 + 32 * s4, cs_vt, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cf[0]), "+v"(cf[1]), "+v"(cf[2]), "+v"(cf[3]) : : "memory");
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) cs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, cf[s4], cs, 0, 0, 0);
       if (lane < 16) a.colpart[(long)(2 * tm_idx + cs_half) * a.K + kbeg + kt * 64 + cs_vt * 16 + lane] = cs[0];
     }
 #pragma unroll
