@@ -89,6 +89,12 @@ def main():
         t = tm(nm, f, lambda: dy @ w)
         if t:
             rec(nm, t[0], 2 * M * n * k, t[1])
+        if tag in ("qkv", "fc1"):  # the NT dgrad on the transposed weight (fp32 out), as the step runs it
+            wt = w.t().contiguous()
+            nm = f"ntdgrad {tag} [{M}x{k}x{n}]"
+            t = tm(nm, lambda: G.linear(dy, wt, out_dtype=torch.float32), lambda: dy @ w)
+            if t:
+                rec(nm, t[0], 2 * M * n * k, t[1])
         dw = torch.zeros(n, k, device=dev)
         nm = f"wgrad {tag} [{n}x{k}x{M}]"
         t = tm(nm, lambda: G.wgrad(dy, x, dw), lambda: dy.t() @ x)

@@ -48,7 +48,7 @@ def hipcc() -> str:
 def _digest(paths, flags=FLAGS) -> str:
     h = hashlib.sha256()
     for p in sorted(paths):
-        h.update(p.encode())
+        h.update(os.path.basename(p).encode())  # path-independent: the box copy reuses this build
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(" ".join(flags).encode())

@@ -1449,6 +1449,163 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 }
 
 // ============================================================================================
+// 128 x (64*CB) tile, 8 waves (2 along M x 4 along N, 64 x 16*CB per wave), NS-stage LDS-DMA ring,
+// phase-interleaved like gemm8p_kernel -- for the layer GEMMs.  Their shapes quantise badly on
+// 128^2 / 256^2 tiles (GPT-2 small: M = 8192 tokens, N = 768 / 2304 / 3072 = 4 / 12 / 16 x 192;
+// GPT-2 medium: N = 1024 / 3072 / 4096 = 4 x 256, 16 x 192, 16 x 256) but make EXACTLY 1, 3 or 4
+// rounds of 256 tiles here, one block per CU, and the 64 x 48 (CB = 3) / 64 x 64 (CB = 4) wave tile
+// keeps LDS reads at 0.58 / 0.5 ds_read_b128 per MFMA (one per MFMA is the CU's limit).
+//  * K-step = 64 k, 2 phases: phase p reads the wave's A fragments of rows 32p..32p+31 (+ all its B
+//    fragments at p = 0), issues its share of the ring's DMA, raw s_barrier, 12 (CB = 3) / 16 (CB = 4) MFMAs between
+//    s_setprio(1)/(0), raw s_barrier; waves 4-7 run one barrier behind (as gemm8p).
+//  * Ring of NS stages (A image = 2 chunks, B image = CB chunks of [64 rows][64 k] -- the gemm8p
+//    chunk images and swizzles).  Stage s is loaded D = NS-1 K-steps ahead: its B chunks in phase 0
+//    of step s-D, its A chunks in phase 1 (each region re-staged 2 phases after its last read: B is
+//    last read in phase 0, A in phase 1 of the slot's previous step).  Stage t+1
+//    is retired by a counted vmcnt at the end of phase 0 of step t, one full phase before its first
+//    read (the staggered wave group reads it one barrier later).  Never vmcnt(0) in steady state.
+//  * NS = 4 for CB = 3 (160 KB: the whole LDS), 3 for CB = 4 (144 KB).
+__device__ __forceinline__ void n8_vmcnt(int n) {  // s_waitcnt vmcnt(n), n a runtime value <= 18
+  switch (n) {
+    case 0: P8_VMCNT(0); break;
+    case 2: P8_VMCNT(2); break;
+    case 3: P8_VMCNT(3); break;
+    case 4: P8_VMCNT(4); break;
+    case 5: P8_VMCNT(5); break;
+    case 6: P8_VMCNT(6); break;
+    case 8: P8_VMCNT(8); break;
+    case 9: P8_VMCNT(9); break;
+    case 10: P8_VMCNT(10); break;
+    case 11: P8_VMCNT(11); break;
+    case 12: P8_VMCNT(12); break;
+    case 15: P8_VMCNT(15); break;
+    case 16: P8_VMCNT(16); break;
+    case 18: P8_VMCNT(18); break;
+    default: P8_VMCNT(0); break;  // over-waiting is always safe
+  }
+}
+
+template <int CB, int NS, bool AK, bool BKM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(NT2, 1)
+gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+              int tiles_m, int tiles_n, int gm, Epi e) {
+  static_assert(NS >= 3, "stage t+1 must be issued before the phase-0 wait of step t");
+  constexpr int CA = 2, TM = 4, TN = CB, BN = 64 * CB, D = NS - 1, PIECES = CA + CB;
+  constexpr int SIMG = PIECES * P8_CHUNK;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * SIMG];  // the only LDS object
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntiles = tiles_m * tiles_n;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+  const int gm_eff = min(gm, tiles_m - grp * gm);
+  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  const int m0 = tm_idx * 128, n0 = tn_idx * BN;
+  const int nk = K / 64;
+  DTC_ASSERT(nk >= 1);
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto imgA = [&](int s) { return smem + (s % NS) * SIMG; };
+  auto imgB = [&](int s) { return smem + (s % NS) * SIMG + CA * P8_CHUNK; };
+  auto dmaA = [&](int s, int q) { p8_dma<AK>(A, lda, m0, M, s * 64, imgA(s), q, wave, lane); };
+  auto dmaB = [&](int s, int q) { p8_dma<BKM>(B, ldb, n0, N, s * 64, imgB(s), q, wave, lane); };
+
+  // prologue: stages 0..D-1 (B then A each), wait for stage 0
+  const int npro = min(D, nk);
+  for (int s = 0; s < npro; ++s) {
+#pragma unroll
+    for (int q = 0; q < CB; ++q) dmaB(s, q);
+#pragma unroll
+    for (int q = 0; q < CA; ++q) dmaA(s, q);
+  }
+  n8_vmcnt((npro - 1) * PIECES);
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // second wave group: one barrier behind
+
+  bf16x8 fb[TN][2], fa[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const bf16* sA = imgA(t);
+    const bf16* sB = imgB(t);
+    const bool issue = t + D < nk;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (p == 0) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) fb[i][kk] = p8_frag<BKM>(sB, TN * wc + i, kk, lane);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fa[jj][kk] = p8_frag<AK>(sA, 4 * wr + 2 * p + jj, kk, lane);
+      if (issue) {
+        if (p == 0) {
+#pragma unroll
+          for (int q = 0; q < CB; ++q) dmaB(t + D, q);
+        } else {
+#pragma unroll
+          for (int q = 0; q < CA; ++q) dmaA(t + D, q);
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) asm volatile("" : "+v"(fa[jj][kk]));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) asm volatile("" : "+v"(fb[i][kk]));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[i][2 * p + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i][kk], fa[jj][kk], acc[i][2 * p + jj], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (p == 0 && t + 1 < nk) {
+        // retire stage t+1: younger than its A pieces are the stages t+2 .. t+D-1 that exist, and
+        // B(t+D) when it was issued this phase
+        if (t + D < nk) {
+          n8_vmcnt((D - 2) * PIECES + CB);  // constant: folds to one s_waitcnt
+        } else {
+          const int full = max(0, min(t + D - 1, nk - 1) - (t + 1));
+          n8_vmcnt(full * PIECES);
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the second group's extra barrier
+
+  const int g4 = 4 * (lane >> 4);
+  if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wr * 64 + j * 16 + (lane & 15);
+      const int n = n0 + wc * 16 * TN + i * 16 + g4;
+      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+    }
+}
+
+// ============================================================================================
 // Stream-K form of gemm8p_kernel for layer-sized GEMMs (a few hundred 256^2 tiles of 12-48 K-steps:
 // whole tiles per block would leave the last round of blocks mostly empty and pay a prologue and an
 // epilogue per tile).  The grid is one block per CU; the ntiles * nk K-steps are cut into equal
@@ -2694,6 +2851,67 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   return 0;
 }
 
+// ---- gemm8n_kernel plans (layer GEMMs, 128 x 64*CB tiles) ----------------------------------------
+// DTC_GEMM8N bit mask: 1 = forwards and NT dgrads (layout 0), 2 = NN dgrads (layout 1), 4 = also
+// multi-round problems.  A problem takes it when its tile count on 128x192 (CB 3) or 128x256 (CB 4)
+// tiles is exactly one round of 256 (the d_model-wide outputs of GPT-2 small / medium at 8192 tokens:
+// out_proj / fc2 forwards, qkv / fc1 / out_proj dgrads).  Measured (profiles/r3_gemm8n.md): one round
+// wins (fc1 NT dgrad 60.8 -> 44.9 us, fc2 forward 63.5 -> 49.5 us); 3-4 rounds lose to the 128^2 /
+// 256^2 kernels (fc1 forward 75.6 -> 85.6 us: each round pays its own prologue fill and epilogue at
+// one block per CU), and so does a vocab-sized K (the lm_head dgrad keeps its split-K 256^2 kernel).
+static int g_n8_mask = [] { const char* v = getenv("DTC_GEMM8N"); return v ? atoi(v) : 3; }();
+
+static int n8_cb(int layout, int M, int N, int K, int epi) {
+  if (layout > 1 || !(g_n8_mask & (1 << layout)) || K % 64 || K > 8192 || M < 128) return 0;
+  if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU && epi != EPI_DGELU) return 0;
+  const long tm = (M + 127) / 128;
+  for (int cb : {3, 4}) {
+    const int bn = 64 * cb;
+    if (N % bn) continue;
+    const long t = tm * (N / bn);
+    if (t == 256 || ((g_n8_mask & 4) && t >= 256 && t % 256 == 0)) return cb;
+  }
+  return 0;
+}
+
+template <int CB, bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_n8(const GemmArgs& a, hipStream_t st) {
+  Epi e{};
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
+  const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / (64 * CB);
+  // an XCD's ~32 concurrent tiles = 8 M-tiles x 4 N-tiles (A panel and B panel both shared)
+  const int gm = tiles_n <= 4 ? std::max(1, std::min(tiles_m, 32 / tiles_n)) : std::min(tiles_m, 8);
+  constexpr int NS = CB == 3 ? 4 : 3;
+  hipLaunchKernelGGL((gemm8n_kernel<CB, NS, AK, BKM, EPI, OUTF32>), dim3(tiles_m * tiles_n), dim3(NT2), 0, st,
+                     (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, e);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_n8cb(const GemmArgs& a, int cb, hipStream_t st) {
+  return cb == 3 ? launch_n8<3, AK, BKM, EPI, OUTF32>(a, st) : launch_n8<4, AK, BKM, EPI, OUTF32>(a, st);
+}
+
+// the (layout, epilogue, output) combinations the layer GEMMs use; -1 = not instantiated
+int launch_n8_any(const GemmArgs& a, int cb, hipStream_t st) {
+  const int epi = a.epi;
+  const bool f32 = a.c_f32 != 0;
+  if (a.layout == 0) {
+    if (epi == EPI_STORE) return f32 ? launch_n8cb<true, true, EPI_STORE, true>(a, cb, st)
+                                     : launch_n8cb<true, true, EPI_STORE, false>(a, cb, st);
+    if (epi == EPI_RESID && f32) return launch_n8cb<true, true, EPI_RESID, true>(a, cb, st);
+    if (epi == EPI_GELU && !f32) return launch_n8cb<true, true, EPI_GELU, false>(a, cb, st);
+    if (epi == EPI_DGELU && !f32) return launch_n8cb<true, true, EPI_DGELU, false>(a, cb, st);
+  } else if (a.layout == 1 && a.N % 8 == 0) {
+    if (epi == EPI_STORE) return f32 ? launch_n8cb<true, false, EPI_STORE, true>(a, cb, st)
+                                     : launch_n8cb<true, false, EPI_STORE, false>(a, cb, st);
+    if (epi == EPI_DGELU && !f32) return launch_n8cb<true, false, EPI_DGELU, false>(a, cb, st);
+  }
+  return -1;
+}
+
 // Paired launch: a1 = dgrad (layout 1, whole-K tiles), a2 = weight gradient (layout 2, split-K slabs
 // left for the caller's batched reducer when split > 1).  Only register-staged, BK = 64 plans pair.
 template <class C1, class C2, int BM1, int BM2, bool BKM1 = false>
@@ -2844,6 +3062,7 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   if (a1->M <= 0 || a1->N <= 0 || a2->M <= 0 || a2->N <= 0) return 1100;
   if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
   if (big_split(a1->layout, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
+  if (n8_cb(a1->layout, a1->M, a1->N, a1->K, a1->epi)) return 1100;  // dgrad on gemm8n_kernel: own launch
   if (sk_wanted(a1->layout, a1->M, a1->N, a1->K) && a1->colsum == nullptr) return 1100;  // stream-K dgrad: own launch
   if (dmaw_plan(a1->layout, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
       dmaw_plan(2, a2->M, a2->N, a2->K, a2->epi, a2->c_f32 != 0, a2->colsum != nullptr).cfg != W_NONE)
@@ -2977,6 +3196,13 @@ long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   return split > 1 ? (long)split * M * N * 4 : 0;
 }
 
+// gemm8n layout mask (DTC_GEMM8N at load time); returns the previous mask (tests / A/B)
+int dtc_gemm_set_n8(int mask) {
+  const int old = g_n8_mask;
+  g_n8_mask = mask;
+  return old;
+}
+
 // stream-K layout mask (DTC_GEMM_SK at load time); returns the previous mask (tests / A/B)
 int dtc_gemm_set_sk(int mask) {
   const int old = g_sk_mask;
@@ -2990,6 +3216,13 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
+  if (a->layout <= 1 && !a->colsum && a->alpha == 1.f) {
+    const int cb = n8_cb(a->layout, a->M, a->N, a->K, epi);
+    if (cb) {
+      const int r = launch_n8_any(*a, cb, st);
+      if (r >= 0) return r;
+    }
+  }
   if (a->layout <= 1 && !a->colsum && sk_wanted(a->layout, a->M, a->N, a->K)) {
     int r = -2;
     if (a->layout == 0) {
