@@ -1496,13 +1496,24 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   const int ntiles = tiles_m * tiles_n;
-  const int tile = xcd_remap(blockIdx.x, ntiles);
-  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
-  const int gm_eff = min(gm, tiles_m - grp * gm);
-  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
-  const int m0 = tm_idx * 128, n0 = tn_idx * BN;
+  // persistent: block b runs tiles bl, bl + G, ... (round r of the grid = tiles [rG, rG + G), the
+  // same XCD-grouped order a one-tile-per-block launch would use); its K-steps form ONE stream, so
+  // the next tile's first stages load under the current tile's last K-steps and its epilogue stores
+  // drain under the next tile's MFMAs
+  const int G = gridDim.x;
+  const int bl = xcd_remap(blockIdx.x, G);
   const int nk = K / 64;
   DTC_ASSERT(nk >= 1);
+  const int nr = bl < ntiles ? (ntiles - bl + G - 1) / G : 0;
+  const int S = nr * nk;
+  if (S == 0) return;
+  auto origin = [&](int r, int& m0, int& n0) {
+    const int tile = bl + r * G;
+    const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+    const int gm_eff = min(gm, tiles_m - grp * gm);
+    m0 = (grp * gm + in_g % gm_eff) * 128;
+    n0 = (in_g / gm_eff) * BN;
+  };
 
   f32x4 acc[TN][TM];
 #pragma unroll
@@ -1512,26 +1523,31 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 
   auto imgA = [&](int s) { return smem + (s % NS) * SIMG; };
   auto imgB = [&](int s) { return smem + (s % NS) * SIMG + CA * P8_CHUNK; };
-  auto dmaA = [&](int s, int q) { p8_dma<AK>(A, lda, m0, M, s * 64, imgA(s), q, wave, lane); };
-  auto dmaB = [&](int s, int q) { p8_dma<BKM>(B, ldb, n0, N, s * 64, imgB(s), q, wave, lane); };
+  // stage s = (round s / nk, K-step s % nk)
+  auto dmaA = [&](int s, int m0, int q) { p8_dma<AK>(A, lda, m0, M, (s % nk) * 64, imgA(s), q, wave, lane); };
+  auto dmaB = [&](int s, int n0, int q) { p8_dma<BKM>(B, ldb, n0, N, (s % nk) * 64, imgB(s), q, wave, lane); };
 
   // prologue: stages 0..D-1 (B then A each), wait for stage 0
-  const int npro = min(D, nk);
+  const int npro = min(D, S);
   for (int s = 0; s < npro; ++s) {
+    int m0, n0;
+    origin(s / nk, m0, n0);
 #pragma unroll
-    for (int q = 0; q < CB; ++q) dmaB(s, q);
+    for (int q = 0; q < CB; ++q) dmaB(s, n0, q);
 #pragma unroll
-    for (int q = 0; q < CA; ++q) dmaA(s, q);
+    for (int q = 0; q < CA; ++q) dmaA(s, m0, q);
   }
   n8_vmcnt((npro - 1) * PIECES);
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // second wave group: one barrier behind
 
   bf16x8 fb[TN][2], fa[2][2];
-  for (int t = 0; t < nk; ++t) {
+  for (int t = 0; t < S; ++t) {
     const bf16* sA = imgA(t);
     const bf16* sB = imgB(t);
-    const bool issue = t + D < nk;
+    const bool issue = t + D < S;
+    int pm0 = 0, pn0 = 0;  // origin of the stage issued this step
+    if (issue) origin((t + D) / nk, pm0, pn0);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       if (p == 0) {
@@ -1547,10 +1563,10 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
       if (issue) {
         if (p == 0) {
 #pragma unroll
-          for (int q = 0; q < CB; ++q) dmaB(t + D, q);
+          for (int q = 0; q < CB; ++q) dmaB(t + D, pn0, q);
         } else {
 #pragma unroll
-          for (int q = 0; q < CA; ++q) dmaA(t + D, q);
+          for (int q = 0; q < CA; ++q) dmaA(t + D, pm0, q);
         }
       }
       __builtin_amdgcn_s_barrier();
@@ -1572,37 +1588,45 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
           for (int jj = 0; jj < 2; ++jj)
             acc[i][2 * p + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i][kk], fa[jj][kk], acc[i][2 * p + jj], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if (p == 0 && t + 1 < nk) {
+      if (p == 0 && t + 1 < S) {
         // retire stage t+1: younger than its A pieces are the stages t+2 .. t+D-1 that exist, and
-        // B(t+D) when it was issued this phase
-        if (t + D < nk) {
+        // B(t+D) when it was issued this phase.  An epilogue's loads / stores issued since are extra
+        // younger operations: they only make this wait stricter (never early)
+        if (t + D < S) {
           n8_vmcnt((D - 2) * PIECES + CB);  // constant: folds to one s_waitcnt
         } else {
-          const int full = max(0, min(t + D - 1, nk - 1) - (t + 1));
+          const int full = max(0, min(t + D - 1, S - 1) - (t + 1));
           n8_vmcnt(full * PIECES);
         }
       }
       __builtin_amdgcn_s_barrier();
     }
+    if (t % nk == nk - 1) {  // last K-step of a tile: its epilogue from registers (no LDS), then restart
+      int m0, n0;
+      origin(t / nk, m0, n0);
+      const int g4 = 4 * (lane >> 4);
+      if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            const int m = m0 + wr * 64 + j * 16 + (lane & 15);
+            const int n = n0 + wc * 16 * TN + i * 16 + g4;
+            if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the second group's extra barrier
-
-  const int g4 = 4 * (lane >> 4);
-  if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wr * 64 + j * 16 + (lane & 15);
-      const int n = n0 + wc * 16 * TN + i * 16 + g4;
-      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
-    }
 }
 
 // ============================================================================================
@@ -2716,6 +2740,8 @@ int launch_sz(const GemmArgs& a, const Plan& p, hipStream_t st) {
 // split so ~256 blocks run (so does layout 0 at K >= 16384: the same dgrad as an NT GEMM on a
 // transposed lm_head weight, ~25% faster main loop with both operands K-major); layout 2 (wgrad): no split (a 103 MB fp32 output; extra slab passes
 // cost more than the last partial wave of tiles).
+static int g_wgrad256 = [] { const char* v = getenv("DTC_WGRAD256"); return v ? atoi(v) : 0; }();
+
 int big_split(int layout, int M, int N, int K) {
   // DTC_GEMM256: bit mask of layouts allowed to use it (1 fwd, 2 dgrad, 4 wgrad; default all)
   static const int enabled = [] { const char* v = getenv("DTC_GEMM256"); return v ? atoi(v) : 7; }();
@@ -2724,7 +2750,15 @@ int big_split(int layout, int M, int N, int K) {
   if (layout == 2 && M % 8) return 0;              // MN-major A extent (wgrad)
   static const int min_tiles = [] { const char* v = getenv("DTC_BIG_MIN_TILES"); return v ? atoi(v) : 512; }();
   const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
-  if (layout == 2) return (t >= 256 && K >= 1024) ? 1 : 0;
+  if (layout == 2) {
+    if (t >= 256 && K >= 1024) return 1;
+    // DTC_WGRAD256=1: layer weight gradients (K = tokens, a few dozen 256^2 tiles) split-K across
+    // ~256 blocks of >= 8 K-steps on this kernel, fp32 slabs summed by the caller's reducer
+    if (!g_wgrad256 || t < 8 || K < 4096) return 0;
+    int split = (int)std::max(1L, 256 / t);
+    while (split > 1 && (K / 64) / split < 8) --split;
+    return split > 1 ? split : 0;
+  }
   // ordinary K: whole tiles, when there are enough of them, or when the last round of 256^2 tiles is
   // nearly empty anyway (GPT-2 small qkv forward: 288 tiles = 1.125 rounds, 54.7 -> 47.7 us;
   // fc1's 384 = 1.5 rounds stays on the 128^2 kernel: 76 vs 85 us, profiles/r3_gemm_bench_gpt2s*.log)
@@ -2883,7 +2917,8 @@ int launch_n8(const GemmArgs& a, hipStream_t st) {
   // an XCD's ~32 concurrent tiles = 8 M-tiles x 4 N-tiles (A panel and B panel both shared)
   const int gm = tiles_n <= 4 ? std::max(1, std::min(tiles_m, 32 / tiles_n)) : std::min(tiles_m, 8);
   constexpr int NS = CB == 3 ? 4 : 3;
-  hipLaunchKernelGGL((gemm8n_kernel<CB, NS, AK, BKM, EPI, OUTF32>), dim3(tiles_m * tiles_n), dim3(NT2), 0, st,
+  const int grid = std::min(tiles_m * tiles_n, sk_cus());  // persistent: one block per CU
+  hipLaunchKernelGGL((gemm8n_kernel<CB, NS, AK, BKM, EPI, OUTF32>), dim3(grid), dim3(NT2), 0, st,
                      (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, e);
   DTC_CHECK_LAUNCH();
   return 0;
@@ -3171,7 +3206,7 @@ int dtc_lmhead_nparts(int M, int N, int K) { return big_split(0, M, N, K) ? ((N 
 // split-K factor dtc_gemm will use for a weight-gradient (layout 2) problem (1 = none); has_db: the
 // caller wants the bias gradient fused (GemmArgs.colsum), which pins the register-staged kernel
 int dtc_gemm_wgrad_split(int M, int N, int K, int has_db) {
-  if (big_split(2, M, N, K)) return 1;
+  if (const int bs = big_split(2, M, N, K)) return bs;
   if (!has_db) {
     const WPlan w = dmaw_plan(2, M, N, K, EPI_STORE, true, false);
     if (w.cfg != W_NONE) return w.split;
@@ -3194,6 +3229,13 @@ long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   int split = bs ? bs : p.split;
   if (layout == 2 && !bs) split = std::max(split, dmaw_plan(2, M, N, K, EPI_STORE, true, false).split);
   return split > 1 ? (long)split * M * N * 4 : 0;
+}
+
+// weight gradients split-K on the 256^2 kernel (DTC_WGRAD256 at load time); returns the previous value
+int dtc_gemm_set_wgrad256(int on) {
+  const int old = g_wgrad256;
+  g_wgrad256 = on;
+  return old;
 }
 
 // gemm8n layout mask (DTC_GEMM8N at load time); returns the previous mask (tests / A/B)
@@ -3236,7 +3278,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
     }
     if (r >= 0) return r;
   }
-  if (a->layout <= 2 && !(a->layout == 2 && a->bias)) {
+  if (a->layout <= 2 && !(a->layout == 2 && (a->bias || big_split(2, a->M, a->N, a->K)))) {
     const WPlan w = dmaw_plan(a->layout, a->M, a->N, a->K, epi, f32, a->colsum != nullptr);
     if (w.cfg != W_NONE) {
       if (a->layout == 0) {
@@ -3298,7 +3340,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
     if (a->M % 8 || a->N % 8) return 1004;
     if (epi != EPI_STORE || !f32 || a->bias) return 1003;
     if (a->colsum && !dtc_gemm_wgrad_fuses_colsum(a->M, a->N, a->K)) return 1009;
-    if (big_split(2, a->M, a->N, a->K)) return launch_big<false, false, EPI_STORE, true>(*a, 1, st);
+    if (const int bs = big_split(2, a->M, a->N, a->K)) return launch_big<false, false, EPI_STORE, true>(*a, bs, st);
     Plan p = make_plan(a->M, a->N, a->K, 1);
     if (p.split > 1 && a->ws_bytes < (long)p.split * a->M * a->N * 4) return 1005;
     return launch_sz<false, false, EPI_STORE, true>(*a, p, st);

@@ -95,3 +95,32 @@ def test_n8_selection(n8):
     torch.cuda.synchronize()
     _close(dx, dy.float() @ w.float(), 2e-3, "pair_dx")
     _close(dw, dy.float().t() @ x.float(), 2e-3, "pair_dw")
+
+
+WGRAD = [(2304, 768, 8192), (3072, 768, 8192), (768, 3072, 8192), (768, 768, 8192)]
+
+
+@pytest.mark.parametrize("Nn,K,M", WGRAD)
+def test_wgrad_split256(cuda, Nn, K, M):
+    """Layer weight gradients split-K on the 256^2 kernel (DTC_WGRAD256): fp32 slabs summed by the
+    reducer, bias gradient by the separate column sum; against fp32 torch and the default plan."""
+    from distributed_training_compare_jax_amd.ops.reduce import GradReducer
+    L = N.lib()
+    dy, x = _r(M, Nn, seed=11), _r(M, K, seed=12)
+    ref = dy.float().t() @ x.float()
+    outs = []
+    for on in (1, 0):
+        old = L.dtc_gemm_set_wgrad256(on)
+        try:
+            red = GradReducer(torch.device("cuda"), arena_mb=128)
+            dw = torch.full((Nn, K), 0.5, device="cuda")
+            db = torch.full((Nn,), 0.25, device="cuda")
+            G.wgrad(dy, x, dw, beta=1.0, red=red, db=db)
+            red.flush_all()
+            torch.cuda.synchronize()
+        finally:
+            L.dtc_gemm_set_wgrad256(old)
+        _close(dw, ref + 0.5, 2e-3, f"dw(w256={on})")
+        _close(db, dy.float().sum(0) + 0.25, 2e-3, f"db(w256={on})")
+        outs.append(dw)
+    _close(outs[0], outs[1], 1e-4, "split256_vs_default")
