@@ -1257,6 +1257,25 @@ __device__ __forceinline__ void p8_dma(const bf16* __restrict__ X, long ldx, int
   }
 }
 
+// the per-lane source address p8_dma uses for chunk q at k0 = 0 (a K-step adds k0, or k0 * ldx
+// for an MN-major operand): kernels that keep it in registers pay one add per DMA instruction
+template <bool KMAJ>
+__device__ __forceinline__ const bf16* p8_src(const bf16* __restrict__ X, long ldx, int r0, int rmax, int q, int wave,
+                                              int lane) {
+  if (KMAJ) {
+    const int r = wave * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    return X + (long)min(r0 + 64 * q + r, rmax - 1) * ldx + c * 8;
+  }
+  const int kr = wave * 8 + (lane >> 3);
+  const int pc = (lane & 7) ^ mn8_swz(kr);
+  return X + (long)kr * ldx + min(r0 + 64 * q + 8 * pc, rmax - 8);
+}
+
+__device__ __forceinline__ void p8_dma_at(const bf16* src, bf16* img, int q, int wave) {
+  __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(img + q * P8_CHUNK + wave * 512), 16, 0, 0);
+}
+
 // ds_read_b64_tr_b16 as inline asm: hipcc puts an s_waitcnt vmcnt(0) in front of every builtin
 // transpose read while an LDS-DMA is in flight (it does not for ds_read_b128), which drained the
 // whole DMA pipeline each phase of the MN-major kernels.  The compiler does not count these reads:
@@ -1465,6 +1484,9 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 //    is retired by a counted vmcnt at the end of phase 0 of step t, one full phase before its first
 //    read (the staggered wave group reads it one barrier later).  Never vmcnt(0) in steady state.
 //  * NS = 4 for CB = 3 (160 KB: the whole LDS), 3 for CB = 4 (144 KB).
+template <int N>  // s_waitcnt vmcnt(N), N a compile-time count
+__device__ __forceinline__ void vmcnt_c() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
 __device__ __forceinline__ void n8_vmcnt(int n) {  // s_waitcnt vmcnt(n), n a runtime value <= 18
   switch (n) {
     case 0: P8_VMCNT(0); break;
@@ -1521,33 +1543,58 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto imgA = [&](int s) { return smem + (s % NS) * SIMG; };
+  auto imgA = [&](int s) { return smem + (s % NS) * SIMG; };  // NS constant: no division
   auto imgB = [&](int s) { return smem + (s % NS) * SIMG + CA * P8_CHUNK; };
-  // stage s = (round s / nk, K-step s % nk)
-  auto dmaA = [&](int s, int m0, int q) { p8_dma<AK>(A, lda, m0, M, (s % nk) * 64, imgA(s), q, wave, lane); };
-  auto dmaB = [&](int s, int n0, int q) { p8_dma<BKM>(B, ldb, n0, N, (s % nk) * 64, imgB(s), q, wave, lane); };
+  // stage s = (round s / nk, K-step s % nk).  The issue side walks the stream with its own counters
+  // (round pr, K-step pk, tile origin pm0 / pn0): no runtime integer division in the loop
+  // per-lane DMA source pointers of the issue side's tile (recomputed only at tile boundaries) plus
+  // the running K offset: one 64-bit add per DMA instruction in the loop
+  int pr = 0, pk = 0;
+  const bf16* srcA[CA];
+  const bf16* srcB[CB];
+  long offA = 0, offB = 0;
+  const long stepA = AK ? 64 : 64 * lda, stepB = BKM ? 64 : 64 * ldb;
+  auto set_src = [&](int r) {
+    int m0, n0;
+    origin(r, m0, n0);
+#pragma unroll
+    for (int q = 0; q < CA; ++q) srcA[q] = p8_src<AK>(A, lda, m0, M, q, wave, lane);
+#pragma unroll
+    for (int q = 0; q < CB; ++q) srcB[q] = p8_src<BKM>(B, ldb, n0, N, q, wave, lane);
+    offA = offB = 0;
+  };
+  set_src(0);
+  auto advance = [&]() {
+    offA += stepA;
+    offB += stepB;
+    if (++pk == nk) {
+      pk = 0;
+      ++pr;
+      if (pr < nr) set_src(pr);
+    }
+  };
+  auto dmaA = [&](int s, int q) { p8_dma_at(srcA[q] + offA, imgA(s), q, wave); };
+  auto dmaB = [&](int s, int q) { p8_dma_at(srcB[q] + offB, imgB(s), q, wave); };
 
   // prologue: stages 0..D-1 (B then A each), wait for stage 0
   const int npro = min(D, S);
   for (int s = 0; s < npro; ++s) {
-    int m0, n0;
-    origin(s / nk, m0, n0);
 #pragma unroll
-    for (int q = 0; q < CB; ++q) dmaB(s, n0, q);
+    for (int q = 0; q < CB; ++q) dmaB(s, q);
 #pragma unroll
-    for (int q = 0; q < CA; ++q) dmaA(s, m0, q);
+    for (int q = 0; q < CA; ++q) dmaA(s, q);
+    advance();
   }
   n8_vmcnt((npro - 1) * PIECES);
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // second wave group: one barrier behind
 
+  int cr = 0, ck = 0;  // consume side: round, K-step
   bf16x8 fb[TN][2], fa[2][2];
   for (int t = 0; t < S; ++t) {
     const bf16* sA = imgA(t);
     const bf16* sB = imgB(t);
     const bool issue = t + D < S;
-    int pm0 = 0, pn0 = 0;  // origin of the stage issued this step
-    if (issue) origin((t + D) / nk, pm0, pn0);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       if (p == 0) {
@@ -1563,10 +1610,11 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
       if (issue) {
         if (p == 0) {
 #pragma unroll
-          for (int q = 0; q < CB; ++q) dmaB(t + D, pn0, q);
+          for (int q = 0; q < CB; ++q) dmaB(t + D, q);
         } else {
 #pragma unroll
-          for (int q = 0; q < CA; ++q) dmaA(t + D, pm0, q);
+          for (int q = 0; q < CA; ++q) dmaA(t + D, q);
+          advance();
         }
       }
       __builtin_amdgcn_s_barrier();
@@ -1593,7 +1641,7 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
         // B(t+D) when it was issued this phase.  An epilogue's loads / stores issued since are extra
         // younger operations: they only make this wait stricter (never early)
         if (t + D < S) {
-          n8_vmcnt((D - 2) * PIECES + CB);  // constant: folds to one s_waitcnt
+          vmcnt_c<(D - 2) * PIECES + CB>();  // steady state: one s_waitcnt, no branch
         } else {
           const int full = max(0, min(t + D - 1, S - 1) - (t + 1));
           n8_vmcnt(full * PIECES);
@@ -1601,9 +1649,10 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
       }
       __builtin_amdgcn_s_barrier();
     }
-    if (t % nk == nk - 1) {  // last K-step of a tile: its epilogue from registers (no LDS), then restart
+    if (++ck == nk) {  // last K-step of a tile: its epilogue from registers (no LDS), then restart
+      ck = 0;
       int m0, n0;
-      origin(t / nk, m0, n0);
+      origin(cr++, m0, n0);
       const int g4 = 4 * (lane >> 4);
       if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
 #pragma unroll
@@ -2740,7 +2789,7 @@ int launch_sz(const GemmArgs& a, const Plan& p, hipStream_t st) {
 // split so ~256 blocks run (so does layout 0 at K >= 16384: the same dgrad as an NT GEMM on a
 // transposed lm_head weight, ~25% faster main loop with both operands K-major); layout 2 (wgrad): no split (a 103 MB fp32 output; extra slab passes
 // cost more than the last partial wave of tiles).
-static int g_wgrad256 = [] { const char* v = getenv("DTC_WGRAD256"); return v ? atoi(v) : 0; }();
+static int g_wgrad256 = [] { const char* v = getenv("DTC_WGRAD256"); return v ? atoi(v) : 1; }();
 
 int big_split(int layout, int M, int N, int K) {
   // DTC_GEMM256: bit mask of layouts allowed to use it (1 fwd, 2 dgrad, 4 wgrad; default all)
@@ -2752,7 +2801,7 @@ int big_split(int layout, int M, int N, int K) {
   const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
   if (layout == 2) {
     if (t >= 256 && K >= 1024) return 1;
-    // DTC_WGRAD256=1: layer weight gradients (K = tokens, a few dozen 256^2 tiles) split-K across
+    // DTC_WGRAD256=1 (default; in-step 14.30 -> 14.23 ms): layer weight gradients (K = tokens, a few dozen 256^2 tiles) split-K across
     // ~256 blocks of >= 8 K-steps on this kernel, fp32 slabs summed by the caller's reducer
     if (!g_wgrad256 || t < 8 || K < 4096) return 0;
     int split = (int)std::max(1L, 256 / t);
@@ -2896,7 +2945,9 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
 static int g_n8_mask = [] { const char* v = getenv("DTC_GEMM8N"); return v ? atoi(v) : 3; }();
 
 static int n8_cb(int layout, int M, int N, int K, int epi) {
-  if (layout > 1 || !(g_n8_mask & (1 << layout)) || K % 64 || K > 8192 || M < 128) return 0;
+  // K >= 1024: at K = 768 (out_proj forward, 12 K-steps) the one-block-per-CU epilogue (fp32 residual
+  // in + out, nothing to hide it under) costs more than the main loop gains (29.2 vs 26.6 us)
+  if (layout > 1 || !(g_n8_mask & (1 << layout)) || K % 64 || K < 1024 || K > 8192 || M < 128) return 0;
   if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU && epi != EPI_DGELU) return 0;
   const long tm = (M + 127) / 128;
   for (int cb : {3, 4}) {
@@ -3116,8 +3167,15 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
 
 // Fused lm_head backward (ce_dgrad256_kernel): dX [M][N] fp32 (= sum of the split-K slabs, written
 // by splitk_reduce), dlogits [M][K] bf16, colpart [2*ceil(M/256)][K] fp32.  K % 64 == 0, N % 8 == 0.
+// split-K of the fused lm_head dgrad: the big_split plan, or DTC_CE_SPLIT when set (A/B)
+static int ce_split(int M, int N, int K) {
+  static const int forced = [] { const char* v = getenv("DTC_CE_SPLIT"); return v ? atoi(v) : 0; }();
+  if (forced > 0) return forced;
+  return std::max(1, big_split(1, M, N, K));
+}
+
 long dtc_ce_dgrad_workspace_bytes(int M, int N, int K) {
-  const int split = big_split(1, M, N, K);
+  const int split = ce_split(M, N, K);
   return split > 1 ? (long)split * M * N * 4 : (long)M * N * 4;
 }
 int dtc_ce_dgrad_colpart_rows(int M) { return 2 * ((M + BIG - 1) / BIG); }
@@ -3126,8 +3184,7 @@ int dtc_ce_dgrad(const bf16* logits, long ldl, const float* lse, const int* labe
                  float scale, const bf16* wt, long ldw, bf16* dlogits, long ldd, float* colpart, float* dx, int M, int N,
                  int K, float* ws, long ws_bytes, hipStream_t st) {
   if (K % 64 || N % 8 || ldl % 8 || ldw % 8 || ldd % 8) return 1300;
-  int split = big_split(1, M, N, K);
-  if (split < 1) split = 1;
+  const int split = ce_split(M, N, K);
   if (ws_bytes < (long)split * M * N * 4) return 1301;
   CeDgradArgs a;
   a.logits = logits; a.ldl = ldl; a.lse = lse; a.labels = labels; a.vocab_start = vocab_start; a.n_valid = n_valid;
