@@ -288,6 +288,33 @@ class Engine:
             O.fill_(self._pending_dev, 0.0)
             self.stage.param_ready.clear()
 
+    class _CommSafeGemms:
+        """GEMM plans for code that runs UNDER asynchronous RCCL collectives (the DP bucket all-reduces
+        during the backward, PP send/recv).  RCCL's kernels hold CUs (and LDS) for the whole transfer;
+        a GEMM built as exactly one round of one-block-per-CU tiles with all 160 KB of LDS (gemm8n) or
+        one ~256-block round of 128 KB-LDS blocks (split-K 256^2 weight gradients) cannot place its last
+        blocks until the collective's CUs free up, and would run about twice as long.  Inside this
+        context those problems take the many-block 128^2 / 256^2 plans that rebalance over the CUs left.
+        No-op on CPU, with a single rank, or with DTC_COMM_SAFE_GEMMS=0."""
+
+        def __init__(self, on: bool):
+            self.on = on and torch.cuda.is_available() and os.environ.get("DTC_COMM_SAFE_GEMMS", "1") == "1"
+
+        def __enter__(self):
+            if self.on:
+                from ..ops import _native as N
+
+                L = N.lib()
+                self.prev = (L.dtc_gemm_set_n8(0), L.dtc_gemm_set_wgrad256(0))
+
+        def __exit__(self, *a):
+            if self.on:
+                from ..ops import _native as N
+
+                L = N.lib()
+                L.dtc_gemm_set_n8(self.prev[0])
+                L.dtc_gemm_set_wgrad256(self.prev[1])
+
     def _step_fn_dp_tp(self):
         st, T, b = self.stage, self.T, self.b_local
         self._launch_deferred_update()
@@ -306,6 +333,11 @@ class Engine:
             # the loss is final here: its DP mean goes out now, under the whole backward, instead of
             # as an exposed collective at the end of the step (joined before the optimizer)
             self._loss_allreduce(name="loss_dp")  # (pp == 1 here)
+        with self._CommSafeGemms(dp > 1 and self.stage.flat.device.type == "cuda"):  # bucket all-reduces overlap it
+            return self._backward_dp_tp(ctx, dp, step, gathered)
+
+    def _backward_dp_tp(self, ctx, dp, step, gathered):
+        st, T, b = self.stage, self.T, self.b_local
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
         bk, opt = self.buckets, self.opt
         side = st.red if st.red is not None else st.side.defer  # where grad-norm chunks are queued
@@ -390,7 +422,8 @@ class Engine:
     def _step_fn_pp(self):
         from ..parallel.pp import run_pipeline
 
-        run_pipeline(self)
+        with self._CommSafeGemms(self.stage.flat.device.type == "cuda"):  # send/recv overlap compute
+            run_pipeline(self)
         self.stage.side.join()
         self.buckets.ready_all()
         # the loss sum overlaps the bucket all-reduces and the optimizer; joined at the very end
