@@ -26,6 +26,7 @@
 #include "common.h"
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -1507,6 +1508,46 @@ __device__ __forceinline__ void n8_vmcnt(int n) {  // s_waitcnt vmcnt(n), n a ru
   }
 }
 
+// compile-time loop: f(integral_constant<I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// One accumulator fragment (row m, columns n..n+3) of the overlapped epilogue: bias and the dGELU
+// factor come from registers, so the only memory operations are the stores.
+template <int EPI, bool OUTF32>
+__device__ __forceinline__ void n8_frag_out(const Epi& e, int m, int n, f32x4 v, f32x4 bias, bf16x4 aux) {
+  float o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = v[r] + bias[r];
+  if (EPI == EPI_DGELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] *= (float)aux[r];
+  }
+  if (OUTF32) {
+    *(f32x4*)((float*)e.C + (long)m * e.ldc + n) = f32x4{o[0], o[1], o[2], o[3]};
+    return;
+  }
+  bf16x4 ob, gb;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (EPI == EPI_GELU) {  // C = gelu'(u), aux_out = gelu(u) (as epilogue_store)
+      float gv, dgv;
+      gelu_tanh_and_grad_f(o[r], gv, dgv);
+      ob[r] = f2bf(dgv);
+      gb[r] = f2bf(gv);
+    } else {
+      ob[r] = f2bf(o[r]);
+    }
+  }
+  *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
+  if (EPI == EPI_GELU) *(bf16x4*)((bf16*)e.aux_out + (long)m * e.ldc + n) = gb;
+}
+
 template <int CB, int NS, bool AK, bool BKM, int EPI, bool OUTF32>
 __global__ void __launch_bounds__(NT2, 1)
 gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
@@ -1542,6 +1583,31 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Overlapped epilogue (bf16 / fp32 stores and the GELU pair: epilogues with no operand to read
+  // but the bias): a finished tile's accumulators move to pacc and are stored two fragments per phase
+  // during the NEXT tile's first NPEEL K-steps, between the MFMA clusters (the staggered wave group
+  // runs its MFMAs meanwhile), instead of stalling all 8 waves at the tile boundary -- at one block
+  // per CU nothing else would hide it.  Those K-steps are peeled (compile-time fragment indices: the
+  // accumulator arrays stay in registers).  The stores are extra younger vector-memory ops for the
+  // counted waits (stricter, never early); the bias is loaded once per tile.  Epilogues that read a
+  // residual / dGELU factor per element keep the immediate form: a load in the loop would make its
+  // use wait for every older in-flight DMA stage.
+  constexpr bool OVL = EPI == EPI_STORE || EPI == EPI_GELU;
+  constexpr int NFRAG = TN * TM, NPEEL = OVL ? NFRAG / 4 : 0;  // 2 fragments per phase, 2 phases per step
+  f32x4 pacc[TN][TM], pbias[TN];
+  bool pend = false;
+  int em0 = 0, en0 = 0;
+  const int g4e = 4 * (lane >> 4);
+  auto epi_frag = [&](auto F) {
+    constexpr int f = decltype(F)::value, i = f / TM, j = f % TM;
+    const int m = em0 + wr * 64 + j * 16 + (lane & 15);
+    const int n = en0 + wc * 16 * TN + i * 16 + g4e;
+    if (m < M) n8_frag_out<EPI, OUTF32>(e, m, n, pacc[i][j], pbias[i], bf16x4{});
+  };
+  int cm0, cn0;  // origin of the tile being computed
+  origin(0, cm0, cn0);
+  DTC_ASSERT(nk >= NPEEL);
 
   auto imgA = [&](int s) { return smem + (s % NS) * SIMG; };  // NS constant: no division
   auto imgB = [&](int s) { return smem + (s % NS) * SIMG + CA * P8_CHUNK; };
@@ -1589,9 +1655,11 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // second wave group: one barrier behind
 
-  int cr = 0, ck = 0;  // consume side: round, K-step
+  int t = 0;  // consume side: K-step of the stream
   bf16x8 fb[TN][2], fa[2][2];
-  for (int t = 0; t < S; ++t) {
+  // one K-step; SL >= 0: also store fragments 4 SL .. 4 SL + 3 of the pending tile
+  auto kstep = [&](auto SLc) {
+    constexpr int SL = decltype(SLc)::value;
     const bf16* sA = imgA(t);
     const bf16* sB = imgB(t);
     const bool issue = t + D < S;
@@ -1636,9 +1704,20 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
           for (int jj = 0; jj < 2; ++jj)
             acc[i][2 * p + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i][kk], fa[jj][kk], acc[i][2 * p + jj], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (SL >= 0) {
+        if (pend) {
+          if (p == 0) {
+            epi_frag(std::integral_constant<int, 4 * SL>{});
+            epi_frag(std::integral_constant<int, 4 * SL + 1>{});
+          } else {
+            epi_frag(std::integral_constant<int, 4 * SL + 2>{});
+            epi_frag(std::integral_constant<int, 4 * SL + 3>{});
+          }
+        }
+      }
       if (p == 0 && t + 1 < S) {
         // retire stage t+1: younger than its A pieces are the stages t+2 .. t+D-1 that exist, and
-        // B(t+D) when it was issued this phase.  An epilogue's loads / stores issued since are extra
+        // B(t+D) when it was issued this phase.  Epilogue loads / stores issued since are extra
         // younger operations: they only make this wait stricter (never early)
         if (t + D < S) {
           vmcnt_c<(D - 2) * PIECES + CB>();  // steady state: one s_waitcnt, no branch
@@ -1649,32 +1728,46 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
       }
       __builtin_amdgcn_s_barrier();
     }
-    if (++ck == nk) {  // last K-step of a tile: its epilogue from registers (no LDS), then restart
-      ck = 0;
-      int m0, n0;
-      origin(cr++, m0, n0);
-      const int g4 = 4 * (lane >> 4);
-      if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
+    ++t;
+  };
+  for (int cr = 0; cr < nr; ++cr) {
+    static_for<0, NPEEL>([&](auto sl) { kstep(sl); });
+    for (int k = NPEEL; k < nk; ++k) kstep(std::integral_constant<int, -1>{});
+    // the tile's last K-step is done: its epilogue (from registers, no LDS), then restart
+    const int m0 = cm0, n0 = cn0;
+    if (cr + 1 < nr) origin(cr + 1, cm0, cn0);
+    const int g4 = 4 * (lane >> 4);
+    if constexpr (OVL) {  // stored during the next tile's first K-steps (after the loop for the last)
 #pragma unroll
-        for (int i = 0; i < TN; ++i)
+      for (int i = 0; i < TN; ++i) {
+        pbias[i] = e.bias ? *(const f32x4*)(e.bias + n0 + wc * 16 * TN + i * 16 + g4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
-      } else {
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int j = 0; j < TM; ++j) {
-            const int m = m0 + wr * 64 + j * 16 + (lane & 15);
-            const int n = n0 + wc * 16 * TN + i * 16 + g4;
-            if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
-          }
+        for (int j = 0; j < TM; ++j) pacc[i][j] = acc[i][j];
       }
+      em0 = m0;
+      en0 = n0;
+      pend = true;
+    } else if constexpr (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int m = m0 + wr * 64 + j * 16 + (lane & 15);
+          const int n = n0 + wc * 16 * TN + i * 16 + g4;
+          if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+        }
     }
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  if constexpr (OVL) static_for<0, NFRAG>([&](auto f) { epi_frag(f); });  // the block's last tile
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the second group's extra barrier
 }
 
@@ -2947,14 +3040,14 @@ static int g_n8_mask = [] { const char* v = getenv("DTC_GEMM8N"); return v ? ato
 static int n8_cb(int layout, int M, int N, int K, int epi) {
   // K >= 1024: at K = 768 (out_proj forward, 12 K-steps) the one-block-per-CU epilogue (fp32 residual
   // in + out, nothing to hide it under) costs more than the main loop gains (29.2 vs 26.6 us)
-  if (layout > 1 || !(g_n8_mask & (1 << layout)) || K % 64 || K < 1024 || K > 8192 || M < 128) return 0;
+  if (layout > 1 || !(g_n8_mask & (1 << layout)) || K % 64 || K < 768 || K > 8192 || M < 128) return 0;
   if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU && epi != EPI_DGELU) return 0;
   const long tm = (M + 127) / 128;
   for (int cb : {3, 4}) {
     const int bn = 64 * cb;
     if (N % bn) continue;
     const long t = tm * (N / bn);
-    if (t == 256 || ((g_n8_mask & 4) && t >= 256 && t % 256 == 0)) return cb;
+    if ((t == 256 && K >= 1024) || ((g_n8_mask & 4) && t > 256 && t % 256 == 0)) return cb;
   }
   return 0;
 }
@@ -3315,7 +3408,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
-  if (a->layout <= 1 && !a->colsum && a->alpha == 1.f) {
+  if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f) {
     const int cb = n8_cb(a->layout, a->M, a->N, a->K, epi);
     if (cb) {
       const int r = launch_n8_any(*a, cb, st);
