@@ -44,7 +44,17 @@ _LMHEAD_WGRAD_MAIN = _os.environ.get("DTC_LMHEAD_WGRAD", "side") == "main"
 # side-stream schedule: 1 = the previous layer's weight gradients are forked one at a time between
 # this layer's dgrad GEMMs; 0 = one fork per layer after its dgrad chain
 _SIDE_INTERLEAVE = _os.environ.get("DTC_SIDE_INTERLEAVE", "0") == "1"  # measured: 1 is slower
-_CE_FUSED = _os.environ.get("DTC_CE_FUSED", "1") == "1"  # ops/xent.py ce_dgrad_fused
+# ops/xent.py ce_dgrad_fused: "1" / "0", or "auto" (default) = fused for lm_head dgrads of at most
+# 4096 x 512 outputs (the reference model: 382 -> 341 us, profiles/r2_ab_ce_fused_dgrad.log); at GPT-2
+# small (8192 x 768: 96 tiles x split 2 = 192 blocks on 256 CUs) the separate CE pass + the DMA-staged
+# 256^2 split-K dgrad measured faster (13.50 vs 13.57 ms, profiles/r3_ab_knobs2.log)
+_CE_FUSED_MODE = _os.environ.get("DTC_CE_FUSED", "auto")
+
+
+def _ce_fused(tokens: int, d: int) -> bool:
+    if _CE_FUSED_MODE == "auto":
+        return tokens * d <= 4096 * 512
+    return _CE_FUSED_MODE == "1"
 # lm_head weight/bias gradients recomputing dlogits from the logits (ops/xent.py ce_wgrad_fused): no
 # tokens x vocab dlogits tensor is written or read (-1.6 GB of HBM traffic per GPT-2 small step) and
 # the bias gradient is summed from fp32 values.  Off by default: the recompute (a second exp pass,
@@ -409,7 +419,8 @@ class GPTStage:
         x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
         wt = f.wt("lm_head.w")  # transposed mirror: NT split-K dgrad, both operands K-major
         red = self.red
-        if wt is not None and _CE_FUSED and logits.is_cuda and _CE_WGRAD and lab.shape[0] % 64 == 0:
+        fused = _ce_fused(x.shape[0], x.shape[1])
+        if wt is not None and fused and logits.is_cuda and _CE_WGRAD and lab.shape[0] % 64 == 0:
             # dx from the fused CE + dgrad kernel; dW / db from the fused CE + weight-gradient kernel:
             # the logits are read twice, no dlogits anywhere
             dyf, dlogits, _ = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt,
@@ -418,7 +429,7 @@ class GPTStage:
                 lg, ls, lb, self.v_start, self.v_valid, grad_scale, y, f.g("lm_head.w"), f.g("lm_head.b"), beta)
             keep = (logits, lse, lab, yf)
         else:
-            if wt is not None and _CE_FUSED and logits.is_cuda:
+            if wt is not None and fused and logits.is_cuda:
                 # CE backward fused into the dgrad's operand staging (no separate dlogits pass)
                 dyf, dlogits, colp = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt)
             else:
