@@ -1367,6 +1367,13 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // second wave group: one barrier behind
 
+  // fused bias gradient of a weight-gradient GEMM (layout TN, e.colsum): column sums over K (tokens) of
+  // the A operand = sum_k A(m, k) * 1, one MFMA of a ones B fragment per A fragment.  Only the n-tile-0
+  // blocks; wave column wc takes the A fragments of phase p = wc (4 MFMAs per K-step per wave, +6 %), so
+  // no wave lags the barriers.  Per split z: colsum[z * M + m] (summed in order by the caller's reducer).
+  const bool do_cs = !AK && EPI == EPI_STORE && OUTF32 && e.colsum != nullptr && tn_idx == 0;
+  const bf16x8 ones = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  f32x4 csacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   bf16x8 fb[TN][2], fa[2][2];
   for (int t = 0; t < nk; ++t) {
     const bf16* sA = imgA(t);
@@ -1401,6 +1408,12 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj)
             acc[i][2 * p + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i][kk], fa[jj][kk], acc[i][2 * p + jj], 0, 0, 0);
+      if (do_cs && p == wc) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) csacc[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fa[jj][kk], csacc[jj], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       if (p == 0) {
         if (more1) P8_VMCNT(6); else P8_VMCNT(0);
@@ -1413,6 +1426,13 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the second group's extra barrier: LDS free after it
 
   const int g4 = 4 * (lane >> 4);
+  if (do_cs && lane < 16) {  // every lane group holds the same sums (the ones operand)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int m = m0 + wr * 128 + (2 * wc + jj) * 16 + lane;
+      if (m < M) e.colsum[(long)z * M + m] = csacc[jj][0];
+    }
+  }
   if (split > 1) {  // fp32 slab z; splitk_reduce sums the slabs in a fixed order
     float* sl = slab + (long)z * M * N;
 #pragma unroll
@@ -2882,6 +2902,8 @@ int launch_sz(const GemmArgs& a, const Plan& p, hipStream_t st) {
 // split so ~256 blocks run (so does layout 0 at K >= 16384: the same dgrad as an NT GEMM on a
 // transposed lm_head weight, ~25% faster main loop with both operands K-major); layout 2 (wgrad): no split (a 103 MB fp32 output; extra slab passes
 // cost more than the last partial wave of tiles).
+// DTC_WGRAD_CS256=0: bias gradients of the split-K 256^2 weight gradients as a separate column sum
+static int g_wgrad_cs256 = [] { const char* v = getenv("DTC_WGRAD_CS256"); return v ? atoi(v) : 1; }();
 static int g_wgrad256 = [] { const char* v = getenv("DTC_WGRAD256"); return v ? atoi(v) : 1; }();
 
 int big_split(int layout, int M, int N, int K) {
@@ -2992,7 +3014,7 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta; e.labels = a.labels; e.vocab_start = a.vocab_start;
   e.n_valid = a.n_valid; e.part = a.part; e.label_out = a.label_out;
-  e.colsum = nullptr;
+  e.colsum = a.colsum;  // fused bias gradient (gemm8p_kernel, layout TN only)
   const int tiles_m = (a.M + BIG - 1) / BIG, tiles_n = (a.N + BIG - 1) / BIG;
   e.nparts = tiles_n * 4;
   const int ntiles = tiles_m * tiles_n;
@@ -3367,7 +3389,8 @@ int dtc_gemm_wgrad_split(int M, int N, int K, int has_db) {
 // 1 if the weight-gradient GEMM runs on the register-staged kernel, which can fuse the bias
 // gradient (GemmArgs.colsum); the 256^2 and DMA kernels cannot
 int dtc_gemm_wgrad_fuses_colsum(int M, int N, int K) {
-  if (big_split(2, M, N, K)) return 0;
+  static const int p8 = [] { const char* v = getenv("DTC_GEMM8P"); return v ? atoi(v) : 2; }();
+  if (big_split(2, M, N, K)) return (p8 == 2 && g_wgrad_cs256) ? 1 : 0;  // gemm8p_kernel sums it with MFMAs
   const Plan p = make_plan(M, N, K, 1);
   if (p.bk != 64) return 1;
   return (gemm_dma_mask() & (p.bm == 64 ? 2 : 4)) ? 0 : 1;
