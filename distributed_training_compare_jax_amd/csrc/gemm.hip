@@ -2929,6 +2929,8 @@ int big_split(int layout, int M, int N, int K) {
   static const int tail_ok = [] { const char* v = getenv("DTC_BIG_TAIL"); return v ? atoi(v) : 64; }();
   if (K < 16384) return (t >= min_tiles || (layout == 0 && t >= 256 && t % 256 <= tail_ok)) ? 1 : 0;
   if (t > 256) return 0;                           // dgrad through the vocab (NN, or NT on W^T): split-K
+  static const int vsplit = [] { const char* v = getenv("DTC_VOCAB_SPLIT"); return v ? atoi(v) : 0; }();
+  if (vsplit > 0) return vsplit;                   // A/B override
   int split = (int)std::max(1L, 256 / t);
   while (split > 1 && (K / 64) / split < 8) --split;
   return split;
