@@ -61,6 +61,14 @@ def _ce_fused(tokens: int, d: int) -> bool:
 # register-staged instead of DMA-staged operand) measured 14.57 vs 14.48 ms (GPT-2 small) and 4.73 vs
 # 4.70 ms (reference model), profiles/r3_ab_ce_wgrad.log
 _CE_WGRAD = _os.environ.get("DTC_CE_WGRAD", "0") == "1"
+# Vocab-chunked lm_head + cross-entropy (DTC_CE_CHUNK = vocab columns per chunk, a multiple of 256; 0 =
+# off): the forward keeps only each chunk's per-row (max, sum exp) and label logit (logits of one chunk
+# at a time), the backward recomputes a chunk's logits, turns them into dlogits in place and runs that
+# chunk's dgrad (accumulated into dX) and weight / bias gradients.  Peak lm_head memory is one
+# tokens x chunk bf16 buffer instead of the full tokens x vocab logits (GPT-2 small: 134 MB at 8192
+# columns vs 824 MB) held from the forward to the backward -- for memory-bound configurations
+# (SURVEY K10 "never materialize full logits"); it costs one extra lm_head GEMM (the recompute).
+_CE_CHUNK = int(_os.environ.get("DTC_CE_CHUNK", "0"))
 
 
 class NoComm:
@@ -403,6 +411,8 @@ class GPTStage:
                                                                      self.act_dtype)
         lab = labels.reshape(-1)
         tp1 = self.tp.size == 1
+        if _CE_CHUNK > 0 and self.v_local > _CE_CHUNK:
+            return self._head_forward_chunked(x, yf, muf, rsf, lab, loss_scale, ctx, loss_out, accumulate)
         logits, rowstat, lab_logit = X.lmhead_logits_partials(yf, f.w("lm_head.w"), f.p("lm_head.b"), lab,
                                                               self.v_start, self.v_valid, combine=not tp1)
         if not tp1:
@@ -414,9 +424,70 @@ class GPTStage:
         ctx["head"] = (x, yf, muf, rsf, logits, lse, lab)
         return loss
 
+    def _chunks(self):
+        """(column offset, columns, valid columns) of each lm_head vocab chunk of this rank's shard."""
+        out = []
+        for c0 in range(0, self.v_local, _CE_CHUNK):
+            vc = min(_CE_CHUNK, self.v_local - c0)
+            out.append((c0, vc, max(0, min(vc, self.v_valid - c0))))
+        return out
+
+    def _head_forward_chunked(self, x, yf, muf, rsf, lab, loss_scale, ctx, loss_out, accumulate):
+        """Vocab-chunked lm_head + CE forward (DTC_CE_CHUNK): per chunk, the lm_head GEMM with the CE
+        partials epilogue into a chunk-sized logits buffer that is dropped right away; the rows'
+        (max, sum exp) of every chunk are combined like vocab-parallel shards (``ce_finalize``)."""
+        f = self.flat
+        w, b = f.w("lm_head.w"), f.p("lm_head.b")
+        stats, lab_logit = [], None
+        for c0, vc, nv in self._chunks():
+            _, rs, ll = X.lmhead_logits_partials(yf, w[c0:c0 + vc], b[c0:c0 + vc], lab, self.v_start + c0, nv,
+                                                 combine=True)
+            stats.append(rs)
+            lab_logit = ll if lab_logit is None else lab_logit + ll
+        rowstat = torch.stack(stats)  # [chunks, M, 2]
+        if self.tp.size > 1:
+            # each rank's chunks combined first, then the shards (as the unchunked vocab-parallel path)
+            lse_l, _ = X.ce_finalize(rowstat, torch.zeros_like(lab_logit), 0.0)
+            one = torch.stack([lse_l, torch.ones_like(lse_l)], -1)  # (max = lse, sum exp = 1) per shard
+            rowstat = self.tp.all_gather_stack(one)
+            self.tp.all_reduce_(lab_logit)
+        lse, loss = X.ce_finalize(rowstat.contiguous(), lab_logit, loss_scale, loss_out, accumulate)
+        ctx["head"] = (x, yf, muf, rsf, None, lse, lab)
+        return loss
+
+    def _head_backward_chunked(self, x, yf, muf, rsf, lse, lab, grad_scale, beta):
+        f = self.flat
+        w, b = f.w("lm_head.w"), f.p("lm_head.b")
+        wt = f.wt("lm_head.w")
+        gw, gb = f.g("lm_head.w"), f.g("lm_head.b")
+        red = self.red
+        dyf = None
+        for c0, vc, nv in self._chunks():
+            logits, _, _ = X.lmhead_logits_partials(yf, w[c0:c0 + vc], b[c0:c0 + vc], lab, self.v_start + c0, nv,
+                                                    combine=True)  # recompute (pad columns -inf)
+            dl, cp = X.ce_backward_inplace(logits, lse, lab, self.v_start + c0, nv, grad_scale, colpart=True)
+            if wt is not None:
+                dyf = G.linear_resid(dl, wt[:, c0:c0 + vc], None, dyf, out=dyf)
+            else:
+                part = G.matmul_nn(dl, w[c0:c0 + vc])
+                dyf = part if dyf is None else dyf.add_(part)
+            G.wgrad(dl, yf, gw[c0:c0 + vc], beta, red=red)
+            G.colsum(cp, gb[c0:c0 + vc], beta, red=red)
+            self.flush_reductions()  # this chunk's split-K slabs: the reducer arena is reused by the next
+            del logits, dl, cp
+        self.tp.all_reduce_(dyf)
+        last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None
+        out = self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
+                           bias_grad=None if last is None else self._prev_fc2b(last))
+        self.side.flush()
+        self.flush_reductions()
+        return out
+
     def head_backward(self, ctx: Dict, grad_scale: float, beta: float):
         f = self.flat
         x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
+        if logits is None:  # vocab-chunked head (DTC_CE_CHUNK)
+            return self._head_backward_chunked(x, yf, muf, rsf, lse, lab, grad_scale, beta)
         wt = f.wt("lm_head.w")  # transposed mirror: NT split-K dgrad, both operands K-major
         red = self.red
         fused = _ce_fused(x.shape[0], x.shape[1])

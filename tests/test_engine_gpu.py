@@ -225,3 +225,31 @@ def test_ln_fusion_matches_unfused(cuda, monkeypatch):
         g3 = res["3"][2][n]
         err = ((g3 - g0).norm() / (g0.norm() + 1e-12)).item()
         assert err < 2e-2, f"{n}: fused vs unfused relative grad difference {err:.3e}"
+
+
+def test_vocab_chunked_head_gpu(cuda, monkeypatch):
+    """DTC_CE_CHUNK on the HIP path (reference model, vocab 50258 padded to 50304, chunks of 8192
+    columns, the last ragged): the first step's gradients match the unchunked head (relative error per
+    parameter; the unchunked reference-model head sums its bias gradient from bf16 dlogits, the chunked
+    one from fp32), and 4 graph-replayed steps give the same losses."""
+    from distributed_training_compare_jax_amd.models import gpt as GPTMOD
+
+    res = []
+    for ch in (0, 8192):
+        monkeypatch.setattr(GPTMOD, "_CE_CHUNK", ch)
+        eng, mc = _engine(cuda, use_graph=True, preset="ref", vocab=50258, batch=2, dropout=0.0)
+        it = get_batch_iterator(2, mc.max_seq_len + 1)
+        losses, g1 = [], None
+        for k in range(4):
+            eng.set_batch(next(it))
+            eng.run_step()
+            losses.append(eng.loss_value())
+            if k == 0:
+                torch.cuda.synchronize()
+                g1 = {n: eng.flat.g(n).float().cpu().clone() for n in eng.flat.slots}
+        res.append((losses, g1))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) < 2e-3 * max(1.0, abs(a)), (res[0][0], res[1][0])
+    for n, g in res[0][1].items():
+        err = (g - res[1][1][n]).norm() / (g.norm() + 1e-12)
+        assert err < 3e-2, f"{n}: relative grad difference {err:.3e}"

@@ -223,3 +223,36 @@ def test_ln_fused_cpu_fallback_and_site_order():
         order += [st._ln_site(l, k, True) for l in reversed(layers) for k in (0, 1)]
         assert order == list(range(4 * len(layers))), order
     assert mc.d_model == 512
+
+
+@pytest.mark.parametrize("chunk", [256, 384])
+def test_vocab_chunked_head_matches_unchunked(monkeypatch, chunk):
+    """DTC_CE_CHUNK: the vocab-chunked lm_head + CE (per-chunk row statistics combined like vocab
+    shards, logits recomputed chunk by chunk in the backward) gives the unchunked loss and gradients;
+    1000 real columns (padded to 1024) -> chunks of 256 (4, the last one 232 valid) or 384 (3, ragged)."""
+    from distributed_training_compare_jax_amd.models import gpt as GPTMOD
+
+    mc = model_config_from_preset("tiny", vocab_size=1000, dropout=0.0)
+    specs = all_param_specs(mc)
+    b = next(get_batch_iterator(4, mc.max_seq_len + 1, vocab=999))
+    ids, lab = torch.from_numpy(b[:, :-1]).contiguous(), torch.from_numpy(b[:, 1:]).contiguous()
+    T = mc.max_seq_len
+    res = []
+    for ch in (0, chunk):
+        monkeypatch.setattr(GPTMOD, "_CE_CHUNK", ch)
+        flat = FlatParams(specs, 0, 1, "cpu", compute_dtype=torch.float32)
+        flat.init_canonical(0)
+        st = GPTStage(mc, flat, StageLayout(range(mc.n_layers), True, True), act_dtype=torch.float32)
+        step = torch.tensor([3])
+        ctx = {}
+        h = st.embed_forward(ids, step, 0, ctx)
+        h = st.stage_forward(h, 4, ctx)
+        loss = st.head_forward(h, lab, 1 / (4 * T), ctx)
+        assert (ctx["head"][4] is None) == (ch > 0)  # chunked: no logits kept for the backward
+        dx, dxc = st.head_backward(ctx, 1 / (4 * T), 0.0)
+        dx, dxc = st.stage_backward(ctx, dx, dxc, 0.0)
+        st.embed_backward(ctx, dx, step, 0.0)
+        res.append((loss.item(), {n: flat.g(n).clone() for n in flat.slots}))
+    assert abs(res[0][0] - res[1][0]) < 1e-5
+    for n in res[0][1]:
+        assert torch.allclose(res[0][1][n], res[1][1][n], rtol=1e-4, atol=1e-6), n
