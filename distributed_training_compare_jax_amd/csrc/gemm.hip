@@ -1310,15 +1310,29 @@ __device__ __forceinline__ void p8_lgkm_wait(bf16x8 (&fa)[2][2], bf16x8 (&fb)[4]
                :
                : "memory");
 }
+__device__ __forceinline__ void p8_lgkm_wait(bf16x8 (&fa)[2][2], bf16x8 (&fb)[3][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                 "+v"(fb[1][0]), "+v"(fb[1][1]), "+v"(fb[2][0]), "+v"(fb[2][1])
+               :
+               : "memory");
+}
 
 #define P8_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
-template <bool AK, bool BKM, int EPI, bool OUTF32>
+template <int N>  // s_waitcnt vmcnt(N), N a compile-time count
+__device__ __forceinline__ void vmcnt_c() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// CB = B chunks of 64 columns: 4 = the 256^2 tile; 3 = 256 x 192 (128 x 48 per wave) for the layer GEMMs
+// whose N = 3072 makes exactly 2 rounds of 256 x 192 tiles (GPT-2 small fc1 forward / fc2 dgrad)
+template <bool AK, bool BKM, int EPI, bool OUTF32, int CB = 4>
 __global__ void __launch_bounds__(NT2, 1)
 gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
               int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
-  constexpr int TM = 8, TN = 4;  // 16x16 fragments per wave: 128 (m) x 64 (n)
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB (the only LDS object)
+  constexpr int TM = 8, TN = CB;  // 16x16 fragments per wave: 128 (m) x 16*CB (n)
+  constexpr int WN = 16 * CB;     // columns per wave
+  static_assert(CB == 4 || (EPI != EPI_LMHEAD), "the CE epilogue assumes 64-column waves");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (4 + CB) * P8_CHUNK];  // [buf][A img | B img] (the only LDS object)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;  // M half (= wave group), 64-column slice
   const int ntiles = tiles_m * tiles_n;
@@ -1327,7 +1341,7 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
   const int gm_eff = min(gm, tiles_m - grp * gm);
   const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
-  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
+  const int m0 = tm_idx * BIG, n0 = tn_idx * (64 * CB);
   const int kbeg = z * k_per_split;
   const int nk = min(k_per_split, K - kbeg) / 64;
   DTC_ASSERT(nk >= 1);
@@ -1338,23 +1352,23 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto imgA = [&](int t) { return smem + (t & 1) * 2 * IMG; };
-  auto imgB = [&](int t) { return smem + (t & 1) * 2 * IMG + IMG; };
+  auto imgA = [&](int t) { return smem + (t & 1) * (4 + CB) * P8_CHUNK; };
+  auto imgB = [&](int t) { return smem + (t & 1) * (4 + CB) * P8_CHUNK + IMG; };
   auto dmaA = [&](int t, int q) { p8_dma<AK>(A, lda, m0, M, kbeg + t * 64, imgA(t), q, wave, lane); };
   auto dmaB = [&](int t, int q) { p8_dma<BKM>(B, ldb, n0, N, kbeg + t * 64, imgB(t), q, wave, lane); };
 
   EpiPre<TN, TM> pre;  // epilogue operands: loaded ahead of every DMA, retired by the prologue wait
   if (split == 1 && (EPI == EPI_LMHEAD || EPI == EPI_STORE))
-    epi_prefetch<TN, TM>(e, m0 + wr * 128, n0 + wc * 64, lane, EPI == EPI_LMHEAD, pre);
+    epi_prefetch<TN, TM>(e, m0 + wr * 128, n0 + wc * WN, lane, EPI == EPI_LMHEAD, pre);
   // prologue: B(0), A(0), B(1) in flight; wait for the first two
 #pragma unroll
-  for (int q = 0; q < 4; ++q) dmaB(0, q);
+  for (int q = 0; q < CB; ++q) dmaB(0, q);
 #pragma unroll
   for (int q = 0; q < 4; ++q) dmaA(0, q);
   if (nk > 1) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dmaB(1, q);
-    P8_VMCNT(4);
+    for (int q = 0; q < CB; ++q) dmaB(1, q);
+    vmcnt_c<CB>();
   } else {
     P8_VMCNT(0);
   }
@@ -1386,7 +1400,7 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 #pragma unroll
         for (int i = 0; i < TN; ++i)
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk) fb[i][kk] = p8_frag<BKM>(sB, 4 * wc + i, kk, lane);
+          for (int kk = 0; kk < 2; ++kk) fb[i][kk] = p8_frag<BKM>(sB, CB * wc + i, kk, lane);
       }
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
@@ -1395,7 +1409,10 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
       if (p < 2) {
         if (more1) { dmaA(t + 1, p); dmaA(t + 1, p + 2); }
       } else {
-        if (more2) { dmaB(t + 2, 2 * p - 4); dmaB(t + 2, 2 * p - 3); }
+        if (more2) {
+          if (2 * p - 4 < CB) dmaB(t + 2, 2 * p - 4);
+          if (2 * p - 3 < CB) dmaB(t + 2, 2 * p - 3);
+        }
       }
       __builtin_amdgcn_s_barrier();
       p8_lgkm_wait(fa, fb);
@@ -1416,7 +1433,7 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
       }
       __builtin_amdgcn_s_setprio(0);
       if (p == 0) {
-        if (more1) P8_VMCNT(6); else P8_VMCNT(0);
+        if (more1) vmcnt_c<CB + 2>(); else P8_VMCNT(0);  // A chunks 1,3 of t landed (B(t+1), A(t+1) 0,2 younger)
       } else if (p == 2) {
         if (more2) P8_VMCNT(4); else if (more1) P8_VMCNT(2); else P8_VMCNT(0);
       }
@@ -1440,17 +1457,17 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         const int m = m0 + wr * 128 + j * 16 + (lane & 15);
-        const int n = n0 + wc * 64 + i * 16 + g4;
+        const int n = n0 + wc * WN + i * 16 + g4;
         if (m < M && n < N) *(f32x4*)(sl + (long)m * N + n) = acc[i][j];  // N % 4 == 0 (checked by host)
       }
     return;
   }
   bf16* stage = smem + wave * (128 * 64);
-  if (EPI == EPI_LMHEAD) {
+  if constexpr (CB == 4 && EPI == EPI_LMHEAD) {
     lmhead_epilogue<TN, TM, true, true>(acc, e, m0 + wr * 128, n0 + wc * 64, tn_idx * 4 + wc, lane, pre, stage);
     return;
   }
-  if (EPI == EPI_STORE && !OUTF32) {
+  if constexpr (CB == 4 && EPI == EPI_STORE && !OUTF32) {
     f32x4 bb[TN];
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
@@ -1483,7 +1500,7 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       int m = m0 + wr * 128 + j * 16 + (lane & 15);
-      int n = n0 + wc * 64 + i * 16 + g4;
+      int n = n0 + wc * WN + i * 16 + g4;
       if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
     }
 }
@@ -1505,9 +1522,6 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 //    is retired by a counted vmcnt at the end of phase 0 of step t, one full phase before its first
 //    read (the staggered wave group reads it one barrier later).  Never vmcnt(0) in steady state.
 //  * NS = 4 for CB = 3 (160 KB: the whole LDS), 3 for CB = 4 (144 KB).
-template <int N>  // s_waitcnt vmcnt(N), N a compile-time count
-__device__ __forceinline__ void vmcnt_c() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
 __device__ __forceinline__ void n8_vmcnt(int n) {  // s_waitcnt vmcnt(n), n a runtime value <= 18
   switch (n) {
     case 0: P8_VMCNT(0); break;
@@ -3115,6 +3129,53 @@ int launch_n8_any(const GemmArgs& a, int cb, hipStream_t st) {
   return -1;
 }
 
+// ---- 256 x 192 tiles on gemm8p_kernel (CB = 3) ------------------------------------------------------
+// DTC_GEMM8P3=1: forwards / dgrads whose N is a multiple of 192 and whose 256 x 192 tile count is a
+// whole number (>= 2) of 256-tile rounds -- GPT-2 small fc1 forward (GELU) and fc2 dgrad (dGELU), N = 3072:
+// 512 tiles, where the 128^2 kernel ran 1536 and the 256^2 one 1.5 rounds.  Measured (profiles/r3_gemm8n.md):
+// fc1 forward 80.2 -> 78.1 us, fc2 dgrad 69.8 -> 78.5 us, whole step 13.22 -> 13.88 ms (the fc2 dgrad also
+// loses its paired weight-gradient launch): off by default.
+static int g_p8cb3 = [] { const char* v = getenv("DTC_GEMM8P3"); return v ? atoi(v) : 0; }();
+
+static bool p8cb3_wanted(int layout, int M, int N, int K, int epi) {
+  if (!g_p8cb3 || layout > 1 || N % 192 || K % 64 || K < 512 || K > 8192) return false;
+  if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU && epi != EPI_DGELU) return false;
+  const long t = (long)((M + BIG - 1) / BIG) * (N / 192);
+  return t >= 512 && t % 256 == 0;
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32>
+int launch_p8cb3(const GemmArgs& a, hipStream_t st) {
+  Epi e{};
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
+  const int tiles_m = (a.M + BIG - 1) / BIG, tiles_n = a.N / 192;
+  const int ntiles = tiles_m * tiles_n;
+  // an XCD's ~32 concurrent tiles: 8 M-tiles x 4 N-tiles
+  const int gm = std::min(tiles_m, 8);
+  hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32, 3>), dim3(ntiles), dim3(NT2), 0, st, (const bf16*)a.A, a.lda,
+                     (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, 1, a.K, (float*)nullptr, e);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int launch_p8cb3_any(const GemmArgs& a, hipStream_t st) {
+  const int epi = a.epi;
+  const bool f32 = a.c_f32 != 0;
+  if (a.layout == 0) {
+    if (epi == EPI_STORE) return f32 ? launch_p8cb3<true, true, EPI_STORE, true>(a, st)
+                                     : launch_p8cb3<true, true, EPI_STORE, false>(a, st);
+    if (epi == EPI_RESID && f32) return launch_p8cb3<true, true, EPI_RESID, true>(a, st);
+    if (epi == EPI_GELU && !f32) return launch_p8cb3<true, true, EPI_GELU, false>(a, st);
+    if (epi == EPI_DGELU && !f32) return launch_p8cb3<true, true, EPI_DGELU, false>(a, st);
+  } else if (a.layout == 1 && a.N % 8 == 0) {
+    if (epi == EPI_STORE) return f32 ? launch_p8cb3<true, false, EPI_STORE, true>(a, st)
+                                     : launch_p8cb3<true, false, EPI_STORE, false>(a, st);
+    if (epi == EPI_DGELU && !f32) return launch_p8cb3<true, false, EPI_DGELU, false>(a, st);
+  }
+  return -1;
+}
+
 // Paired launch: a1 = dgrad (layout 1, whole-K tiles), a2 = weight gradient (layout 2, split-K slabs
 // left for the caller's batched reducer when split > 1).  Only register-staged, BK = 64 plans pair.
 template <class C1, class C2, int BM1, int BM2, bool BKM1 = false>
@@ -3266,6 +3327,7 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
   if (big_split(a1->layout, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
   if (n8_cb(a1->layout, a1->M, a1->N, a1->K, a1->epi)) return 1100;  // dgrad on gemm8n_kernel: own launch
+  if (a1->alpha == 1.f && a1->beta == 0.f && p8cb3_wanted(a1->layout, a1->M, a1->N, a1->K, a1->epi)) return 1100;
   if (sk_wanted(a1->layout, a1->M, a1->N, a1->K) && a1->colsum == nullptr) return 1100;  // stream-K dgrad: own launch
   if (dmaw_plan(a1->layout, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
       dmaw_plan(2, a2->M, a2->N, a2->K, a2->epi, a2->c_f32 != 0, a2->colsum != nullptr).cfg != W_NONE)
@@ -3413,6 +3475,13 @@ int dtc_gemm_set_wgrad256(int on) {
   return old;
 }
 
+// 256 x 192 gemm8p plans (DTC_GEMM8P3 at load time); returns the previous value
+int dtc_gemm_set_p8cb3(int on) {
+  const int old = g_p8cb3;
+  g_p8cb3 = on;
+  return old;
+}
+
 // gemm8n layout mask (DTC_GEMM8N at load time); returns the previous mask (tests / A/B)
 int dtc_gemm_set_n8(int mask) {
   const int old = g_n8_mask;
@@ -3437,6 +3506,10 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
     const int cb = n8_cb(a->layout, a->M, a->N, a->K, epi);
     if (cb) {
       const int r = launch_n8_any(*a, cb, st);
+      if (r >= 0) return r;
+    }
+    if (p8cb3_wanted(a->layout, a->M, a->N, a->K, epi)) {
+      const int r = launch_p8cb3_any(*a, st);
       if (r >= 0) return r;
     }
   }

@@ -98,6 +98,7 @@ def _declare(lib):
         "dtc_gemm_wgrad_split": ([i, i, i, i], i),
         "dtc_gemm_set_sk": ([i], i),
         "dtc_gemm_set_n8": ([i], i),
+        "dtc_gemm_set_p8cb3": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
         "dtc_gemm_pair": ([ctypes.POINTER(GemmArgs), ctypes.POINTER(GemmArgs), vp], i),
         "dtc_gemm_ln": ([ctypes.POINTER(LnArgs), vp], i),
