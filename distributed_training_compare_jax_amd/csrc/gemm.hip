@@ -2815,6 +2815,17 @@ Plan make_plan(int M, int N, int K, int allow_split) {
   return p;
 }
 
+// Tile-group height for grids with many N-tiles (> 16): groups of gm M-tiles sweep the N-tiles, so the
+// blocks an XCD runs at once share gm A panels (L2-resident) and stream the B panels.  Was gm = tiles_m
+// (every M-tile of one N-tile in a row): an XCD then re-fetched all of A for each N-tile -- the GPT-2
+// small fc1 forward / fc2 dgrad (24 N-tiles of 128) pulled 408 MB per call through L2 and the lm_head
+// forward 3.5 GB (rocprofv3 FETCH_SIZE, profiles/r3_gpt2_small_pmc_final.md).  DTC_WIDE_GM: the height
+// (0 = the old tiles_m).
+inline int wide_gm(int tiles_m) {
+  static const int g = [] { const char* v = getenv("DTC_WIDE_GM"); return v ? atoi(v) : 4; }();
+  return g > 0 ? std::min(tiles_m, g) : tiles_m;
+}
+
 // exact byte extent of an operand (rows x K if K-major, K x rows if MN-major) for the buffer range check
 inline int operand_bytes(bool kmajor, int rows, int K, long ld) {
   long n = kmajor ? ((long)(rows - 1) * ld + K) : ((long)(K - 1) * ld + rows);
@@ -2838,7 +2849,7 @@ GemmLaunch make_launch(const GemmArgs& a, const Plan& p) {
   const int nk = a.K / p.bk;
   g.kps = ((nk + p.split - 1) / p.split) * p.bk;
   const int ntiles = g.tiles_m * g.tiles_n;
-  g.gm = g.tiles_m;
+  g.gm = wide_gm(g.tiles_m);
   if (g.tiles_n <= 16) g.gm = std::max(1, std::min(g.tiles_m, (ntiles / 8 + g.tiles_n - 1) / g.tiles_n));
   g.split = p.split;
   g.nblocks = ntiles * p.split;
@@ -2862,7 +2873,7 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   const int kps = ((nk + p.split - 1) / p.split) * p.bk;
   const int ntiles = tiles_m * tiles_n;
   // per-XCD share of tiles = ntiles*split/8: with few N-tiles make each XCD own whole M-row groups
-  int gm = tiles_m;
+  int gm = wide_gm(tiles_m);
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
   dim3 grid(ntiles * p.split);
   const int ab = operand_bytes(AK, a.M, a.K, a.lda), bb = operand_bytes(BKM, a.N, a.K, a.ldb);
@@ -3038,7 +3049,7 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   // ~32 blocks an XCD runs at once, so the N-tiles sharing an A panel run together on one L2 (a group
   // spanning a whole XCD run -- 74 tiles of the lm_head weight gradient -- left 2 of its 3 N-tiles
   // re-fetching their A panel from HBM: 2x FETCH_SIZE, profiles/r3_gemm8p.md)
-  int gm = tiles_m;
+  int gm = wide_gm(tiles_m);
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, 32 / tiles_n));
   const int kps = big_kps(a.K, split);
   if (split > 1 && (a.ws_bytes < (long)split * a.M * a.N * 4 || a.N % 4)) return 1005;
@@ -3280,7 +3291,7 @@ int launch_w(const GemmArgs& a, int split, hipStream_t st) {
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   e.nparts = tiles_n * WGN;
   const int ntiles = tiles_m * tiles_n;
-  int gm = tiles_m;
+  int gm = wide_gm(tiles_m);
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
   const int nk = a.K / 64;
   const int kps = ((nk + split - 1) / split) * 64;

@@ -1,0 +1,5 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+PMC_TAG=cur bash scripts/pmc_step.sh || exit $?
+python scripts/pmc_summary.py gpurun_out --tag cur --out gpurun_out/pmc_cur.md --title "GPT-2 small step, round-3 final kernels: hardware counters (rocprofv3 --pmc, 3 passes)" > /dev/null && head -45 gpurun_out/pmc_cur.md
