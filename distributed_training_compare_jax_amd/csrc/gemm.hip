@@ -2822,7 +2822,7 @@ Plan make_plan(int M, int N, int K, int allow_split) {
 // forward 3.5 GB (rocprofv3 FETCH_SIZE, profiles/r3_gpt2_small_pmc_final.md).  DTC_WIDE_GM: the height
 // (0 = the old tiles_m).
 inline int wide_gm(int tiles_m) {
-  static const int g = [] { const char* v = getenv("DTC_WIDE_GM"); return v ? atoi(v) : 4; }();
+  static const int g = [] { const char* v = getenv("DTC_WIDE_GM"); return v ? atoi(v) : 3; }();
   return g > 0 ? std::min(tiles_m, g) : tiles_m;
 }
 
