@@ -2943,7 +2943,9 @@ int big_split(int layout, int M, int N, int K) {
     if (t >= 256 && K >= 1024) return 1;
     // DTC_WGRAD256=1 (default; in-step 14.30 -> 14.23 ms): layer weight gradients (K = tokens, a few dozen 256^2 tiles) split-K across
     // ~256 blocks of >= 8 K-steps on this kernel, fp32 slabs summed by the caller's reducer
-    if (!g_wgrad256 || t < 8 || K < 4096) return 0;
+    // K >= 8192 tokens: at the reference model's 4096 the split pieces are 4-8 K-steps and the grid half
+    // empty (whole step 4.65 -> 5.04 ms with it, profiles/r3_ab_ref_regress.log)
+    if (!g_wgrad256 || t < 8 || K < 8192) return 0;
     int split = (int)std::max(1L, 256 / t);
     while (split > 1 && (K / 64) / split < 8) --split;
     return split > 1 ? split : 0;
