@@ -2948,6 +2948,8 @@ int big_split(int layout, int M, int N, int K) {
     if (!g_wgrad256 || t < 8 || K < 8192) return 0;
     int split = (int)std::max(1L, 256 / t);
     while (split > 1 && (K / 64) / split < 8) --split;
+    // fp32 slabs of one problem <= 96 MB (a layer's four weight gradients share the reducer's window)
+    while (split > 1 && (long)split * M * N * 4 > (96L << 20)) --split;
     return split > 1 ? split : 0;
   }
   // ordinary K: whole tiles, when there are enough of them, or when the last round of 256^2 tiles is

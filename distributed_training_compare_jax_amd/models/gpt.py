@@ -153,7 +153,8 @@ class GPTStage:
         # gradient slabs, LN dgamma/dbeta partials, bias column partials, grad-norm chunks) goes
         # into ONE batched launch per layer (ops/reduce.py); with the side stream, per-op kernels
         dev = torch.device(flat.device)
-        self.red = GradReducer(dev) if (dev.type == "cuda" and self.side.stream is None) else None
+        # 512 MB window: a layer's split-K weight-gradient slabs (GPT-2 medium: 4 x ~67 MB) + LN partials
+        self.red = GradReducer(dev, arena_mb=512) if (dev.type == "cuda" and self.side.stream is None) else None
         self._bias_fused = set()  # layers whose fc2.b grad an upstream LN backward already produced
         # deferred optimizer (train/engine.py): params of layer l / "head" become valid when this
         # side-stream event fires; the forward waits on it right before first use

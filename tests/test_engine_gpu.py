@@ -253,3 +253,18 @@ def test_vocab_chunked_head_gpu(cuda, monkeypatch):
     for n, g in res[0][1].items():
         err = (g - res[1][1][n]).norm() / (g.norm() + 1e-12)
         assert err < 3e-2, f"{n}: relative grad difference {err:.3e}"
+
+
+def test_gpt2_medium_steps(cuda):
+    """GPT-2 medium (d 1024, 24 layers, T 1024) through the default plans: eager step, graph capture,
+    replays -- its per-layer split-K weight-gradient slabs must fit the reducer's window (a 256 MB
+    window overflowed at 4 x ~67 MB)."""
+    eng, mc = _engine(cuda, use_graph=True, preset="gpt2-medium", vocab=50258, batch=8, dropout=0.0)
+    it = get_batch_iterator(8, mc.max_seq_len + 1)
+    losses = []
+    for _ in range(3):
+        eng.set_batch(next(it))
+        eng.run_step()
+        losses.append(eng.loss_value())
+    assert all(5.0 < x < 15.0 for x in losses), losses
+    eng.check_health()
