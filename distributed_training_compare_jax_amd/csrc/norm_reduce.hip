@@ -6,50 +6,66 @@
 // dgrad/wgrad GEMM; dgamma/dbeta go through per-block partial slabs + an ordered reduce (no
 // float atomics -> bitwise reproducible).
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
-template <int NV>
+// RPW rows per wave, every row's loads issued before the first reduction (as the backward): with one
+// row per wave a wave had 3 x 16 B in flight per lane and the kernel ran at ~4 TB/s
+template <int NV, int RPW>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                      const float* __restrict__ b, void* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int M, int D, float eps, int out_f32) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= M) return;
   const int D4 = D / 4;
-  const f32x4* xr = (const f32x4*)(x + (long)row * D);
-  f32x4 v[NV], gv[NV], bv[NV];
-  float s = 0.f;
-  // gamma/beta are issued with the row load so their latency hides under the two row reductions
+  f32x4 v[RPW][NV], gv[NV], bv[NV];
+  // gamma/beta are issued with the row loads so their latency hides under the row reductions
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int row = row0 + q;
+    const f32x4* xr = (const f32x4*)(x + (long)min(row, M - 1) * D);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int c = lane + 64 * i;
+      v[q][i] = c < D4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     int c = lane + 64 * i;
-    v[i] = c < D4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
     gv[i] = c < D4 ? ((const f32x4*)g)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
     bv[i] = c < D4 ? ((const f32x4*)b)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int i = 0; i < NV; ++i) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-  const float mean = warp_sum(s) / D;
-  float q = 0.f;
+  for (int q = 0; q < RPW; ++q) {
+    const int row = row0 + q;
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    int c = lane + 64 * i;
-    if (c < D4) {
-      f32x4 d = v[i] - mean;
-      q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    for (int i = 0; i < NV; ++i) s += v[q][i][0] + v[q][i][1] + v[q][i][2] + v[q][i][3];
+    const float mean = warp_sum(s) / D;
+    float qs = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int c = lane + 64 * i;
+      if (c < D4) {
+        f32x4 d = v[q][i] - mean;
+        qs += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+      }
     }
-  }
-  const float rstd = rsqrtf(warp_sum(q) / D + eps);
-  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+    const float rstd = rsqrtf(warp_sum(qs) / D + eps);
+    if (row >= M) continue;
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    int c = lane + 64 * i;
-    if (c < D4) {
-      f32x4 o = (v[i] - mean) * rstd * gv[i] + bv[i];
-      if (out_f32) ((f32x4*)((float*)y + (long)row * D))[c] = o;
-      else ((bf16x4*)((bf16*)y + (long)row * D))[c] = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+    for (int i = 0; i < NV; ++i) {
+      int c = lane + 64 * i;
+      if (c < D4) {
+        f32x4 o = (v[q][i] - mean) * rstd * gv[i] + bv[i];
+        if (out_f32) ((f32x4*)((float*)y + (long)row * D))[c] = o;
+        else ((bf16x4*)((bf16*)y + (long)row * D))[c] = bf16x4{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+      }
     }
   }
 }
@@ -312,8 +328,15 @@ int dtc_layernorm_fwd(const float* x, const float* g, const float* b, void* y, f
                       float eps, int out_f32, hipStream_t st) {
   if (D % 4) return 2002;
   int nv = (D / 4 + 63) / 64;
-  dim3 grid((M + 3) / 4);
-  DTC_NV_SWITCH(nv, hipLaunchKernelGGL(ln_fwd_kernel<NVC>, grid, dim3(256), 0, st, x, g, b, y, mean, rstd, M, D, eps, out_f32));
+  // DTC_LN_FWD_RPW: rows per wave (1 or 2)
+  static const int rpw = [] { const char* v = getenv("DTC_LN_FWD_RPW"); return v ? atoi(v) : 1; }();
+  if (rpw == 2) {
+    dim3 grid((M + 7) / 8);
+    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 2>), grid, dim3(256), 0, st, x, g, b, y, mean, rstd, M, D, eps, out_f32));
+  } else {
+    dim3 grid((M + 3) / 4);
+    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 1>), grid, dim3(256), 0, st, x, g, b, y, mean, rstd, M, D, eps, out_f32));
+  }
   DTC_CHECK_LAUNCH();
   return 0;
 }
