@@ -3112,7 +3112,9 @@ int launch_n8(const GemmArgs& a, hipStream_t st) {
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
   const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / (64 * CB);
   // an XCD's ~32 concurrent tiles = 8 M-tiles x 4 N-tiles (A panel and B panel both shared)
-  const int gm = tiles_n <= 4 ? std::max(1, std::min(tiles_m, 32 / tiles_n)) : std::min(tiles_m, 8);
+  static const int n8gm = [] { const char* v = getenv("DTC_N8_GM"); return v ? atoi(v) : 0; }();  // A/B override
+  const int gm = n8gm > 0 ? std::min(tiles_m, n8gm)
+                          : (tiles_n <= 4 ? std::max(1, std::min(tiles_m, 32 / tiles_n)) : std::min(tiles_m, 8));
   constexpr int NS = CB == 3 ? 4 : 3;
   const int grid = std::min(tiles_m * tiles_n, sk_cus());  // persistent: one block per CU
   hipLaunchKernelGGL((gemm8n_kernel<CB, NS, AK, BKM, EPI, OUTF32>), dim3(grid), dim3(NT2), 0, st,
