@@ -28,7 +28,10 @@ are optional and default to the reference behaviour:
   forward in that many layer groups, on its own stream with a capped grid, ``DTC_DEFER_BLOCKS``;
   exact, off by default: measured slower at the reference size because the forward GEMMs run
   ~2x slower while the AdamW blocks share their CUs, ``profiles/r2_ab_defer_optimizer.log``),
-  ``zero_stage`` (1 = ZeRO-1 Adam-state sharding over the DP group, ``ShardedAdamW``; pure DP only).
+  ``zero_stage`` (1 = ZeRO-1 Adam-state sharding over the DP group, ``ShardedAdamW``; pure DP only),
+  ``wgrad_group`` (weight gradients deferred to grouped launches of that many layers, 0 = the whole
+  stage plus the lm_head in one launch, -1 = each Dense's right after its dgrad; None = auto: 0 at
+  dp = 1, 2 under DP so each group's buckets overlap the rest of the backward).
 """
 
 from __future__ import annotations
@@ -123,6 +126,7 @@ class TrainConfig:
     dp_tail_mb: float = 16.0
     dp_embed_gather: bool = True
     zero_stage: int = 0  # 1 = ZeRO-1: Adam state sharded over the DP group (train/optimizer.py)
+    wgrad_group: Optional[int] = None  # deferred grouped weight gradients (models/gpt.py set_wgrad_group)
     warmup_steps: int = 5
     ckpt_every: int = 0
     resume: bool = False

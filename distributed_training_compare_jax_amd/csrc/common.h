@@ -42,6 +42,28 @@ struct GemmArgs {
                      // of A(k, m) — the bias gradient of the same dY, fused into its weight gradient
 };
 
+// Grouped weight gradients (csrc/gemm.hip gemm8p_group_kernel, ops/gemm.py wgrad_group): problem i is
+// dW_i[M][N] (fp32, row-major) = beta*dW_i + A_i^T B_i with A_i = dY_i [K][M] and B_i = X_i [K][N] (bf16,
+// contiguous rows), plus db_i[M] = beta*db_i + sum_k A_i[k][m] when cs != null.  Mirror of ops/gemm.py
+// WgEntry / WgBatch (keep field order and types identical).  Passed by value as the kernel argument.
+struct WgEntry {
+  const bf16* A;
+  const bf16* B;
+  float* C;
+  float* cs;
+  int M, N;
+  int tile0;  // first logical tile (filled by the host entry point)
+  int pad;
+};
+constexpr int WG_MAX = 64;
+struct WgBatch {
+  int n;
+  int K;
+  float beta;
+  int ntiles;
+  WgEntry e[WG_MAX];
+};
+
 // Batched deferred reductions (csrc/norm_reduce.hip reduce_tasks_kernel): one launch finishes
 // every split-K slab / partial-slab reduction and grad-norm partial a backward layer queued.
 enum { RED_WIDE = 0, RED_TALL = 1, RED_SUMSQ = 2 };

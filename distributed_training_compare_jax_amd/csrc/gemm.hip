@@ -158,6 +158,7 @@ struct Epi {
   float* part; int nparts;
   float* label_out;
   float* colsum;
+  int cs_accum;  // colsum IS the bias gradient: colsum[m] = beta*colsum[m] + sum (split == 1 only)
   LnEpi ln;
 };
 
@@ -1325,22 +1326,18 @@ __device__ __forceinline__ void vmcnt_c() { asm volatile("s_waitcnt vmcnt(%0)" :
 
 // CB = B chunks of 64 columns: 4 = the 256^2 tile; 3 = 256 x 192 (128 x 48 per wave) for the layer GEMMs
 // whose N = 3072 makes exactly 2 rounds of 256 x 192 tiles (GPT-2 small fc1 forward / fc2 dgrad)
-template <bool AK, bool BKM, int EPI, bool OUTF32, int CB = 4>
-__global__ void __launch_bounds__(NT2, 1)
-gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
-              int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+// One 256 x 64*CB output tile (tm_idx, tn_idx) of split z: the body of gemm8p_kernel and of the
+// grouped weight-gradient kernel (gemm8p_group_kernel).  All LDS is the one array below.
+template <bool AK, bool BKM, int EPI, bool OUTF32, int CB>
+__device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb,
+                                            int M, int N, int K, int tm_idx, int tn_idx, int z, int split,
+                                            int k_per_split, float* __restrict__ slab, const Epi& e) {
   constexpr int TM = 8, TN = CB;  // 16x16 fragments per wave: 128 (m) x 16*CB (n)
   constexpr int WN = 16 * CB;     // columns per wave
   static_assert(CB == 4 || (EPI != EPI_LMHEAD), "the CE epilogue assumes 64-column waves");
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (4 + CB) * P8_CHUNK];  // [buf][A img | B img] (the only LDS object)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;  // M half (= wave group), 64-column slice
-  const int ntiles = tiles_m * tiles_n;
-  const int lid = xcd_remap(blockIdx.x, ntiles * split);
-  const int tile = lid % ntiles, z = lid / ntiles;
-  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
-  const int gm_eff = min(gm, tiles_m - grp * gm);
-  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
   const int m0 = tm_idx * BIG, n0 = tn_idx * (64 * CB);
   const int kbeg = z * k_per_split;
   const int nk = min(k_per_split, K - kbeg) / 64;
@@ -1447,7 +1444,11 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int m = m0 + wr * 128 + (2 * wc + jj) * 16 + lane;
-      if (m < M) e.colsum[(long)z * M + m] = csacc[jj][0];
+      if (m < M) {
+        float v = csacc[jj][0];
+        if (e.cs_accum && e.beta != 0.f) v += e.beta * e.colsum[m];  // grouped weight gradients: db itself
+        e.colsum[(long)z * M + m] = v;
+      }
     }
   }
   if (split > 1) {  // fp32 slab z; splitk_reduce sums the slabs in a fixed order
@@ -1503,6 +1504,43 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
       int n = n0 + wc * WN + i * 16 + g4;
       if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
     }
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32, int CB = 4>
+__global__ void __launch_bounds__(NT2, 1)
+gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
+              int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
+  const int ntiles = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, ntiles * split);
+  const int tile = lid % ntiles, z = lid / ntiles;
+  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
+  const int gm_eff = min(gm, tiles_m - grp * gm);
+  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
+  gemm8p_tile<AK, BKM, EPI, OUTF32, CB>(A, lda, B, ldb, M, N, K, tm_idx, tn_idx, z, split, k_per_split, slab, e);
+}
+
+// Grouped weight gradients: dW_i = beta*dW_i + dY_i^T X_i (+ db_i = beta*db_i + colsum(dY_i)) for up to
+// WG_MAX problems that share K (the tokens) in ONE launch of whole 256^2 tiles (no split-K, no fp32
+// slabs, no reduction pass).  The backward defers every layer's four weight gradients to here: at
+// K = 8192 tokens a layer's four GEMMs are only 108 tiles, which used to need split-K x 7 across the
+// CUs plus a 400 MB/layer slab reduction (profiles/r3_gpt2_small_profile_final.md: 3.6 ms of a
+// 13.2 ms step); twelve layers together are 1296 whole tiles, ~5 rounds of 256 CUs.
+// Block -> (problem, tile): XCD-remapped logical id, problems back to back, M-tiles fastest (the
+// blocks an XCD runs together share the X panel of one N-tile).
+__global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
+  const int lid = xcd_remap(blockIdx.x, b.ntiles);
+  int i = 0;
+  while (i + 1 < b.n && lid >= b.e[i + 1].tile0) ++i;
+  const WgEntry& w = b.e[i];
+  const int t = lid - w.tile0;
+  const int tiles_m = (w.M + BIG - 1) / BIG;
+  const int tm_idx = t % tiles_m, tn_idx = t / tiles_m;
+  DTC_ASSERT(tn_idx * BIG < w.N);
+  Epi e{};
+  e.M = w.M; e.N = w.N; e.C = w.C; e.ldc = w.N; e.alpha = 1.f; e.beta = b.beta;
+  e.colsum = w.cs; e.cs_accum = 1;
+  gemm8p_tile<false, false, EPI_STORE, true, 4>(w.A, w.M, w.B, w.N, w.M, w.N, b.K, tm_idx, tn_idx, 0, 1, b.K,
+                                                 nullptr, e);
 }
 
 // ============================================================================================
@@ -3511,6 +3549,28 @@ int dtc_gemm_set_sk(int mask) {
   const int old = g_sk_mask;
   g_sk_mask = mask;
   return old;
+}
+
+int dtc_wg_entry_bytes() { return (int)sizeof(WgEntry); }
+int dtc_wg_max() { return WG_MAX; }
+
+// Grouped weight gradients (gemm8p_group_kernel).  Host-side checks: K a positive multiple of 64,
+// M and N multiples of 8 (MN-major operand extents), 16-B aligned operands.
+int dtc_wgrad_group(const WgBatch* in, hipStream_t st) {
+  DTC_HOST_CHECK(in && in->n >= 1 && in->n <= WG_MAX && in->K >= 64 && in->K % 64 == 0);
+  WgBatch b = *in;
+  int t = 0;
+  for (int i = 0; i < b.n; ++i) {
+    WgEntry& w = b.e[i];
+    DTC_HOST_CHECK(w.A && w.B && w.C && w.M >= 8 && w.N >= 8 && w.M % 8 == 0 && w.N % 8 == 0);
+    DTC_HOST_CHECK(((unsigned long)w.A % 16) == 0 && ((unsigned long)w.B % 16) == 0 && ((unsigned long)w.C % 16) == 0);
+    w.tile0 = t;
+    t += ((w.M + BIG - 1) / BIG) * ((w.N + BIG - 1) / BIG);
+  }
+  b.ntiles = t;
+  hipLaunchKernelGGL(gemm8p_group_kernel, dim3(t), dim3(NT2), 0, st, b);
+  DTC_CHECK_LAUNCH();
+  return 0;
 }
 
 int dtc_gemm(const GemmArgs* a, hipStream_t st) {

@@ -33,6 +33,7 @@ from ..ops import layernorm as LN
 from ..ops import ln_fused as LF
 from ..ops import xent as X
 from ..ops.reduce import GradReducer
+from .params import head_split
 from ..parallel.buffers import FlatParams
 
 
@@ -166,15 +167,46 @@ class GPTStage:
         self.act_dtype = act_dtype
         D, H = cfg.d_model, cfg.n_heads
         assert D % H == 0
-        assert H % self.tp.size == 0, f"n_heads {H} not divisible by tp {self.tp.size}"
-        self.heads_local = H // self.tp.size
+        # whole heads per TP rank, uneven when tp does not divide H (models/params.py head_split)
+        self.heads_local = head_split(H, self.tp.size)[self.tp.rank][1]
         self.v_local = cfg.padded_vocab // self.tp.size
         self.v_start = self.tp.rank * self.v_local
         self.v_valid = max(0, min(self.v_local, cfg.vocab_size - self.v_start))
         self.eps = cfg.layernorm_eps
+        # Deferred weight gradients (set_wgrad_group): the dgrad chain runs alone and every (dY, X, dW, db)
+        # of wgrad_group consecutive layers (0 = the whole stage, + the lm_head) goes out as ONE grouped
+        # launch of whole 256^2 tiles (ops/gemm.py wgrad_group) -- single-stream backward only
+        self.wg_group = -1  # -1 = off
+        self.wg_queue = []
         # LayerNorm fused into the layer GEMMs (ops/ln_fused.py), set up by enable_ln_fusion
         self.ln_sync: Optional[LF.LnSync] = None
         self._fuse_fwd = self._fuse_bwd = False
+
+    def set_wgrad_group(self, layers: int):
+        """Defer weight gradients to grouped launches of ``layers`` consecutive layers (0 = all layers of
+        the stage in one launch, with the lm_head's; -1 = off: each Dense's weight gradient right after
+        its dgrad).  Needs the single-stream backward (no side stream)."""
+        self.wg_group = int(layers) if self.side.stream is None else -1
+        return self.wg_group
+
+    @property
+    def _defer_wg(self) -> bool:
+        return self.wg_group >= 0
+
+    def _wg(self, dy, x, dense: str, bias: bool = False):
+        """Queue (or run now) the weight gradient of Dense ``dense`` (+ its bias gradient)."""
+        f = self.flat
+        db = f.g(dense + ".b") if bias else None
+        if self._defer_wg:
+            self.wg_queue.append((dy, x, f.g(dense + ".w"), db))
+        else:
+            G.wgrad(dy, x, f.g(dense + ".w"), self._beta, red=self.red, db=db)
+
+    def flush_wgrads(self, beta: float):
+        """Launch every queued weight gradient (one grouped launch), then the reducer's batched launch."""
+        if self.wg_queue:
+            q, self.wg_queue = self.wg_queue, []
+            G.wgrad_group(q, beta, red=self.red)
 
     def enable_ln_fusion(self, tokens: int, step: torch.Tensor, fwd: bool, bwd: bool) -> bool:
         """Fuse the LayerNorms into the GEMMs that produce their input (forward) and their output
@@ -289,13 +321,23 @@ class GPTStage:
         # dx3 (lnf or the next block's ln1) unless dx3 arrived from another pipeline stage
         fc2b_fused = l in self._bias_fused
         self._bias_fused.discard(l)
-        if side.stream is None:
+        self._beta = beta
+        if side.stream is None and self._defer_wg:
+            # deferred weight gradients: the dgrad chain alone, (dY, X) pairs queued for the grouped launch
+            wt2 = f.wt(p + "fc2.w")
+            du = (G.matmul_nt_dgelu(dx3_c, wt2, u) if wt2 is not None
+                  else G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u))
+            self._wg(dx3_c, gact, p + "fc2")
+            if not fc2b_fused:
+                G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
+        elif side.stream is None:
             # single stream: each Dense's dgrad and weight gradient share one launch
             # (G.linear_backward), weight-gradient reductions go to the layer's batched launch
             # with a transposed fc2 weight the paired dgrad runs NT (+ GELU backward), both operands K-major
             du = G.linear_backward(dx3_c, f.w(p + "fc2.w"), gact, f.g(p + "fc2.w"), beta, red=red, dgelu_u=u,
                                    wt=f.wt(p + "fc2.w"))
-            if not fc2b_fused:
+        if side.stream is None:
+            if not fc2b_fused and not self._defer_wg:
                 G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
             # paired launches measured per Dense (in-step, us): fc2 44.1 vs 46.8 and qkv 35.6 vs 38.1
             # separate; fc1 48.7 vs 48.1 and out_proj 22.4 vs 21.7 -> those two stay separate
@@ -306,7 +348,7 @@ class GPTStage:
                 dx2, dx2_c = LF.dgrad_ln_bwd(du, wt1, x2, f.p(p + "ln2.g"), mu2, rs2, dx3, f.g(p + "ln2.g"),
                                              f.g(p + "ln2.b"), beta, dbias=f.g(p + "out.b"), red=red,
                                              sync=self.ln_sync, site=self._ln_site(l, 0, True))
-                G.wgrad(du, y2, f.g(p + "fc1.w"), beta, red=red, db=f.g(p + "fc1.b"))
+                self._wg(du, y2, p + "fc1", bias=True)
             else:
                 dy2 = self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False)
                 tp.all_reduce_(dy2)
@@ -314,7 +356,10 @@ class GPTStage:
             wto = f.wt(p + "out.w")
             if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
                 do = G.linear(dx2_c, wto)
-                G.wgrad(dx2_c, o, f.g(p + "out.w"), beta, red=red)
+                self._wg(dx2_c, o, p + "out")
+            elif self._defer_wg:
+                do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
+                self._wg(dx2_c, o, p + "out")
             else:
                 do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
                                        out_dtype=self.act_dtype, pair=False)
@@ -328,7 +373,7 @@ class GPTStage:
                                       site=self._ln_site(l, 1, True))
                 if dx_hook is not None:
                     dx_hook(out[0])
-                G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta, red=red, db=f.g(p + "qkv.b"))
+                self._wg(dqkv, y1, p + "qkv", bias=True)
                 return out
             dy1 = self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True)
             tp.all_reduce_(dy1)
@@ -372,6 +417,10 @@ class GPTStage:
         NN dgrad (paired with the weight gradient in one launch when ``pair``)."""
         f = self.flat
         wt = f.wt(dense + ".w")
+        if self._defer_wg:
+            dx = G.linear_resid(dy, wt, None, None) if wt is not None else G.matmul_nn(dy, f.w(dense + ".w"))
+            self._wg(dy, x, dense, bias=True)
+            return dx
         if wt is None:
             return G.linear_backward(dy, f.w(dense + ".w"), x, f.g(dense + ".w"), beta, red=red, db=f.g(dense + ".b"),
                                      pair=pair)
@@ -515,7 +564,15 @@ class GPTStage:
             wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
                                                     G.colsum(cp, f.g("lm_head.b"), beta, red=red))
             keep = (dlogits, yf, colp)
-        if _LMHEAD_WGRAD_MAIN:
+            if self._defer_wg and self.side.stream is None:
+                # the bias gradient from the CE pass's fp32 column partials now; the weight gradient joins
+                # the grouped launch (its 591 tiles at GPT-2 small fill the layers' last round)
+                G.colsum(colp, f.g("lm_head.b"), beta, red=red)
+                self.wg_queue.append((dlogits, yf, f.g("lm_head.w"), None))
+                wg = None
+        if wg is None:
+            pass
+        elif _LMHEAD_WGRAD_MAIN:
             wg()
         else:
             self.side.defer(wg, *keep)
@@ -537,14 +594,30 @@ class GPTStage:
         """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist,
         ``dx_hook(dx)`` as soon as the stage's input gradient is final (inside the first layer)."""
         first = self.layout.layers[0] if len(self.layout.layers) else None
+        waiting = []  # layers whose weight gradients are still queued (deferred mode)
         for l in reversed(list(self.layout.layers)):
             dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta, dx_hook=dx_hook if l == first else None)
             self.side.flush()
+            if self._defer_wg:
+                waiting.append(l)
+                if l == first or (self.wg_group > 0 and len(waiting) >= self.wg_group):
+                    self.flush_wgrads(beta)
+                    self.flush_reductions()  # the group's grads are final after these launches
+                    if hook is not None:
+                        for ll in waiting:
+                            hook(ll)
+                    waiting = []
+                else:
+                    self.flush_reductions()  # this layer's LayerNorm / bias partials
+                continue
             self.flush_reductions()  # layer l's grads are final after this launch
             if hook is not None:
                 hook(l)
             if not _SIDE_INTERLEAVE:
                 self.side.flush()  # one fork per layer: its wgrads (+ anything the hook queued)
+        if self.wg_queue:  # a stage without layers: the lm_head's weight gradient alone
+            self.flush_wgrads(beta)
+            self.flush_reductions()
         return dx, dx_c
 
 

@@ -16,6 +16,10 @@ layer axis by ``nn.scan`` (``GPTModel.py:58-64``), then the final ``LayerNorm`` 
 * TP rules mirror ``parallel/sharding.py:29-60`` (column-parallel qkv/fc1, row-parallel
   out/fc2, vocab-parallel lm_head) except that column-parallel BIASES are sharded with
   their kernels (no extra comm) and the vocab is padded so N=4/8 work.
+* Attention is sharded by whole HEADS (``CausalSelfAttention.py:28-31``): qkv rows and out_proj
+  input columns follow :func:`head_split`, which also covers a head count the TP degree does not
+  divide (GPT-2 small's 12 heads on 8 ranks: 2,2,2,2,1,1,1,1 -- the reference cannot shard it at
+  all).  Everything else (fc1/fc2, the padded vocab) splits evenly.
 
 Flat-buffer order = the order backward produces gradients (head → layers L-1..0 →
 embeddings), so DP buckets are contiguous ranges that become ready in sequence.
@@ -41,14 +45,15 @@ class ParamSpec:
     shape: Tuple[int, ...]     # full (unsharded) shape
     init: str                  # embed | dense | zeros | ones
     fan_in: int
-    tp: str                    # rep | rows | cols | qkv_rows
+    tp: str                    # rep | rows | cols | qkv_rows | head_cols
     layer: int                 # -1 embed, -2 head, else layer index
     mirror: bool               # has a bf16 compute copy (GEMM weight / bias / LN)
     valid_rows: int = -1       # for padded lm_head: rows >= valid_rows are zero
+    heads: int = 0             # head-sharded (qkv_rows / head_cols): attention heads along the split dim
 
 
 def layer_param_specs(cfg: ModelConfig, l: int) -> List[ParamSpec]:
-    D, F = cfg.d_model, cfg.d_ff
+    D, F, H = cfg.d_model, cfg.d_ff, cfg.n_heads
     p = f"h.{l}."
     # backward production order inside a block
     return [
@@ -58,10 +63,10 @@ def layer_param_specs(cfg: ModelConfig, l: int) -> List[ParamSpec]:
         ParamSpec(p + "fc1.b", (F,), "zeros", D, "rows", l, True),
         ParamSpec(p + "ln2.g", (D,), "ones", D, "rep", l, True),
         ParamSpec(p + "ln2.b", (D,), "zeros", D, "rep", l, True),
-        ParamSpec(p + "out.w", (D, D), "dense", D, "cols", l, True),
+        ParamSpec(p + "out.w", (D, D), "dense", D, "head_cols", l, True, heads=H),
         ParamSpec(p + "out.b", (D,), "zeros", D, "rep", l, True),
-        ParamSpec(p + "qkv.w", (3 * D, D), "dense", D, "qkv_rows", l, True),
-        ParamSpec(p + "qkv.b", (3 * D,), "zeros", D, "qkv_rows", l, True),
+        ParamSpec(p + "qkv.w", (3 * D, D), "dense", D, "qkv_rows", l, True, heads=H),
+        ParamSpec(p + "qkv.b", (3 * D,), "zeros", D, "qkv_rows", l, True, heads=H),
         ParamSpec(p + "ln1.g", (D,), "ones", D, "rep", l, True),
         ParamSpec(p + "ln1.b", (D,), "zeros", D, "rep", l, True),
     ]
@@ -130,11 +135,37 @@ def init_full(spec: ParamSpec, seed: int) -> torch.Tensor:
     raise ValueError(spec.init)
 
 
-def local_shape(spec: ParamSpec, tp_size: int) -> Tuple[int, ...]:
+def head_split(n_heads: int, tp_size: int) -> List[Tuple[int, int]]:
+    """(first head, heads) of each TP rank: whole heads, the first ``n_heads % tp`` ranks one more."""
+    if n_heads < tp_size:
+        raise ValueError(f"n_heads {n_heads} < tp {tp_size}: every TP rank needs at least one attention head")
+    base, rem = divmod(n_heads, tp_size)
+    out, h0 = [], 0
+    for r in range(tp_size):
+        n = base + (1 if r < rem else 0)
+        out.append((h0, n))
+        h0 += n
+    return out
+
+
+def _head_range(spec: ParamSpec, width: int, tp_rank: int, tp_size: int) -> Tuple[int, int]:
+    """[lo, hi) of a head-sharded dimension of ``width`` = heads * head_dim owned by ``tp_rank``."""
+    hd = width // spec.heads
+    h0, n = head_split(spec.heads, tp_size)[tp_rank]
+    return h0 * hd, (h0 + n) * hd
+
+
+def local_shape(spec: ParamSpec, tp_size: int, tp_rank: int = 0) -> Tuple[int, ...]:
     s = list(spec.shape)
     if tp_size == 1 or spec.tp == "rep":
         return tuple(s)
-    if spec.tp in ("rows", "qkv_rows"):
+    if spec.tp == "qkv_rows" and spec.heads:
+        lo, hi = _head_range(spec, s[0] // 3, tp_rank, tp_size)
+        s[0] = 3 * (hi - lo)
+    elif spec.tp == "head_cols":
+        lo, hi = _head_range(spec, s[1], tp_rank, tp_size)
+        s[1] = hi - lo
+    elif spec.tp in ("rows", "qkv_rows"):
         assert s[0] % tp_size == 0, f"{spec.name}: dim0 {s[0]} not divisible by tp={tp_size}"
         s[0] //= tp_size
     elif spec.tp == "cols":
@@ -150,8 +181,14 @@ def shard(spec: ParamSpec, full: torch.Tensor, tp_rank: int, tp_size: int) -> to
         return full.chunk(tp_size, 0)[tp_rank].contiguous()
     if spec.tp == "cols":
         return full.chunk(tp_size, 1)[tp_rank].contiguous()
+    if spec.tp == "head_cols":
+        lo, hi = _head_range(spec, full.shape[1], tp_rank, tp_size)
+        return full[:, lo:hi].contiguous()
     if spec.tp == "qkv_rows":  # [3D, ...] -> per q/k/v slab, heads split
         three = full.reshape(3, full.shape[0] // 3, *full.shape[1:])
+        if spec.heads:
+            lo, hi = _head_range(spec, three.shape[1], tp_rank, tp_size)
+            return three[:, lo:hi].reshape(-1, *full.shape[1:]).contiguous()
         return three.chunk(tp_size, 1)[tp_rank].reshape(-1, *full.shape[1:]).contiguous()
     raise ValueError(spec.tp)
 
@@ -162,7 +199,7 @@ def unshard(spec: ParamSpec, shards: List[torch.Tensor]) -> torch.Tensor:
         return shards[0]
     if spec.tp == "rows":
         return torch.cat(shards, 0)
-    if spec.tp == "cols":
+    if spec.tp in ("cols", "head_cols"):
         return torch.cat(shards, 1)
     if spec.tp == "qkv_rows":
         parts = [s.reshape(3, s.shape[0] // 3, *s.shape[1:]) for s in shards]

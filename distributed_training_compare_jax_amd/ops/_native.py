@@ -77,6 +77,20 @@ class LnArgs(ctypes.Structure):
     ]
 
 
+class WgEntry(ctypes.Structure):
+    """Mirror of ``struct WgEntry`` in csrc/common.h: one problem of a grouped weight-gradient launch."""
+
+    _fields_ = [("A", c_vp), ("B", c_vp), ("C", c_vp), ("cs", c_vp), ("M", c_int), ("N", c_int),
+                ("tile0", c_int), ("pad", c_int)]
+
+
+WG_MAX = 64  # csrc/common.h WG_MAX
+
+
+class WgBatch(ctypes.Structure):
+    _fields_ = [("n", c_int), ("K", c_int), ("beta", c_float), ("ntiles", c_int), ("e", WgEntry * WG_MAX)]
+
+
 EPI_STORE = 0       # C = alpha*acc (+bias) (+beta*C if fp32)
 EPI_RESID = 1       # C(f32) = aux(f32) + acc + bias
 EPI_GELU = 2        # u = acc+bias: C(bf16) = gelu_tanh'(u) ; aux_out(bf16) = gelu_tanh(u)
@@ -100,6 +114,9 @@ def _declare(lib):
         "dtc_gemm_set_n8": ([i], i),
         "dtc_gemm_set_p8cb3": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
+        "dtc_wgrad_group": ([ctypes.POINTER(WgBatch), vp], i),
+        "dtc_wg_entry_bytes": ([], i),
+        "dtc_wg_max": ([], i),
         "dtc_gemm_pair": ([ctypes.POINTER(GemmArgs), ctypes.POINTER(GemmArgs), vp], i),
         "dtc_gemm_ln": ([ctypes.POINTER(LnArgs), vp], i),
         "dtc_gemm_ln_sync_words": ([i, i], l),

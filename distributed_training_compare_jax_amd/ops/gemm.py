@@ -23,6 +23,7 @@ oracle / gloo path).
 
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Optional
 
@@ -282,6 +283,50 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
     if db is not None:
         colsum(dy, db, beta)
     return dw
+
+
+_WG_CHECKED = [False]
+
+
+def wgrad_group(items, beta: float = 0.0, red=None):
+    """Weight gradients of several Dense layers that share the token dimension, in ONE launch:
+    for every ``(dy, x, dw, db)``: dW = β·dW + dYᵀ·X and (``db`` not None) db = β·db + Σ_rows dY.
+
+    GPU bf16: ``gemm8p_group_kernel`` (csrc/gemm.hip) runs whole 256² tiles of every problem — no
+    split-K slabs and no reduction pass, the bias gradients summed by the tiles' MFMAs.  Problems it
+    cannot take (fp32 operands, a width not a multiple of 8, tokens not a multiple of 64) go through
+    :func:`wgrad` one by one (``red``: its batched reducer), as do CPU tensors."""
+    if not items:
+        return
+    dy0 = items[0][0]
+    K = dy0.shape[0]
+    ok = (dy0.is_cuda and dy0.dtype == torch.bfloat16 and K % 64 == 0)
+    fast, slow = [], []
+    for it in items:
+        dy, x, dw, db = it
+        good = (ok and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.shape[0] == K
+                and x.shape[0] == K and dy.is_contiguous() and x.is_contiguous() and dw.is_contiguous()
+                and dw.dtype == torch.float32 and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0
+                and tuple(dw.shape) == (dy.shape[1], x.shape[1]) and dw.data_ptr() % 16 == 0
+                and (db is None or (db.is_contiguous() and db.dtype == torch.float32)))
+        (fast if good else slow).append(it)
+    for dy, x, dw, db in slow:
+        wgrad(dy, x, dw, beta, red=red, db=db)
+    if not fast:
+        return
+    L = N.lib()
+    if not _WG_CHECKED[0]:
+        assert L.dtc_wg_entry_bytes() == ctypes.sizeof(N.WgEntry) and L.dtc_wg_max() == N.WG_MAX
+        _WG_CHECKED[0] = True
+    # largest problems first: their tiles start in the first rounds, the small ones fill the tail
+    fast.sort(key=lambda it: -(it[0].shape[1] * it[1].shape[1]))
+    for i0 in range(0, len(fast), N.WG_MAX):
+        chunk = fast[i0:i0 + N.WG_MAX]
+        b = N.WgBatch()
+        b.n, b.K, b.beta, b.ntiles = len(chunk), K, float(beta), 0
+        for j, (dy, x, dw, db) in enumerate(chunk):
+            b.e[j] = N.WgEntry(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N.ptr(db), dy.shape[1], x.shape[1], 0, 0)
+        N.check(L.dtc_wgrad_group(ctypes.byref(b), N.stream_ptr(dy0.device)), "dtc_wgrad_group")
 
 
 _PAIR = __import__("os").environ.get("DTC_GEMM_PAIR", "1") == "1"  # A/B knob for the paired launch

@@ -54,7 +54,7 @@ class FlatParams:
         n_mirror = 0
         seen_nonmirror = False
         for s in specs:
-            shp = local_shape(s, tp_size)
+            shp = local_shape(s, tp_size, tp_rank)
             slot = Slot(s, off, shp)
             self.slots[s.name] = slot
             off = _align(off + slot.numel)

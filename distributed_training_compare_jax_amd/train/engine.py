@@ -82,6 +82,13 @@ class Engine:
                               act_dtype=self.act_dtype,
                               side_stream=on_gpu and os.environ.get("DTC_SIDE_STREAM", "0") == "1")
         self.program.before_comm.append(self.stage.side.join)
+        # deferred grouped weight gradients (models/gpt.py set_wgrad_group): all layers + the lm_head in
+        # one launch when no collective waits on per-layer grads (dp == 1), else groups of wgrad_group
+        # layers so each group's DP buckets go out under the next group's backward
+        wg = train_cfg.wgrad_group
+        if wg is None:
+            wg = 0 if dp == 1 else 2
+        self.stage.set_wgrad_group(wg)
         # DP embedding-grad gather (pp == 1): instead of all-reducing the dense wte/wpe grads
         # (103 MB fp32 for the reference vocab, issued last -> fully exposed), all-gather the
         # embedding-output grads (b_local*T*D fp32 per rank) and let every rank rebuild the
@@ -341,9 +348,18 @@ class Engine:
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
         bk, opt = self.buckets, self.opt
         side = st.red if st.red is not None else st.side.defer  # where grad-norm chunks are queued
+        # deferred weight gradients: the head's grads are final only after the first grouped launch, so
+        # what would follow the head backward runs at the first layer hook (which fires after it)
+        head_later = [st._defer_wg]
         if dp == 1:
-            opt.ready_upto(bk.head_end_offset(), side)
-            hook = lambda l: opt.ready_upto(bk.layer_end_offset(l), side)
+            if not head_later[0]:
+                opt.ready_upto(bk.head_end_offset(), side)
+
+            def hook(l):
+                if head_later[0]:
+                    opt.ready_upto(bk.head_end_offset(), side)
+                    head_later[0] = False
+                opt.ready_upto(bk.layer_end_offset(l), side)
         else:
             # Single stream: layer l's grads are final once its reduction launch is queued (before
             # the hook), so its bucket goes out right away; the head's bucket right after the head
@@ -355,10 +371,14 @@ class Engine:
             layers = list(self.layout.layers)
             first = layers[0]
             lag = st.side.stream is not None
-            if not lag and not self.zero:  # (ZeRO-1 reduce-scatters all grads in ShardedAdamW.step)
+            if not lag and not self.zero and not head_later[0]:  # (ZeRO-1: ShardedAdamW.step reduce-scatters)
                 bk.ready_upto(bk.head_end_offset())
 
             def hook(l):
+                if head_later[0]:
+                    head_later[0] = False
+                    if not lag and not self.zero:
+                        bk.ready_upto(bk.head_end_offset())
                 if self.embed_gather and l == first:
                     return
                 if not lag:

@@ -92,8 +92,35 @@ def test_tp_shard_roundtrip(name):
     full = init_full(spec, 3)
     if spec.init == "zeros":
         full = torch.randn(spec.shape)
-    parts = [shard(spec, full, r, 4) for r in range(4)]
+    tp = 2 if spec.heads else 4  # head-sharded params: whole heads (the tiny preset has 2)
+    parts = [shard(spec, full, r, tp) for r in range(tp)]
     assert torch.equal(unshard(spec, parts), full)
+
+
+@pytest.mark.parametrize("tp", [3, 5, 8, 12])
+@pytest.mark.parametrize("name", ["h.0.qkv.w", "h.0.qkv.b", "h.0.out.w"])
+def test_uneven_head_shard_roundtrip(name, tp):
+    """12 heads on tp ranks that do not divide it: whole heads per rank (head_split), exact round trip."""
+    from distributed_training_compare_jax_amd.models.params import head_split, local_shape
+
+    mc = model_config_from_preset("gpt2-small", vocab_size=1000, n_layers=1)
+    spec = {s.name: s for s in all_param_specs(mc)}[name]
+    full = torch.randn(spec.shape)
+    parts = [shard(spec, full, r, tp) for r in range(tp)]
+    split = head_split(12, tp)
+    assert sum(n for _, n in split) == 12 and max(n for _, n in split) - min(n for _, n in split) <= 1
+    for r, t in enumerate(parts):
+        assert tuple(t.shape) == local_shape(spec, tp, r)
+        width = t.shape[0] // 3 if spec.tp == "qkv_rows" else t.shape[1]
+        assert width == split[r][1] * 64
+    assert torch.equal(unshard(spec, parts), full)
+
+
+def test_head_split_rejects_too_many_ranks():
+    from distributed_training_compare_jax_amd.models.params import head_split
+
+    with pytest.raises(ValueError):
+        head_split(2, 4)
 
 
 def test_gelu_is_tanh_approx():
