@@ -31,7 +31,10 @@ are optional and default to the reference behaviour:
   ``zero_stage`` (1 = ZeRO-1 Adam-state sharding over the DP group, ``ShardedAdamW``; pure DP only),
   ``wgrad_group`` (weight gradients deferred to grouped launches of that many layers, 0 = the whole
   stage plus the lm_head in one launch, -1 = each Dense's right after its dgrad; None = auto: 0 at
-  dp = 1, 2 under DP so each group's buckets overlap the rest of the backward).
+  dp = 1, 2 under DP so each group's buckets overlap the rest of the backward), ``pp_split``
+  (``cost``: the contiguous layer split minimising the most expensive stage, counting lm_head + CE as
+  ``pp_head_cost`` blocks on the last stage -- default from FLOPs, ``parallel/mesh.py``; ``even``: the
+  remainder layers to the earliest stages).
 """
 
 from __future__ import annotations
@@ -127,6 +130,8 @@ class TrainConfig:
     dp_embed_gather: bool = True
     zero_stage: int = 0  # 1 = ZeRO-1: Adam state sharded over the DP group (train/optimizer.py)
     wgrad_group: Optional[int] = None  # deferred grouped weight gradients (models/gpt.py set_wgrad_group)
+    pp_split: str = "cost"  # cost | even: PP layer split (parallel/mesh.py split_layers)
+    pp_head_cost: Optional[float] = None  # lm_head + CE in blocks (None: parallel/mesh.py head_cost_blocks)
     warmup_steps: int = 5
     ckpt_every: int = 0
     resume: bool = False

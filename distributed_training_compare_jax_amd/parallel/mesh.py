@@ -105,14 +105,76 @@ def build_mesh(rank: int, world: int, dp: int, tp: int, pp: int) -> Mesh:
     return m
 
 
+def head_cost_blocks(cfg, head_speedup: float = 1.7) -> float:
+    """Cost of lm_head + cross-entropy (forward + backward) in units of one transformer block, from
+    FLOPs: per token the head is 6·D·V against a block's 6·(4·D² + 2·D·F) + causal attention
+    6·T·D, divided by ``head_speedup`` -- the head's large GEMMs run at ~1.7x the MFMA rate of a block's
+    mix (layer GEMMs + attention + LayerNorm passes).  GPT-2 small: 4.9 by FLOPs, 2.9 by this model;
+    measured 2.8 in the round-3 kernel table (profiles/r3_gpt2_small_profile_final.md: lm_head
+    fwd 713 + dgrad 657 + wgrad 569 + CE 306 us against ~0.8 ms per block)."""
+    D, F, V, T = cfg.d_model, cfg.d_ff, cfg.padded_vocab, cfg.max_seq_len
+    block = 6.0 * (4 * D * D + 2 * D * F) + 6.0 * T * D
+    return 6.0 * D * V / block / head_speedup
+
+
 def split_layers(n_layers: int, pp: int, weights=None):
     """Contiguous layer ranges per stage.  Fixes the reference quirk ``layers_per_stage =
-    n_layers // N`` (``train/train.py:118``) that silently drops layers when N ∤ L: the
-    remainder goes to the EARLIEST stages (the last stage also carries lm_head+CE)."""
-    base, rem = divmod(n_layers, pp)
+    n_layers // N`` (``train/train.py:118``) that silently drops layers when N ∤ L.
+
+    ``weights=None``: an even split, the remainder to the EARLIEST stages (the last stage also
+    carries lm_head+CE).  ``weights=(first, last)``: extra cost (in blocks) of the first stage
+    (embedding) and the last (lm_head + CE, :func:`head_cost_blocks`): the contiguous split that
+    minimises the most expensive stage, then the spread (sum of squared stage costs); every stage but
+    the last keeps at least one layer, the last may hold the head alone."""
+    if weights is None:
+        base, rem = divmod(n_layers, pp)
+        out, start = [], 0
+        for s in range(pp):
+            n = base + (1 if s < rem else 0)
+            out.append(range(start, start + n))
+            start += n
+        return out
+    first, last = (float(w) for w in weights)
+    if n_layers < pp - 1:  # not enough layers for one per non-last stage
+        return split_layers(n_layers, pp)
+    extra = [0.0] * pp
+    extra[0] += first
+    extra[-1] += last
+    # DP over (stage, layers placed): minimise (max stage cost, sum of squared stage costs); every stage
+    # but the last holds >= 1 layer (an empty middle stage would only relay activations)
+    INF = (float("inf"), float("inf"))
+    best = [[INF] * (n_layers + 1) for _ in range(pp + 1)]
+    arg = [[0] * (n_layers + 1) for _ in range(pp + 1)]
+    best[0][0] = (0.0, 0.0)
+    for s_ in range(pp):
+        lo_k = 0 if s_ == pp - 1 else 1
+        for used in range(n_layers + 1):
+            if best[s_][used] == INF:
+                continue
+            mx, sq = best[s_][used]
+            for k in range(lo_k, n_layers - used + 1):
+                c = k + extra[s_]
+                cand = (max(mx, c), sq + c * c)
+                if cand < best[s_ + 1][used + k]:
+                    best[s_ + 1][used + k] = cand
+                    arg[s_ + 1][used + k] = k
+    counts, used = [], n_layers
+    for s_ in range(pp, 0, -1):
+        k = arg[s_][used]
+        counts.append(k)
+        used -= k
+    counts.reverse()
     out, start = [], 0
-    for s in range(pp):
-        n = base + (1 if s < rem else 0)
-        out.append(range(start, start + n))
-        start += n
+    for k in counts:
+        out.append(range(start, start + k))
+        start += k
     return out
+
+
+def stage_costs(ranges, weights):
+    """Per-stage cost (blocks) of a split under ``weights=(first, last)``."""
+    first, last = weights
+    c = [float(len(r)) for r in ranges]
+    c[0] += first
+    c[-1] += last
+    return c

@@ -26,7 +26,7 @@ from ..ops import optim as O
 from ..parallel.buffers import FlatParams
 from ..parallel.dist import DistInfo
 from ..parallel.dp import GradBuckets
-from ..parallel.mesh import Mesh, build_mesh, resolve_degrees, split_layers
+from ..parallel.mesh import Mesh, build_mesh, head_cost_blocks, resolve_degrees, split_layers
 from ..parallel.program import StepProgram, csig
 from ..parallel.tp import TPComm
 from .optimizer import FusedAdamW, ShardedAdamW
@@ -57,7 +57,14 @@ class Engine:
         self.row0 = m.dp_idx * self.b_local
 
         # ---- ownership
-        layer_ranges = split_layers(model_cfg.n_layers, pp)
+        if train_cfg.pp_split not in ("cost", "even"):
+            raise ValueError(f"pp_split={train_cfg.pp_split!r}: expected 'cost' or 'even'")
+        weights = None
+        if pp > 1 and train_cfg.pp_split == "cost":
+            hc = train_cfg.pp_head_cost
+            weights = (0.05, head_cost_blocks(model_cfg) if hc is None else float(hc))
+        layer_ranges = split_layers(model_cfg.n_layers, pp, weights)
+        self.layer_ranges = layer_ranges
         self.layout = StageLayout(layer_ranges[m.pp_idx], has_embed=m.pp_idx == 0, has_head=m.pp_idx == pp - 1)
         specs = stage_param_specs(model_cfg, self.layout.layers, self.layout.has_embed, self.layout.has_head)
         self.flat = FlatParams(specs, m.tp_idx, tp, self.device, compute_dtype=self.act_dtype)

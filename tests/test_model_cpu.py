@@ -50,6 +50,27 @@ def test_strategy_resolution():
     assert sum(len(x) for x in r) == 12 and r[0].start == 0 and r[-1].stop == 12
 
 
+@pytest.mark.parametrize("L,pp,head", [(12, 2, 2.9), (12, 4, 2.9), (12, 8, 2.9), (24, 8, 2.2), (12, 8, 4.5), (4, 4, 1.0)])
+def test_cost_aware_pp_split(L, pp, head):
+    """split_layers(weights=(embed, head)) is contiguous, keeps every layer, puts >= 1 layer on every
+    non-last stage and minimises the most expensive stage (checked against brute force)."""
+    import itertools
+
+    from distributed_training_compare_jax_amd.parallel.mesh import stage_costs
+
+    w = (0.05, head)
+    r = split_layers(L, pp, w)
+    assert len(r) == pp and r[0].start == 0 and r[-1].stop == L
+    assert all(a.stop == b.start for a, b in zip(r, r[1:]))
+    assert all(len(x) >= 1 for x in r[:-1])
+    if pp <= 4:  # brute force over the non-last stage sizes
+        best = min(max(stage_costs([range(0, k) for k in ks], w))  # only lengths matter
+                   for ks in itertools.product(range(1, L + 1), repeat=pp - 1) if sum(ks) <= L
+                   for ks in [ks + (L - sum(ks),)])
+        assert max(stage_costs(r, w)) == pytest.approx(best)
+    assert max(stage_costs(r, w)) <= max(stage_costs(split_layers(L, pp), w)) + 1e-9
+
+
 def test_synthetic_data_contract():
     it = get_batch_iterator(8, 513)
     a = next(it)
