@@ -34,36 +34,27 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-# HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), in
-# order: two streams on one queue execute as one.  A multi-rank step has more streams than that (the
-# step stream, the side stream, every communicator's RCCL stream, gloo's copy streams) and kernels
-# that wait on OTHER processes (RCCL's, the P2P all-reduce barrier): a barrier queued ahead of an
-# unrelated collective on a shared queue blocks that collective, and across ranks this closes a
-# cycle.  Measured: dp2 x tp2 with the P2P all-reduce on one GPU timed out at the default 4 queues
-# and passes at 16 (profiles/r3_hw_queues.log).  So every multi-rank GPU process gets >= 16 queues.
-MIN_HW_QUEUES = 16
-
-
-def _ensure_hw_queues():
-    cur = os.environ.get("GPU_MAX_HW_QUEUES")
-    if cur is not None and cur.isdigit() and int(cur) >= MIN_HW_QUEUES:
-        return
-    if torch.cuda.is_initialized():
-        import warnings
-
-        warnings.warn(f"HIP was initialised before init_distributed: GPU_MAX_HW_QUEUES={cur} stays in effect "
-                      f"(multi-rank steps want >= {MIN_HW_QUEUES}; set it in the launcher's environment)")
-        return
-    os.environ["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
-
-
+# Why cross-process spin waits cannot deadlock here, whatever GPU_MAX_HW_QUEUES is.
+# HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) in FIFO
+# order, so two streams that share a queue execute as one, and a kernel that waits on OTHER processes
+# (an RCCL collective, the P2P all-reduce barrier of parallel/p2p.py) blocks everything queued behind
+# it.  That is safe as long as every blocking operation is ENQUEUED BY THE MAIN THREAD IN PROGRAM
+# ORDER, which is identical on every rank (StepProgram issues graphs and collectives in one fixed
+# sequence, and program.check_collective_sequences proves the ranks agree): then the globally
+# earliest unfinished blocking operation has, on every participating rank, only finished or
+# non-blocking work ahead of it in any queue, so it completes, and by induction every later one does
+# -- a cycle would need some rank to have enqueued a later operation ahead of an earlier one.  The
+# one way that order broke was gloo on GPU tensors (the one-GPU multi-rank test rig): gloo enqueues
+# its device copy-back from a worker thread at an unpredictable time, behind later barriers
+# (profiles/r3_hw_queues.log: dp2 x tp2 hung at 4 queues).  StepProgram.sync_comms therefore waits
+# every gloo collective on GPU tensors where it is issued (the Engine sets it), and the queue count
+# is left at the box default.  The in-launch LayerNorm statistics exchange (ops/ln_fused.py) waits
+# only on blocks of its own grid and is enabled for single-rank runs only.
 def init_distributed(device: str = "auto", timeout_s: float = 600.0) -> DistInfo:
     """Initialise (or reuse) the default process group from the environment."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world > 1 and device != "cpu":
-        _ensure_hw_queues()  # before the first HIP call of this process
     use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
     if use_cuda:
         ndev = torch.cuda.device_count()

@@ -144,15 +144,24 @@ def pp_program(kind: str, S: int, s: int, M: int) -> List[tuple]:
     return prog
 
 
-def simulate(kind: str, S: int, M: int) -> Dict[str, int]:
+def simulate(kind: str, S: int, M: int, model: str = "pair") -> Dict[str, int]:
     """Run every stage's :func:`pp_program` under RCCL p2p semantics and return counters.
 
     Model: each stage executes its items in order on one compute stream; a ``post`` enqueues its
-    entry on the (stage, peer) pair queue once every earlier compute item of the stage is done
-    (the comm stream waits on the compute stream); the heads of the two queues of a pair complete
-    TOGETHER when both are posted and complementary (sends of one == receives of the other, as
-    sets: a grouped call); a ``wait`` blocks the stage until its entries completed.  Raises
-    RuntimeError on a deadlock or on a head pair that does not match (wrong message order)."""
+    entry once every earlier compute item of the stage is done (the comm stream waits on the compute
+    stream); a ``wait`` blocks the stage until its entries completed.  Queues:
+
+    * ``model="pair"``: one ordered queue per (stage, peer) pair -- the heads of the two queues of a
+      pair complete TOGETHER when both are posted and complementary (sends of one == receives of
+      the other, as sets: a grouped call);
+    * ``model="rank"``: ONE ordered queue per stage for all its peers -- what PyTorch's coalesced p2p
+      does on RCCL (every ``batch_isend_irecv`` of a group is one kernel on the group communicator's
+      single stream, so a stage's posts to s-1 and to s+1 serialise in issue order).  A head entry
+      completes only when the peer's head entry is its complement.
+
+    Raises RuntimeError on a deadlock or on a head pair that does not match (wrong message order)."""
+    if model not in ("pair", "rank"):
+        raise ValueError(model)
     progs = [pp_program(kind, S, s, M) for s in range(S)]
     pc = [0] * S
     queues: Dict[Tuple[int, int], List[tuple]] = {}
@@ -165,7 +174,8 @@ def simulate(kind: str, S: int, M: int) -> Dict[str, int]:
                 it = progs[s][pc[s]]
                 if it[0] == "post":
                     _, name, peer, snd, rcv = it
-                    queues.setdefault((s, s + peer), []).append((name, frozenset(snd), frozenset(rcv)))
+                    key = (s, s + peer) if model == "pair" else (s, -1)
+                    queues.setdefault(key, []).append((name, frozenset(snd), frozenset(rcv), s + peer))
                     counts["posts"] += 1
                 elif it[0] == "wait":
                     if not all((s, n) in done for n in it[1]):
@@ -176,10 +186,13 @@ def simulate(kind: str, S: int, M: int) -> Dict[str, int]:
                 pc[s] += 1
                 progressed = True
         for (a, b), qa in list(queues.items()):
-            qb = queues.get((b, a), [])
-            while qa and qb:
-                na, sa, ra = qa[0]
-                nb, sb, rb = qb[0]
+            while qa:
+                b = qa[0][3]  # the head entry's peer
+                qb = queues.get((b, a) if model == "pair" else (b, -1), [])
+                if not qb or qb[0][3] != a:
+                    break  # rank model: the peer's stream is busy with another peer first
+                na, sa, ra, _ = qa[0]
+                nb, sb, rb, _ = qb[0]
                 if sa != rb or ra != sb:
                     # two sends (or two receives) at the heads of a pair wait on each other forever
                     what = "deadlock (head-of-line)" if (sa and sb and not (ra or rb)) or (ra and rb and not (

@@ -122,6 +122,13 @@ class StepProgram:
         self._ev: List[List[Any]] = []  # per step (FIFO): [(start, end) event pairs | host ms floats]
         # collective signatures of the step being collected (None = not collecting)
         self.sigs: Optional[List[Tuple]] = None
+        # sync_comms: wait every collective where it is issued (no collective in flight while later
+        # kernels are enqueued).  Set for GPU tensors on a gloo group (the one-GPU multi-rank test rig):
+        # gloo copies results back to the device from its WORKER thread, at a time no other rank can
+        # predict, so that copy lands in a hardware queue behind whatever the main thread issued in
+        # the meantime -- e.g. a P2P all-reduce barrier that spins on a peer whose own progress waits on
+        # this rank's gloo result: a cycle whenever streams share a queue (parallel/dist.py).
+        self.sync_comms = False
 
     def begin_step(self):
         self.step_comms = 0
@@ -174,6 +181,9 @@ class StepProgram:
             self._begin()
             return None
         res = self._timed(fn)
+        if self.sync_comms and res is not None:
+            self._wait_handle(res)
+            res = None
         if name is not None:
             self._handles[name] = res
         return res
@@ -207,7 +217,10 @@ class StepProgram:
             raise RuntimeError(f"ranks disagree on the collectives of the {what}: {err}")
 
     def _wait(self, name):
-        h = self._handles.pop(name, None)
+        self._wait_handle(self._handles.pop(name, None))
+
+    @staticmethod
+    def _wait_handle(h):
         if h is not None:
             if isinstance(h, (list, tuple)):
                 for x in h:
@@ -275,6 +288,9 @@ class StepProgram:
                 obj.replay()
             elif kind == "comm":
                 res = self._timed(obj)
+                if self.sync_comms and res is not None:
+                    self._wait_handle(res)
+                    res = None
                 if name is not None:
                     self._handles[name] = res
             else:

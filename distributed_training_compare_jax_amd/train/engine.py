@@ -77,6 +77,10 @@ class Engine:
 
         # ---- step program, comms, model, optimizer
         self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu)
+        # gloo on GPU tensors (the one-GPU multi-rank rig): collectives complete where they are issued,
+        # so no copy-back from gloo's worker thread can queue behind a later cross-process wait
+        # (parallel/dist.py explains the ordering argument)
+        self.program.sync_comms = bool(on_gpu and dinfo.world > 1 and dinfo.backend == "gloo")
         self.p2p = None
         mode = train_cfg.tp_comm
         if tp > 1 and on_gpu and (mode == "p2p" or (mode == "auto" and dinfo.backend == "nccl")):

@@ -22,7 +22,8 @@ def _worker(parallel, kw, out_dir):
     from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
     from distributed_training_compare_jax_amd.train.loop import train
 
-    mc = model_config_from_preset("tiny", vocab_size=1000, n_layers=4)
+    kw = dict(kw)
+    mc = _model_cfg(kw.pop("model", None))
     tc = TrainConfig(seed=0, parallel=parallel, batch=4, steps=STEPS, log_every=1000, output_dir="/tmp/unused",
                      device="cuda", warmup_steps=2, **kw)
     oc = OptimConfig(lr=3e-3, weight_decay=0.1, grad_clip=1.0)
@@ -37,17 +38,17 @@ def _worker(parallel, kw, out_dir):
     destroy()
 
 
-def _model_cfg():
+def _model_cfg(model=None):
     from distributed_training_compare_jax_amd.config.schema import model_config_from_preset
 
-    return model_config_from_preset("tiny", vocab_size=1000, n_layers=4)
+    return model_config_from_preset("tiny", vocab_size=1000, **dict({"n_layers": 4}, **(model or {})))
 
 
-def _full_params(results):
+def _full_params(results, model=None):
     """Reassemble the full model from TP shards / PP stages (DP replica 0)."""
     from distributed_training_compare_jax_amd.models.params import all_param_specs, unshard
 
-    specs = {s.name: s for s in all_param_specs(_model_cfg())}
+    specs = {s.name: s for s in all_param_specs(_model_cfg(model))}
     pieces = {}
     for r in results:
         if r["dp_idx"] != 0:
@@ -122,6 +123,36 @@ def test_two_ranks_match_single_gpu(single, init_params, parallel, world, kw):
         assert res[0]["graphs"] >= 2  # step was captured and cut at the collectives
     if parallel == "dp" and "tp" not in kw:  # replicas stay bit-identical (deterministic local embedding grads)
         assert torch.equal(res[0]["params"], res[1]["params"])
+
+
+# GPT-2 small's 12 heads (head_dim 32 here, a size the attention kernels take) on 8 TP ranks: whole
+# heads 2,2,2,2,1,1,1,1 (models/params.py head_split) -- BASELINE.json config 3's layout
+HEADS12 = {"d_model": 384, "n_heads": 12, "d_ff": 512, "n_layers": 2}
+
+
+@pytest.mark.parametrize("world,kw", [
+    (8, {"parallel": "tp", "tp_comm": "p2p"}),
+    (4, {"parallel": "dp", "tp": 2, "tp_comm": "p2p"}),  # dp2 x tp2 at the box's default HW queue count
+])
+def test_uneven_heads_and_hybrid_one_gpu(world, kw):
+    """TP=8 with 12 heads and dp2 x tp2, 8 / 4 processes on one GPU through the P2P all-reduce kernels,
+    against a single-process GPU run of the same model (losses + parameter updates, bf16 tolerances)."""
+    kw = dict(kw)
+    parallel = kw.pop("parallel")
+    single = _run("dp", 1, model=HEADS12)
+    res = _run(parallel, world, model=HEADS12, **kw)
+    assert res[0]["losses"] == pytest.approx(single[0]["losses"], rel=2e-2, abs=2e-2)
+    from distributed_training_compare_jax_amd.models.params import all_param_specs, init_full
+
+    p0 = {sp.name: init_full(sp, 0) for sp in all_param_specs(_model_cfg(HEADS12))}  # canonical init (seed 0)
+    full, one = _full_params(res, HEADS12), _full_params(single, HEADS12)
+    assert set(full) == set(one)
+    for n in one:
+        a, b, q = full[n], one[n], p0[n]
+        if n.endswith("qkv.b"):
+            a, b, q = (x.view(3, -1)[[0, 2]] for x in (a, b, q))
+        err = (((a - q) - (b - q)).norm() / ((b - q).norm() + 1e-12)).item()
+        assert err < 0.15, f"{n}: update differs from the single-GPU run by {err:.3f} (relative)"
 
 
 def _p2p_worker(out_dir):

@@ -12,11 +12,14 @@ import pytest
 from distributed_training_compare_jax_amd.parallel import pp as PP
 
 
+@pytest.mark.parametrize("model", ["pair", "rank"])
 @pytest.mark.parametrize("kind", ["gpipe", "1f1b"])
 @pytest.mark.parametrize("S", [1, 2, 3, 4, 8])
-def test_programs_never_deadlock(kind, S):
+def test_programs_never_deadlock(kind, S, model):
+    """Both queue models: per-pair streams, and one serialised stream per rank (PyTorch's coalesced
+    p2p on RCCL runs every grouped call of a rank on its group communicator's single stream)."""
     for M in range(1, 17):
-        c = PP.simulate(kind, S, M)
+        c = PP.simulate(kind, S, M, model=model)
         assert c["compute"] == 2 * M * S  # every stage: one forward and one backward per microbatch
 
 
@@ -63,3 +66,17 @@ def test_comm_cuts_per_microbatch(kind):
                 runs += 1
             prev_comm = is_comm
         assert runs <= 2 * M + 1, (s, runs)
+
+
+def test_rank_model_is_stricter(monkeypatch):
+    """A three-rank send cycle whose receives sit second on each rank: fine with per-pair streams, a
+    deadlock once each rank's posts serialise on one stream (the rank model must see it)."""
+    progs = {
+        0: [("post", "a", +1, (("f", 0),), ()), ("post", "c", +2, (), (("x", 0),)), ("wait", ("a", "c"))],
+        1: [("post", "b", +1, (("f", 1),), ()), ("post", "a", -1, (), (("f", 0),)), ("wait", ("a", "b"))],
+        2: [("post", "c", -2, (("x", 0),), ()), ("post", "b", -1, (), (("f", 1),)), ("wait", ("b", "c"))],
+    }
+    monkeypatch.setattr(PP, "pp_program", lambda kind, S, s, M: progs[s])
+    PP.simulate("gpipe", 3, 1, model="pair")
+    with pytest.raises(RuntimeError, match="deadlock"):
+        PP.simulate("gpipe", 3, 1, model="rank")
