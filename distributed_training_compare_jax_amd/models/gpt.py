@@ -70,6 +70,10 @@ _CE_WGRAD = _os.environ.get("DTC_CE_WGRAD", "0") == "1"
 # columns vs 824 MB) held from the forward to the backward -- for memory-bound configurations
 # (SURVEY K10 "never materialize full logits"); it costs one extra lm_head GEMM (the recompute).
 _CE_CHUNK = int(_os.environ.get("DTC_CE_CHUNK", "0"))
+if _CE_CHUNK < 0 or _CE_CHUNK % 256:
+    # chunk offsets feed 16-byte vector loads of w[c0:], wt[:, c0:] and gw[c0:]: a ragged offset would
+    # surface as an opaque native error deep in the backward
+    raise ValueError(f"DTC_CE_CHUNK={_CE_CHUNK}: must be 0 (off) or a positive multiple of 256 vocab columns")
 
 
 class NoComm:

@@ -283,6 +283,15 @@ def run_pipeline(eng) -> None:
             else:
                 steps.append(it)
         local = {}
+        replayed = prog.recording  # a recorded item is re-run by every replay: it must keep its tensors
+
+        def release(name):
+            """Eager steps: a send whose post was waited no longer needs its buffer -- drop the stage's
+            references (forward output / input gradient), so 1F1B holds ~S microbatches, not M."""
+            if replayed:
+                return
+            for d, i in sent_tags.get(name, ()):  # (the post may belong to an earlier run)
+                (outs if d == "f" else dx_out).pop(i, None)
 
         def fn():
             for st_ in steps:
@@ -300,6 +309,7 @@ def run_pipeline(eng) -> None:
                                 w.wait()
                         else:
                             prog._wait(n)
+                        release(n)
 
         sig = []
         for st_ in steps:
@@ -310,6 +320,7 @@ def run_pipeline(eng) -> None:
         prog.comm(fn, sig=sig)
 
     items = pp_program(eng.tcfg.pp_schedule, S, s, M)
+    sent_tags = {it[1]: it[3] for it in items if it[0] == "post"}  # post name -> tags it sends
     dx_out: Dict[int, torch.Tensor] = {}
     k = 0
     while k < len(items):
