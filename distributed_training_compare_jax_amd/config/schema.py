@@ -34,7 +34,8 @@ are optional and default to the reference behaviour:
   dp = 1, 2 under DP so each group's buckets overlap the rest of the backward), ``pp_split``
   (``cost``: the contiguous layer split minimising the most expensive stage, counting lm_head + CE as
   ``pp_head_cost`` blocks on the last stage -- default from FLOPs, ``parallel/mesh.py``; ``even``: the
-  remainder layers to the earliest stages).
+  remainder layers to the earliest stages), ``dp_grad_dtype`` / ``pp_comm_dtype`` (``bf16``: the DP
+  gradient buckets / PP stage messages travel as bf16 and are summed in fp32, ``ops/payload.py``).
 """
 
 from __future__ import annotations
@@ -131,6 +132,8 @@ class TrainConfig:
     zero_stage: int = 0  # 1 = ZeRO-1: Adam state sharded over the DP group (train/optimizer.py)
     wgrad_group: Optional[int] = None  # deferred grouped weight gradients (models/gpt.py set_wgrad_group)
     pp_split: str = "cost"  # cost | even: PP layer split (parallel/mesh.py split_layers)
+    dp_grad_dtype: str = "fp32"  # fp32 | bf16: DP gradient payload (bf16: all-to-all + fp32 shard sums)
+    pp_comm_dtype: str = "fp32"  # fp32 | bf16: PP activation / gradient messages
     pp_head_cost: Optional[float] = None  # lm_head + CE in blocks (None: parallel/mesh.py head_cost_blocks)
     warmup_steps: int = 5
     ckpt_every: int = 0

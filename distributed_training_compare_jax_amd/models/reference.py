@@ -31,9 +31,9 @@ def oracle_loss(cfg: ModelConfig, params: dict, ids: torch.Tensor, labels: torch
     eps = cfg.layernorm_eps
     h = params["wte"][ids.long()] + params["wpe"][:T][None]
     if cfg.dropout > 0:
-        keep = dropout_keep_mask(B * T, D, row0 * T, cfg.dropout, seed, step).view(B, T, D)
+        keep = dropout_keep_mask(B * T, D, row0 * T, cfg.dropout, seed, step).view(B, T, D).to(h.device)
         h = torch.where(keep, h / (1 - cfg.dropout), torch.zeros_like(h))
-    mask = torch.tril(torch.ones(T, T))
+    mask = torch.tril(torch.ones(T, T, device=h.device))
     add_mask = torch.where(mask == 1, 0.0, -1e9)  # GPTModel.py:50-51
     for l in range(cfg.n_layers):
         p = lambda n: params[f"h.{l}.{n}"]  # noqa: E731

@@ -157,6 +157,8 @@ def _declare(lib):
         "dtc_tr_max_tasks": ([], i),
         "dtc_tr_task_bytes": ([], i),
         "dtc_fill_f32": ([vp, f, l, vp], i),
+        "dtc_shard_sum_bf16": ([vp, i, l, vp, vp], i),
+        "dtc_cast_bf16_f32": ([vp, vp, l, vp], i),
         "dtc_ce_dgrad": ([vp, l, vp, vp, i, i, f, vp, l, vp, l, vp, vp, i, i, i, vp, l, vp], i),
         "dtc_ce_dgrad_workspace_bytes": ([i, i, i], l),
         "dtc_ce_dgrad_colpart_rows": ([i], i),

@@ -19,8 +19,21 @@ from typing import List, Tuple
 
 import torch.distributed as dist
 
+import torch
+
+from ..ops.payload import cast_bf16_to_f32, cast_to_bf16, shard_sum_bf16
 from .buffers import FlatParams
 from .program import csig
+
+
+class _StreamJoin:
+    """Work-like handle of a chain run on a side stream: wait() makes the current stream wait for it."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
 
 
 class GradBuckets:
@@ -38,11 +51,16 @@ class GradBuckets:
     backward, its all-reduce fully exposed)."""
 
     def __init__(self, flat: FlatParams, group, dp: int, program, bucket_mb: float = 64.0, tail_mb: float = 16.0,
-                 local_names=(), boundaries=None):
+                 local_names=(), boundaries=None, payload: str = "fp32"):
         self.flat = flat
         self.group = group
         self.dp = dp
         self.program = program
+        if payload not in ("fp32", "bf16"):
+            raise ValueError(f"dp_grad_dtype={payload!r}: expected 'fp32' or 'bf16'")
+        self.payload = payload
+        self._bf16 = {}  # bucket -> (send, recv, reduced shard, gathered) bf16 buffers
+        self._cs = None  # GPU: the stream the bf16 exchange chain runs on
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
         tail_cap = max(1, int(tail_mb * 1024 * 1024 / 4))
         end = flat.numel
@@ -112,9 +130,55 @@ class GradBuckets:
         a, b = self.buckets[i]
         view = self.flat.grads[a:b]
         g = self.group
-        self.program.comm(lambda: dist.all_reduce(view, group=g, async_op=True), name=f"dp_bucket{i}",
-                          sig=csig("all_reduce", g, view))
+        if self.payload == "bf16":
+            self._issue_bf16(i, view)
+        else:
+            self.program.comm(lambda: dist.all_reduce(view, group=g, async_op=True), name=f"dp_bucket{i}",
+                              sig=csig("all_reduce", g, view))
         self.issued[i] = True
+
+    def _buffers(self, i: int, n: int):
+        """Persistent bf16 buffers of bucket i (allocated at its first issue, i.e. in the eager warmup
+        step, before any graph capture): the padded send image [dp*s] (pad stays zero), the all-to-all
+        result [dp*s], this rank's reduced shard [s] and the all-gathered bucket [dp*s]."""
+        if i not in self._bf16:
+            s = -(-n // (self.dp * 64)) * 64
+            kw = dict(dtype=torch.bfloat16, device=self.flat.device)
+            self._bf16[i] = (torch.zeros(self.dp * s, **kw), torch.zeros(self.dp * s, **kw), torch.zeros(s, **kw),
+                             torch.zeros(self.dp * s, **kw))
+        return self._bf16[i]
+
+    def _issue_bf16(self, i: int, view):
+        """bf16 payload, fp32 accumulation: cast -> all-to-all (shard r of every rank to rank r) -> fixed-order
+        fp32 sum of the dp shards -> all-gather of the bf16 shards -> cast back into the fp32 grads.  Half the
+        bytes of an fp32 ring all-reduce, every rank-pair xGMI link busy at once, identical replicas.  On the
+        GPU the chain runs on its own stream (the backward keeps going); the returned handle's wait() joins it."""
+        n = view.numel()
+        send, recv, red, gath = self._buffers(i, n)
+        g, dp = self.group, self.dp
+
+        def chain():
+            cast_to_bf16(view, send[:n])
+            dist.all_to_all_single(recv, send, group=g)
+            shard_sum_bf16(recv, dp, red)
+            dist.all_gather_into_tensor(gath, red, group=g)
+            cast_bf16_to_f32(gath[:n], view)
+
+        def fn():
+            if not view.is_cuda:
+                chain()
+                return None
+            if self._cs is None:
+                self._cs = torch.cuda.Stream(view.device)
+            cur = torch.cuda.current_stream(view.device)
+            self._cs.wait_stream(cur)
+            with torch.cuda.stream(self._cs):
+                chain()
+            ev = torch.cuda.Event()
+            ev.record(self._cs)
+            return _StreamJoin(ev)
+
+        self.program.comm(fn, name=f"dp_bucket{i}", sig=csig("all_to_all", g, send) + csig("all_gather", g, red))
 
     def wait_all(self):
         if self.dp == 1:

@@ -36,6 +36,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops.optim import cast_to_bf16, fill_
+from ..ops.payload import cast_bf16_to_f32
 from .dist import staged_p2p
 from .program import psig
 
@@ -251,8 +252,14 @@ def run_pipeline(eng) -> None:
     staged = staged_p2p() and eng.device.type == "cuda"
     outs: Dict[int, torch.Tensor] = {}  # forward outputs (sent to the next stage)
 
+    bf = getattr(eng, "pp_bf16", False)  # bf16 stage messages (pp_comm_dtype): the bf16 images travel
+
     def tensor_of(tag, sending):
         d, i = tag
+        if bf:
+            if d == "f":
+                return eng.send_x_bf[i] if sending else eng.recv_x_bf[i]
+            return eng.send_dx_bf[i] if sending else eng.recv_dx_bf[i]
         if d == "f":
             return outs[i] if sending else eng.recv_x[i]
         return dx_out[i] if sending else eng.recv_dx[i]
@@ -337,12 +344,16 @@ def run_pipeline(eng) -> None:
         row0 = eng.row0 + i * rows
         ctx = ctxs[i]
         if kind == "F":
+            if not first and bf:
+                cast_bf16_to_f32(eng.recv_x_bf[i], eng.recv_x[i])
             h = st.embed_forward(ids, step, row0, ctx) if first else eng.recv_x[i]
             h = st.stage_forward(h, rows, ctx)
             if last:
                 st.head_forward(h, labels, loss_scale, ctx, loss_out=eng.loss, accumulate=(i > 0))
             else:
                 outs[i] = h
+                if bf:
+                    cast_to_bf16(h, eng.send_x_bf[i])
         else:
             beta = 0.0 if n_bwd_done == 0 else 1.0
             n_bwd_done += 1
@@ -351,11 +362,17 @@ def run_pipeline(eng) -> None:
             else:
                 dx = eng.recv_dx[i]
                 dx_c = eng.recv_dx_c[i]
-                if dx_c is not dx:
+                if bf:  # the received bf16 image is the compute-dtype copy; the fp32 one is cast from it
+                    cast_bf16_to_f32(eng.recv_dx_bf[i], dx)
+                    if dx_c is not dx:
+                        dx_c = eng.recv_dx_bf[i]
+                elif dx_c is not dx:
                     cast_to_bf16(dx, dx_c)
             dx, dx_c = st.stage_backward(ctx, dx, dx_c, beta)
             if first:
                 st.embed_backward(ctx, dx, step, beta)
             else:
                 dx_out[i] = dx
+                if bf:
+                    cast_to_bf16(dx, eng.send_dx_bf[i])
         k += 1

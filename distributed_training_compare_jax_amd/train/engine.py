@@ -124,7 +124,8 @@ class Engine:
             bnd = ends + ([self.flat.range_of(head)[1]] if head else [])
         self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb,
                                    tail_mb=train_cfg.dp_tail_mb,
-                                   local_names=("wte", "wpe") if self.embed_gather else (), boundaries=bnd)
+                                   local_names=("wte", "wpe") if self.embed_gather else (), boundaries=bnd,
+                                   payload=train_cfg.dp_grad_dtype)
         if self.zero:
             self.opt = ShardedAdamW(self.flat, opt_cfg, self.program, m.dp_group, dp, m.dp_idx)
         else:
@@ -179,6 +180,15 @@ class Engine:
                             for _ in range(self.n_micro)]
             self.recv_dx_c = [torch.zeros(self.mb_rows * T, D, dtype=self.act_dtype, device=self.device)
                               for _ in range(self.n_micro)] if self.act_dtype != torch.float32 else self.recv_dx
+            # pp_comm_dtype=bf16: stage messages travel as bf16 (send images cast after the producing compute,
+            # received images cast back to the fp32 residual stream before the consuming compute)
+            if train_cfg.pp_comm_dtype not in ("fp32", "bf16"):
+                raise ValueError(f"pp_comm_dtype={train_cfg.pp_comm_dtype!r}: expected 'fp32' or 'bf16'")
+            self.pp_bf16 = train_cfg.pp_comm_dtype == "bf16"
+            if self.pp_bf16:
+                mk = lambda: [torch.zeros(self.mb_rows * T, D, dtype=torch.bfloat16, device=self.device)
+                              for _ in range(self.n_micro)]
+                self.send_x_bf, self.send_dx_bf, self.recv_x_bf, self.recv_dx_bf = mk(), mk(), mk(), mk()
         self.steps_done = 0
         # Deferred optimizer (pp == 1, GPU): the step ends with the global norm and the AdamW of
         # the embedding tables only; the rest of the update runs at the START of the next step

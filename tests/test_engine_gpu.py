@@ -45,6 +45,37 @@ def test_model_grads_vs_oracle(cuda):
         assert err < 5e-2, f"{n}: relative grad error {err:.3e}"
 
 
+def test_gpt2_small_step_vs_oracle(cuda):
+    """The headline configuration end to end: one GPT-2 small step (batch 8 x T1024 = 8192 tokens, vocab
+    50258, dropout 0.1) through the engine's real step program with the default plans as composed there
+    (layer GEMMs, grouped deferred weight gradients, hd64 chunked flash attention, the CE path, the
+    fused LayerNorm backward), against the fp32 autograd oracle (models/reference.py) of the same
+    weights, data and dropout mask: loss and every parameter's gradient."""
+    eng, mc = _engine(cuda, use_graph=False, preset="gpt2-small", vocab=50258, batch=8)
+    b = next(get_batch_iterator(8, mc.max_seq_len + 1))
+    p0 = {n: eng.flat.p(n).detach().clone() for n in eng.flat.slots}  # before the step's AdamW
+    eng.set_batch(b)
+    eng.run_step()
+    loss = eng.loss_value()
+    grads = {n: eng.flat.g(n).detach().clone() for n in eng.flat.slots}
+    del eng
+    torch.cuda.empty_cache()
+    params = {n: t.requires_grad_(True) for n, t in p0.items()}
+    ids, lab = torch.from_numpy(b[:, :-1]).to(cuda), torch.from_numpy(b[:, 1:]).to(cuda)
+    lo = oracle_loss(mc, params, ids, lab, 0, 0)
+    lo.backward()
+    assert abs(loss - lo.item()) < 1e-2, (loss, lo.item())
+    worst = []
+    for n, g in grads.items():
+        go = params[n].grad
+        if n.endswith("qkv.b"):  # the key bias's gradient is analytically zero (softmax shift invariance)
+            g, go = g.view(3, -1)[[0, 2]], go.view(3, -1)[[0, 2]]
+        err = ((g - go).norm() / (go.norm() + 1e-12)).item()
+        worst.append((err, n))
+        assert err < 5e-2, f"{n}: relative grad error {err:.3e}"
+    print("worst relative grad errors:", sorted(worst)[-5:])
+
+
 def test_graph_replay_matches_eager(cuda):
     losses = {}
     for mode in (False, True):
