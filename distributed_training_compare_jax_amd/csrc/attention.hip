@@ -644,133 +644,6 @@ __global__ void __launch_bounds__(CH_THREADS) attn_fwd_chunk_kernel(const bf16* 
   }
 }
 
-// Two query groups per wave (32 rows): the K and V fragments a wave reads from LDS for a 64-key tile
-// feed the MFMAs of BOTH groups, halving LDS read traffic per score (the single-group kernel reads
-// 16 fragments per 16 MFMAs: with 16 waves per CU the fragment reads take ~2x the MFMA time).  8 waves
-// x 32 rows = the same 256 queries per block; one barrier per 128 keys.  64-key tiles and 32-row wave
-// groups are both aligned, so a tile is needed by both groups of a wave or by neither.
-constexpr int CH2_THREADS = 512;
-template <int HD>
-__global__ void __launch_bounds__(CH2_THREADS) attn_fwd_chunk2_kernel(const bf16* __restrict__ qkv,
-                                                                     bf16* __restrict__ o, float* __restrict__ lse,
-                                                                     int B, int T, int H, float scale) {
-  constexpr int KC = HD / 32, HT = HD / 16, QG = 2;
-  using L = AttnLds<HD>;
-  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nqb = (T + CH_QROWS - 1) / CH_QROWS, nbh = B * H;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);
-  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
-  const long ts = 3L * H * HD;
-  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
-  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
-  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
-  const int qbase = qblk * CH_QROWS + 32 * w;  // this wave's rows qbase .. qbase + 31
-  int q[QG];
-  bf16x8 qf[QG][KC];
-#pragma unroll
-  for (int gq = 0; gq < QG; ++gq) {
-    q[gq] = qbase + 16 * gq + j;
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      qf[gq][kc] = q[gq] < T ? *(const bf16x8*)(Qb + (long)q[gq] * ts + kc * 32 + 8 * g) : bf16x8{};
-  }
-  const float c = scale * LOG2E;
-  float m[QG], l[QG];
-  f32x4 acc[QG][HT];
-#pragma unroll
-  for (int gq = 0; gq < QG; ++gq) {
-    m[gq] = -INFINITY;
-    l[gq] = 0.f;
-#pragma unroll
-    for (int t = 0; t < HT; ++t) acc[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-
-  auto body = [&](const bf16* sK, const bf16* sV, int it) {
-#pragma unroll
-    for (int t2 = 0; t2 < CH_KEYS / 64; ++t2) {
-      const int kb = it * CH_KEYS + t2 * 64;
-      if (kb > qbase + 31 || qbase >= T) continue;  // wave-uniform (see above)
-      const bool diag = kb + 63 > qbase;
-      const bf16* tK = sK + t2 * 64 * L::KLD;
-      const bf16* tV = sV + t2 * 64 * L::VLD;
-      f32x4 sc[QG][4];
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-#pragma unroll
-        for (int gq = 0; gq < QG; ++gq) sc[gq][st] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-          const bf16x8 kf = row_frag(tK, L::KLD, st * 16, kc * 32, lane);
-#pragma unroll
-          for (int gq = 0; gq < QG; ++gq) sc[gq][st] = mfma(kf, qf[gq][kc], sc[gq][st]);
-        }
-      }
-      bf16x8 pf[QG][2];
-#pragma unroll
-      for (int gq = 0; gq < QG; ++gq) {
-        float mt = -INFINITY;
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float x = sc[gq][st][r];
-            if (diag) {
-              const int key = kb + st * 16 + 4 * g + r;
-              x = (key <= q[gq] && key < T) ? x : -INFINITY;
-            }
-            sc[gq][st][r] = x;
-            mt = fmaxf(mt, x);
-          }
-        mt = group_max(mt) * c;
-        const float mn = fmaxf(m[gq], mt);
-        const float alpha = fast_exp2(m[gq] - mn);
-        m[gq] = mn;
-        float ls = 0.f;
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pv = fast_exp2(fmaf(sc[gq][st][r], c, -mn));
-            sc[gq][st][r] = pv;
-            ls += pv;
-          }
-        l[gq] = l[gq] * alpha + ls;
-#pragma unroll
-        for (int t = 0; t < HT; ++t) acc[gq][t] *= alpha;
-        pf[gq][0] = pack_p(sc[gq][0], sc[gq][1]);
-        pf[gq][1] = pack_p(sc[gq][2], sc[gq][3]);
-      }
-#pragma unroll
-      for (int t = 0; t < HT; ++t) {
-        const bf16x8 v0 = tr_frag(tV, L::VLD, 0, t * 16, lane), v1 = tr_frag(tV, L::VLD, 32, t * 16, lane);
-#pragma unroll
-        for (int gq = 0; gq < QG; ++gq) {
-          acc[gq][t] = mfma(v0, pf[gq][0], acc[gq][t]);
-          acc[gq][t] = mfma(v1, pf[gq][1], acc[gq][t]);
-        }
-      }
-    }
-  };
-  const int nch = (min(T, qblk * CH_QROWS + CH_QROWS) + CH_KEYS - 1) / CH_KEYS;
-  pipelined_tiles<HD, CH_KEYS, CH2_THREADS>(nch, [](int it) { return it * CH_KEYS; }, Kb, ts, Vb, ts, T, lds, L::KLD,
-                                            L::VLD, tid, body);
-#pragma unroll
-  for (int gq = 0; gq < QG; ++gq) {
-    const float ll = group_sum(l[gq]);
-    if (q[gq] < T) {
-      const float inv = 1.f / ll;
-      bf16* orow = o + ((long)b * T + q[gq]) * H * HD + h * HD;
-#pragma unroll
-      for (int t = 0; t < HT; ++t)
-        *(bf16x4*)(orow + t * 16 + 4 * g) = bf16x4{f2bf(acc[gq][t][0] * inv), f2bf(acc[gq][t][1] * inv),
-                                                    f2bf(acc[gq][t][2] * inv), f2bf(acc[gq][t][3] * inv)};
-      if (g == 0) lse[((long)b * H + h) * T + q[gq]] = (m[gq] + __log2f(ll)) * LN2;
-    }
-  }
-}
-
 // Chunked backward for T > RES_MAXT / head_dim 64 (the tiled kernels above with 16 waves = 256
 // rows per block, 128-row Q/dO or K/V chunks, wave-uniform tile skips, diagonal-only masks and a
 // grid-wide heavy-first block order; see attn_fwd_chunk_kernel).
@@ -1484,14 +1357,7 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
   }
   if (attn_chunk_enabled() && (HD == 32 || HD == 64)) {
     const dim3 g(B * H * ((T + CH_QROWS - 1) / CH_QROWS));
-    // DTC_ATTN_QG=2: two 16-row query groups per wave (attn_fwd_chunk2_kernel, half the K/V fragment
-    // reads; correct but measured slower: 36.8 vs 33.7 us, profiles/r3_ab_attn_qg.log)
-    static const int qg = [] { const char* v = getenv("DTC_ATTN_QG"); return v ? atoi(v) : 1; }();
-    if (HD == 64 && qg == 2) {
-      allow_lds(attn_fwd_chunk2_kernel<64>, ch_lds_fwd<64>());
-      hipLaunchKernelGGL(attn_fwd_chunk2_kernel<64>, g, dim3(CH2_THREADS), ch_lds_fwd<64>(), st, qkv, o, lse, B, T, H,
-                         scale);
-    } else if (HD == 64) {
+    if (HD == 64) {
       allow_lds(attn_fwd_chunk_kernel<64>, ch_lds_fwd<64>());
       hipLaunchKernelGGL(attn_fwd_chunk_kernel<64>, g, dim3(CH_THREADS), ch_lds_fwd<64>(), st, qkv, o, lse, B, T, H, scale);
     } else {

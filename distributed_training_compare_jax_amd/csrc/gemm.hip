@@ -1098,126 +1098,9 @@ __device__ __forceinline__ bf16x8 big_frag(const bf16* img, int t, int kk, int l
   }
 }
 
-template <bool AK, bool BKM, int EPI, bool OUTF32>
-__global__ void __launch_bounds__(NT2, 1)
-gemm256_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
-               int tiles_m, int tiles_n, int gm, int split, int k_per_split, float* __restrict__ slab, Epi e) {
-  constexpr int TM = 8, TN = 4;  // 16x16 fragments per wave: 128 (m) x 64 (n)
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int ntiles = tiles_m * tiles_n;
-  const int lid = xcd_remap(blockIdx.x, ntiles * split);
-  const int tile = lid % ntiles, z = lid / ntiles;
-  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
-  const int gm_eff = min(gm, tiles_m - grp * gm);
-  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
-  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
-  const int kbeg = z * k_per_split;
-  const int nk = min(k_per_split, K - kbeg) / 64;
-
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  dma_tile<AK>(A, lda, m0, M, kbeg, smem, wave, lane);
-  dma_tile<BKM>(B, ldb, n0, N, kbeg, smem + IMG, wave, lane);
-  EpiPre<TN, TM> pre;  // epilogue operands: loaded under the main loop, not after it
-  if (split == 1 && (EPI == EPI_LMHEAD || EPI == EPI_STORE))
-    epi_prefetch<TN, TM>(e, m0 + wm * 128, n0 + wn * 64, lane, EPI == EPI_LMHEAD, pre);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (EPI == EPI_LMHEAD && split == 1) {  // the bias is the accumulators' starting value
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = pre.bb[i];
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const bf16* sA = smem + (kt & 1) * 2 * IMG;
-    const bf16* sB = sA + IMG;
-    if (kt + 1 < nk) {
-      bf16* nA = smem + ((kt + 1) & 1) * 2 * IMG;
-      dma_tile<AK>(A, lda, m0, M, kbeg + (kt + 1) * 64, nA, wave, lane);
-      dma_tile<BKM>(B, ldb, n0, N, kbeg + (kt + 1) * 64, nA + IMG, wave, lane);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 fa[TM], fb[TN];
-#pragma unroll
-      for (int j = 0; j < TM; ++j) fa[j] = big_frag<AK>(sA, wm * 8 + j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TN; ++i) fb[i] = big_frag<BKM>(sB, wn * 4 + i, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 landed
-    __syncthreads();                                  // ... and every other wave's; reads of kt done
-  }
-
-  const int g4 = 4 * (lane >> 4);
-  if (split > 1) {  // fp32 slab z; splitk_reduce sums the slabs in a fixed order
-    float* sl = slab + (long)z * M * N;
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        const int m = m0 + wm * 128 + j * 16 + (lane & 15);
-        const int n = n0 + wn * 64 + i * 16 + g4;
-        if (m < M && n < N) *(f32x4*)(sl + (long)m * N + n) = acc[i][j];  // N % 4 == 0 (checked by host)
-      }
-    return;
-  }
-  bf16* stage = smem + wave * (128 * 64);  // main-loop buffers are free after the last barrier
-  if (EPI == EPI_LMHEAD) {
-    lmhead_epilogue<TN, TM, true, true>(acc, e, m0 + wm * 128, n0 + wn * 64, tn_idx * 4 + wn, lane, pre, stage);
-    return;
-  }
-  if (EPI == EPI_STORE && !OUTF32) {
-    f32x4 bb[TN];
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wn * 64 + i * 16 + g4;
-      bb[i] = pre.bb[i];
-      if (e.bias && n < N && n + 4 > N)
-        for (int r = 0; r < 4; ++r) bb[i][r] = n + r < N ? e.bias[n + r] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < TM; ++j)
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        bf16x4 ob;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ob[r] = f2bf(e.alpha * acc[i][j][r] + bb[i][r]);
-        stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
-      }
-    stage_out<128>(stage, (bf16*)e.C, e.ldc, m0 + wm * 128, n0 + wn * 64, M, N, lane);
-    return;
-  }
-  if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      int m = m0 + wm * 128 + j * 16 + (lane & 15);
-      int n = n0 + wn * 64 + i * 16 + g4;
-      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
-    }
-}
-
 // ============================================================================================
 // 256x256 tile, phase-interleaved ("ping-pong") main loop: the same tile, waves and epilogues as
-// gemm256_kernel, with the staging pipeline rebuilt for ~1 block per CU
+// a plain 2-buffer 256^2 loop (the round-2 gemm256_kernel), with the staging pipeline rebuilt for ~1 block per CU
 // (cdna_hip_programming.md §5 "The 256² 8-phase template", T3-T5):
 //  * each K-step (64 k) is 4 phases; in phase p a wave ds-reads its A fragments of output rows
 //    32p..32p+31 (+ all its B fragments at p = 0), issues 2 LDS-DMA instructions of the pipeline,
@@ -1844,256 +1727,6 @@ gemm8n_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 }
 
 // ============================================================================================
-// Stream-K form of gemm8p_kernel for layer-sized GEMMs (a few hundred 256^2 tiles of 12-48 K-steps:
-// whole tiles per block would leave the last round of blocks mostly empty and pay a prologue and an
-// epilogue per tile).  The grid is one block per CU; the ntiles * nk K-steps are cut into equal
-// contiguous ranges of L, one per block, so every CU does the same MFMA work.  A block's range runs
-// through the phase pipeline as ONE K-step stream (the DMA of the next tile's first K-steps is in
-// flight while a tile finishes).  A range cuts at most two tiles; a cut tile's pieces store fp32
-// partials (wave-fragment order, coalesced) and bump the tile's counter; the last arriver sums all
-// pieces IN PIECE ORDER (deterministic) and runs the epilogue (agent-scope release / acquire around
-// the counter: cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2).  No block ever
-// waits for another, so a partly occupied chip cannot deadlock it.
-struct SkPlan {
-  int tiles_m, tiles_n, gm, nk, L, iters;
-  float* part;  // [2 * grid][256 * 256] fp32 piece partials (slot 2c: block c's first piece, 2c+1: its last)
-  int* cnt;     // [tiles] arrival counters, zero between launches (the last arriver resets its tile's)
-};
-
-__device__ __forceinline__ void sk_tile(const SkPlan& s, int T, int& tm, int& tn) {
-  const int grp = T / (s.gm * s.tiles_n), in_g = T % (s.gm * s.tiles_n);
-  const int gm_eff = min(s.gm, s.tiles_m - grp * s.gm);
-  tm = grp * s.gm + in_g % gm_eff;
-  tn = in_g / gm_eff;
-}
-
-// Epilogue of one wave's 128 x 64 from registers (the pipeline owns the LDS).  Its operand loads go
-// out a column of fragments at a time before any is used (see the fixup above); N % 4 == 0.
-template <int EPI, bool OUTF32>
-__device__ __forceinline__ void sk_epilogue(const f32x4 (&acc)[4][8], const Epi& e, int m_w, int n_w, int lane) {
-  constexpr int TN = 4;
-  const int g4 = 4 * (lane >> 4), li = lane & 15;
-  f32x4 bias[TN];
-#pragma unroll
-  for (int i = 0; i < TN; ++i) {
-    const int n = n_w + i * 16 + g4;
-    bias[i] = (e.bias && n < e.N) ? *(const f32x4*)(e.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  constexpr bool AUX = EPI == EPI_RESID || EPI == EPI_DGELU || (EPI == EPI_STORE && OUTF32);
-#pragma unroll
-  for (int h = 0; h < 2 * TN; ++h) {
-    const int i = h >> 1, j0 = (h & 1) * 4;
-    const int n = n_w + i * 16 + g4;
-    f32x4 ax[4];
-    if constexpr (AUX) {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int m = m_w + (j0 + jj) * 16 + li;
-        ax[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (m < e.M && n < e.N) {
-          if (EPI == EPI_RESID) ax[jj] = *(const f32x4*)((const float*)e.aux + (long)m * e.ldaux + n);
-          if (EPI == EPI_DGELU) {
-            const bf16x4 u = *(const bf16x4*)((const bf16*)e.aux + (long)m * e.ldaux + n);
-            ax[jj] = f32x4{(float)u[0], (float)u[1], (float)u[2], (float)u[3]};
-          }
-          if (EPI == EPI_STORE && OUTF32 && e.beta != 0.f) ax[jj] = *(const f32x4*)((const float*)e.C + (long)m * e.ldc + n);
-        }
-      }
-    }
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int m = m_w + (j0 + jj) * 16 + li;
-      if (m >= e.M || n >= e.N) continue;
-      f32x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = e.alpha * acc[i][j0 + jj][r] + bias[i][r];
-      if (EPI == EPI_RESID) o += ax[jj];
-      if (EPI == EPI_DGELU) o *= ax[jj];
-      if (EPI == EPI_STORE && OUTF32 && e.beta != 0.f) o += e.beta * ax[jj];
-      if (OUTF32) {
-        *(f32x4*)((float*)e.C + (long)m * e.ldc + n) = o;
-      } else {
-        bf16x4 ob, gb;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (EPI == EPI_GELU) {  // C = gelu'(u) (read in the backward only: non-temporal), aux_out = gelu(u)
-            float gv, dgv;
-            gelu_tanh_and_grad_f(o[r], gv, dgv);
-            ob[r] = f2bf(dgv);
-            gb[r] = f2bf(gv);
-          } else {
-            ob[r] = f2bf(o[r]);
-          }
-        }
-        if (EPI == EPI_GELU) {
-          __builtin_nontemporal_store(ob, (bf16x4*)((bf16*)e.C + (long)m * e.ldc + n));
-          *(bf16x4*)((bf16*)e.aux_out + (long)m * e.ldc + n) = gb;
-        } else {
-          *(bf16x4*)((bf16*)e.C + (long)m * e.ldc + n) = ob;
-        }
-      }
-    }
-  }
-}
-
-template <bool AK, bool BKM, int EPI, bool OUTF32>
-__global__ void __launch_bounds__(NT2, 1)
-gemm_sk_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, SkPlan s, Epi e) {
-  constexpr int TM = 8, TN = 4;
-  // pipeline buffers + one word (the counter broadcast): a single LDS object (§5 trap 4a)
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG + 8];
-  int* bcast = (int*)(smem + 4 * IMG);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int G = gridDim.x;
-  const int c = xcd_remap(blockIdx.x, G);  // logical block: each XCD runs a contiguous stretch of the stream
-  const int it0 = c * s.L, it1 = min(s.iters, it0 + s.L);
-  if (it0 >= it1) return;
-  const int n_it = it1 - it0;
-
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto imgA = [&](int j) { return smem + (j & 1) * 2 * IMG; };
-  auto imgB = [&](int j) { return smem + (j & 1) * 2 * IMG + IMG; };
-  // Running (tile, k-step) coordinates, advanced once per step (no divisions in the phases): the
-  // A stream runs one step ahead (step j+1), the B stream two (step j+2), `cur` is step j.
-  struct Pos { int T, k, base; };  // base: the tile's first row (A) / column (B)
-  auto tile_of = [&](int T, bool rows) { int tm, tn; sk_tile(s, T, tm, tn); return (rows ? tm : tn) * BIG; };
-  auto advance = [&](Pos& q, bool rows) {
-    if (++q.k == s.nk) { q.k = 0; ++q.T; if (q.T * s.nk < s.iters) q.base = tile_of(q.T, rows); }
-  };
-  Pos cur{it0 / s.nk, it0 % s.nk, 0};
-  Pos pa = cur, pb = cur;
-  pa.base = tile_of(pa.T, true);
-  pb.base = tile_of(pb.T, false);
-  auto dmaA = [&](const Pos& q, int j, int c4) { p8_dma<AK>(A, lda, q.base, M, q.k * 64, imgA(j), c4, wave, lane); };
-  auto dmaB = [&](const Pos& q, int j, int c4) { p8_dma<BKM>(B, ldb, q.base, N, q.k * 64, imgB(j), c4, wave, lane); };
-
-  // prologue: B(0), A(0), B(1); afterwards pa = step 1, pb = step 2
-#pragma unroll
-  for (int q = 0; q < 4; ++q) dmaB(pb, 0, q);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) dmaA(pa, 0, q);
-  advance(pa, true);
-  advance(pb, false);
-  if (n_it > 1) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dmaB(pb, 1, q);
-    advance(pb, false);
-    P8_VMCNT(4);
-  } else {
-    P8_VMCNT(0);
-  }
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();
-
-  // piece partials: write-through (sc1) 16-B stores and sc1 loads, so no L2 writeback / invalidate
-  // fence is needed around the counter (§6 Guideline 16 R1); slot = 256 KB, wave-fragment order
-  const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc((void*)s.part, (short)0, 0x7fffffff, 0x00020000);
-  constexpr int SC1 = 16;
-
-  bf16x8 fb[TN][2], fa[2][2];
-  for (int j = 0; j < n_it; ++j) {
-    const bf16* sA = imgA(j);
-    const bf16* sB = imgB(j);
-    const bool more1 = j + 1 < n_it, more2 = j + 2 < n_it;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      if (p == 0) {
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) fb[i][kk] = p8_frag<BKM>(sB, 4 * wc + i, kk, lane);
-      }
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) fa[jj][kk] = p8_frag<AK>(sA, 8 * wr + 2 * p + jj, kk, lane);
-      if (p < 2) {
-        if (more1) { dmaA(pa, j + 1, p); dmaA(pa, j + 1, p + 2); }
-      } else {
-        if (more2) { dmaB(pb, j + 2, 2 * p - 4); dmaB(pb, j + 2, 2 * p - 3); }
-      }
-      __builtin_amdgcn_s_barrier();
-      p8_lgkm_wait(fa, fb);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            acc[i][2 * p + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i][kk], fa[jj][kk], acc[i][2 * p + jj], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      if (p == 0) {
-        if (more1) P8_VMCNT(6); else P8_VMCNT(0);
-      } else if (p == 2) {
-        if (more2) P8_VMCNT(4); else if (more1) P8_VMCNT(2); else P8_VMCNT(0);
-      }
-      __builtin_amdgcn_s_barrier();
-    }
-    const int T = cur.T, k = cur.k;
-    advance(pa, true);
-    advance(pb, false);
-    if (++cur.k == s.nk) { cur.k = 0; ++cur.T; }
-    if (k != s.nk - 1 && j != n_it - 1) continue;  // not the end of a piece
-    // ---------------- piece end: realign the two wave groups (block-wide barriers from here on)
-    if (wr == 0) __builtin_amdgcn_s_barrier();
-    int tm, tn;
-    sk_tile(s, T, tm, tn);
-    const int m_w = tm * BIG + wr * 128, n_w = tn * BIG + wc * 64;
-    const int k_first = j >= k ? 0 : k - j;  // this piece covers the tile's k-steps [k_first, k]
-    bool emit = true;
-    if (k_first != 0 || k != s.nk - 1) {
-      // a cut tile: pieces are the blocks c_lo..c_hi covering its K-steps
-      const int c_lo = (T * s.nk) / s.L, c_hi = ((T + 1) * s.nk - 1) / s.L;
-      const int np = c_hi - c_lo + 1;
-      // byte offset of block cb's slot for this tile (slot 2cb: cb's first piece, 2cb+1: its last)
-      auto slot = [&](int cb) { return (2 * cb + ((cb * s.L) / s.nk == T ? 0 : 1)) * (65536 * 4) + wave * (TN * TM * 1024); };
-      const int mine = slot(c);
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int jj = 0; jj < TM; ++jj)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][jj]), rsP,
-                                                 mine + ((i * TM + jj) * 64 + lane) * 16, 0, SC1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) *bcast = __hip_atomic_fetch_add(s.cnt + T, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      emit = *bcast == np - 1;
-      if (emit) {  // last arriver: acc = sum of every piece in piece order (its own read back too:
-                   // no per-element register-or-load select, §5 trap 4c)
-        if (tid == 0) __hip_atomic_store(s.cnt + T, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int pi = 0; pi < np; ++pi) {
-          const int src = slot(c_lo + pi);
-#pragma unroll
-          for (int h = 0; h < 2 * TN; ++h) {  // 4 loads out before any use: one round trip per batch
-            const int i = h >> 1, j0 = (h & 1) * 4;
-            f32x4 v[4];
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj)
-              v[jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, src + ((i * TM + j0 + jj) * 64 + lane) * 16, 0, SC1));
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) acc[i][j0 + jj] = pi == 0 ? v[jj] : acc[i][j0 + jj] + v[jj];
-          }
-        }
-      }
-    }
-    if (emit) sk_epilogue<EPI, OUTF32>(acc, e, m_w, n_w, lane);
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int jj = 0; jj < TM; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (j + 1 < n_it && wr == 1) __builtin_amdgcn_s_barrier();  // re-stagger for the next piece
-  }
-}
-
-// ============================================================================================
 // lm_head backward with the cross-entropy backward fused into the dgrad's A operand.
 //   dlogits[t][v] = (exp(logit[t][v] - lse[t]) - [v == label[t]]) * scale   (pad columns 0)
 //   dX[t][:]      = sum_v dlogits[t][v] * W[v][:]    (NT split-K on W^T, as the unfused dgrad)
@@ -2141,7 +1774,7 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
   const int kbeg = z * a.kps;
   const int nk = min(a.kps, a.K - kbeg) / 64;
   // the dlogits stores + column sums of k-step kt go to n-tile kt % 2 (the two n-tiles share them)
-  // no dlogits output (the weight gradient recomputes them, ce_wgrad256_kernel): nothing to own
+  // no dlogits output requested: nothing to own
   const int nown = a.dlogits ? min(a.tiles_n, 2) : 0;
   auto owns = [&](int kt) { return tn_idx < nown && kt % nown == tn_idx; };
 
@@ -2259,144 +1892,6 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
       const int m = m0 + wm * 128 + j * 16 + (lane & 15);
       const int n = n0 + wn * 64 + i * 16 + g4;
       if (m < a.M && n < a.N) *(f32x4*)(sl + (long)m * a.N + n) = acc[i][j];
-    }
-}
-
-// ============================================================================================
-// lm_head WEIGHT gradient with the cross-entropy backward fused into its A operand:
-//   dW[v][d] = beta*dW[v][d] + sum_t dlogits[t][v] * h[t][d]      (TN: both operands token-major)
-//   db[v]    = beta*db[v]    + sum_t dlogits[t][v]                 (fp32, summed before any rounding)
-// dlogits is never stored: each block recomputes its [64 tokens][256 vocab] slice of it from the bf16
-// logits on the way into the LDS image (ce_grad8, the same bits ce_dgrad256 / ce_bwd produce), so
-// the lm_head backward reads the logits twice (dgrad, wgrad) and writes nothing of size tokens x
-// vocab (round 2 wrote and re-read 412 / 824 MB of dlogits per step).  The A image is the MN-major
-// [64 k][256 m] layout of dma_tile<false> (16-B chunk c of k-row r at c ^ mn_swz(r)), so the MFMA
-// fragment reads are the verified big_frag<false> ones; h (B) still streams by LDS DMA.  Each
-// thread stages the SAME 8 vocab columns for every k-row (columns tid % 32), so the bias gradient is
-// 8 register sums per thread + one fixed-order LDS combine at the end (n-tile 0 blocks write it).
-struct CeWgradArgs {
-  const bf16* logits; long ldl;   // [tokens][V] bf16 (A, m = vocab, k = token)
-  const float* lse; const int* labels; int vocab_start, n_valid; float scale;
-  const bf16* h; long ldh;        // [tokens][D] bf16 (B, n = d, k = token)
-  float* dw; long lddw;           // [V][D] fp32
-  float* db;                      // [V] fp32 (or null)
-  float beta;
-  int M, N, K, tiles_m, tiles_n, gm;  // M = V, N = D, K = tokens
-};
-
-__global__ void __launch_bounds__(NT2, 1) ce_wgrad256_kernel(CeWgradArgs a) {
-  constexpr int TM = 8, TN = 4;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * IMG];  // [buf][A img | B img], 128 KB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int ntiles = a.tiles_m * a.tiles_n;
-  const int tile = xcd_remap(blockIdx.x, ntiles);
-  const int grp = tile / (a.gm * a.tiles_n), in_g = tile % (a.gm * a.tiles_n);
-  const int gm_eff = min(a.gm, a.tiles_m - grp * a.gm);
-  const int tm_idx = grp * a.gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
-  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
-  const int nk = a.K / 64;
-
-  // staging: 8 vocab columns v0 = m0 + 8*cc of k-rows kr0 + 16q (q = 0..3) of each 64-token k-step
-  const int cc = tid & 31, kr0 = tid >> 5;
-  const int v0 = m0 + cc * 8;
-  const int vload = min(v0, a.M - 8);  // ragged vocab edge: clamped (those columns are never stored)
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  u32x4 R[4];
-  float cr[4];
-  int lab[4];
-  auto load_a = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int t = k0 + kr0 + 16 * q;
-      R[q] = *(const u32x4*)(a.logits + (long)t * a.ldl + vload);
-      cr[q] = a.lse[t];
-      lab[q] = a.labels[t];
-    }
-  };
-  auto put_a = [&](bf16* img) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float g[8];
-      ce_grad8(__builtin_bit_cast(bf16x8, R[q]), v0, ce_row_c(cr[q], a.scale), lab[q] - a.vocab_start, a.n_valid,
-               a.scale, g);
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        cs[e] += g[e];
-        o[e] = f2bf(g[e]);
-      }
-      const int kr = kr0 + 16 * q;
-      *(bf16x8*)(img + kr * 256 + ((cc ^ mn_swz(kr)) << 3)) = o;
-    }
-  };
-
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  dma_tile<false>(a.h, a.ldh, n0, a.N, 0, smem + IMG, wave, lane);
-  if (nk > 0) {
-    load_a(0);
-    put_a(smem);
-  }
-  if (nk > 1) load_a(64);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const bf16* sA = smem + (kt & 1) * 2 * IMG;
-    const bf16* sB = sA + IMG;
-    bf16* nA = smem + ((kt + 1) & 1) * 2 * IMG;
-    const bool more = kt + 1 < nk, more2 = kt + 2 < nk;
-    if (more) {
-      dma_tile<false>(a.h, a.ldh, n0, a.N, (kt + 1) * 64, nA + IMG, wave, lane);
-      put_a(nA);
-    }
-    if (more2) load_a((kt + 2) * 64);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 fa[TM], fb[TN];
-#pragma unroll
-      for (int j = 0; j < TM; ++j) fa[j] = big_frag<false>(sA, wm * 8 + j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TN; ++i) fb[i] = big_frag<false>(sB, wn * 4 + i, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-    }
-    // the k+2 loads (12 ops, issued after this k-step's DMA) may stay in flight across the barrier
-    if (more2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // bias gradient: the 16 threads of column group cc combine in a fixed order (n-tile 0 writes)
-  if (a.db && tn_idx == 0) {
-    float* red = (float*)smem;  // the main-loop buffers are free after the last barrier
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[kr0 * 256 + cc * 8 + e] = cs[e];
-    __syncthreads();
-    if (tid < 256 && m0 + tid < a.M) {
-      float s = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s += red[r * 256 + tid];
-      float* d = a.db + m0 + tid;
-      *d = (a.beta != 0.f ? a.beta * *d : 0.f) + s;
-    }
-  }
-  Epi e{};
-  e.M = a.M; e.N = a.N; e.C = a.dw; e.ldc = a.lddw; e.alpha = 1.f; e.beta = a.beta;
-  const int g4 = 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wm * 128 + j * 16 + (lane & 15);
-      const int n = n0 + wn * 64 + i * 16 + g4;
-      if (m < a.M && n < a.N) epilogue_store<EPI_STORE, true>(e, m, n, acc[i][j]);
     }
 }
 
@@ -3005,76 +2500,14 @@ int big_split(int layout, int M, int N, int K) {
 
 inline int big_kps(int K, int split) { return ((K / 64 + split - 1) / split) * 64; }
 
-// ---- stream-K (gemm_sk_kernel): one workspace per device (piece partials + tile counters), allocated
-// on first use OUTSIDE graph capture.  Only forwards and dgrads take this path, which never run on two
-// streams at once (the optional side stream carries weight gradients), so one workspace suffices.
-struct SkWs { int dev; float* part; int* cnt; };
-constexpr int SK_MAX_DEV = 16, SK_MAX_TILES = 1 << 16;
-static SkWs g_skws[SK_MAX_DEV];
-static int g_nskws = 0;
-
-static int sk_cus() {
+// compute units of the current device (one-block-per-CU persistent grids)
+static int cu_count() {
   static const int n = [] {
     int d = 0, v = 0;
     if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) v = 0;
     return v > 0 ? v : 256;
   }();
   return n;
-}
-
-static const SkWs* sk_ws(hipStream_t st) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  for (int i = 0; i < g_nskws; ++i) if (g_skws[i].dev == dev) return &g_skws[i];
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  if (g_nskws == SK_MAX_DEV) return nullptr;
-  SkWs w{dev, nullptr, nullptr};
-  if (hipMalloc(&w.part, (size_t)2 * sk_cus() * 65536 * sizeof(float)) != hipSuccess) return nullptr;
-  if (hipMalloc(&w.cnt, SK_MAX_TILES * sizeof(int)) != hipSuccess) return nullptr;
-  if (hipMemset(w.cnt, 0, SK_MAX_TILES * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
-  g_skws[g_nskws++] = w;
-  return &g_skws[g_nskws - 1];
-}
-
-// DTC_GEMM_SK: bit mask of the layouts (1 fwd, 2 dgrad) whose layer-sized GEMMs run stream-K.  A
-// problem qualifies when its 256^2 tiles would leave the chip unevenly loaded as whole tiles.
-static int g_sk_mask = [] { const char* v = getenv("DTC_GEMM_SK"); return v ? atoi(v) : 0; }();
-static int sk_mask() { return g_sk_mask; }
-static bool sk_wanted(int layout, int M, int N, int K) {
-  if (!(sk_mask() & (1 << layout)) || K % 64 || N % 4 || M < 256 || N < 256) return false;
-  if (layout != 0 && N % 8) return false;
-  const long tiles = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
-  if (tiles > SK_MAX_TILES) return false;
-  const long iters = tiles * (K / 64);
-  return iters >= 2L * sk_cus();  // at least 2 K-steps per CU
-}
-
-template <bool AK, bool BKM, int EPI, bool OUTF32>
-int launch_sk(const GemmArgs& a, hipStream_t st) {
-  const SkWs* ws = sk_ws(st);
-  if (!ws) return -1;  // no workspace (first use under capture): caller takes the tiled path
-  Epi e{};
-  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
-  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
-  SkPlan p{};
-  p.tiles_m = (a.M + BIG - 1) / BIG;
-  p.tiles_n = (a.N + BIG - 1) / BIG;
-  p.nk = a.K / 64;
-  const long iters = (long)p.tiles_m * p.tiles_n * p.nk;
-  const int G0 = sk_cus();
-  p.L = (int)((iters + G0 - 1) / G0);
-  p.iters = (int)iters;
-  const int G = (int)((iters + p.L - 1) / p.L);
-  // an XCD's 1/8 of the stream: groups of gm M-tiles sweep the N-tiles within it
-  const long per_xcd = std::max(1L, (iters / 8) / p.nk);
-  p.gm = (int)std::max(1L, std::min((long)p.tiles_m, per_xcd / std::max(1, p.tiles_n)));
-  p.part = ws->part;
-  p.cnt = ws->cnt;
-  hipLaunchKernelGGL((gemm_sk_kernel<AK, BKM, EPI, OUTF32>), dim3(G), dim3(NT2), 0, st, (const bf16*)a.A, a.lda,
-                     (const bf16*)a.B, a.ldb, a.M, a.N, p, e);
-  DTC_CHECK_LAUNCH();
-  return 0;
 }
 
 template <bool AK, bool BKM, int EPI, bool OUTF32>
@@ -3095,18 +2528,9 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, 32 / tiles_n));
   const int kps = big_kps(a.K, split);
   if (split > 1 && (a.ws_bytes < (long)split * a.M * a.N * 4 || a.N % 4)) return 1005;
-  // DTC_GEMM8P: 2 = the phase-interleaved main loop (gemm8p_kernel) for every layout, 1 = only with a
-  // K-major A operand, 0 = gemm256_kernel.  GPT-2 small lm_head: forward 793 -> 770 us, vocab-K dgrad
-  // 852 -> 636 us, weight gradient 843 -> 679 us (profiles/r3_gemm8p.md).
-  static const int p8 = [] { const char* v = getenv("DTC_GEMM8P"); return v ? atoi(v) : 2; }();
-  if (p8 == 2 || (p8 == 1 && AK))
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
-                       (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
-                       (float*)a.workspace, e);
-  else
-    hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
-                       (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
-                       (float*)a.workspace, e);
+  hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
+                     (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
+                     (float*)a.workspace, e);
   DTC_CHECK_LAUNCH();
   if (split > 1 && !a.defer_reduce) {
     long MN = (long)a.M * a.N;
@@ -3154,7 +2578,7 @@ int launch_n8(const GemmArgs& a, hipStream_t st) {
   const int gm = n8gm > 0 ? std::min(tiles_m, n8gm)
                           : (tiles_n <= 4 ? std::max(1, std::min(tiles_m, 32 / tiles_n)) : std::min(tiles_m, 8));
   constexpr int NS = CB == 3 ? 4 : 3;
-  const int grid = std::min(tiles_m * tiles_n, sk_cus());  // persistent: one block per CU
+  const int grid = std::min(tiles_m * tiles_n, cu_count());  // persistent: one block per CU
   hipLaunchKernelGGL((gemm8n_kernel<CB, NS, AK, BKM, EPI, OUTF32>), dim3(grid), dim3(NT2), 0, st,
                      (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, e);
   DTC_CHECK_LAUNCH();
@@ -3180,53 +2604,6 @@ int launch_n8_any(const GemmArgs& a, int cb, hipStream_t st) {
     if (epi == EPI_STORE) return f32 ? launch_n8cb<true, false, EPI_STORE, true>(a, cb, st)
                                      : launch_n8cb<true, false, EPI_STORE, false>(a, cb, st);
     if (epi == EPI_DGELU && !f32) return launch_n8cb<true, false, EPI_DGELU, false>(a, cb, st);
-  }
-  return -1;
-}
-
-// ---- 256 x 192 tiles on gemm8p_kernel (CB = 3) ------------------------------------------------------
-// DTC_GEMM8P3=1: forwards / dgrads whose N is a multiple of 192 and whose 256 x 192 tile count is a
-// whole number (>= 2) of 256-tile rounds -- GPT-2 small fc1 forward (GELU) and fc2 dgrad (dGELU), N = 3072:
-// 512 tiles, where the 128^2 kernel ran 1536 and the 256^2 one 1.5 rounds.  Measured (profiles/r3_gemm8n.md):
-// fc1 forward 80.2 -> 78.1 us, fc2 dgrad 69.8 -> 78.5 us, whole step 13.22 -> 13.88 ms (the fc2 dgrad also
-// loses its paired weight-gradient launch): off by default.
-static int g_p8cb3 = [] { const char* v = getenv("DTC_GEMM8P3"); return v ? atoi(v) : 0; }();
-
-static bool p8cb3_wanted(int layout, int M, int N, int K, int epi) {
-  if (!g_p8cb3 || layout > 1 || N % 192 || K % 64 || K < 512 || K > 8192) return false;
-  if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU && epi != EPI_DGELU) return false;
-  const long t = (long)((M + BIG - 1) / BIG) * (N / 192);
-  return t >= 512 && t % 256 == 0;
-}
-
-template <bool AK, bool BKM, int EPI, bool OUTF32>
-int launch_p8cb3(const GemmArgs& a, hipStream_t st) {
-  Epi e{};
-  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
-  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
-  const int tiles_m = (a.M + BIG - 1) / BIG, tiles_n = a.N / 192;
-  const int ntiles = tiles_m * tiles_n;
-  // an XCD's ~32 concurrent tiles: 8 M-tiles x 4 N-tiles
-  const int gm = std::min(tiles_m, 8);
-  hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32, 3>), dim3(ntiles), dim3(NT2), 0, st, (const bf16*)a.A, a.lda,
-                     (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, 1, a.K, (float*)nullptr, e);
-  DTC_CHECK_LAUNCH();
-  return 0;
-}
-
-int launch_p8cb3_any(const GemmArgs& a, hipStream_t st) {
-  const int epi = a.epi;
-  const bool f32 = a.c_f32 != 0;
-  if (a.layout == 0) {
-    if (epi == EPI_STORE) return f32 ? launch_p8cb3<true, true, EPI_STORE, true>(a, st)
-                                     : launch_p8cb3<true, true, EPI_STORE, false>(a, st);
-    if (epi == EPI_RESID && f32) return launch_p8cb3<true, true, EPI_RESID, true>(a, st);
-    if (epi == EPI_GELU && !f32) return launch_p8cb3<true, true, EPI_GELU, false>(a, st);
-    if (epi == EPI_DGELU && !f32) return launch_p8cb3<true, true, EPI_DGELU, false>(a, st);
-  } else if (a.layout == 1 && a.N % 8 == 0) {
-    if (epi == EPI_STORE) return f32 ? launch_p8cb3<true, false, EPI_STORE, true>(a, st)
-                                     : launch_p8cb3<true, false, EPI_STORE, false>(a, st);
-    if (epi == EPI_DGELU && !f32) return launch_p8cb3<true, false, EPI_DGELU, false>(a, st);
   }
   return -1;
 }
@@ -3382,8 +2759,6 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
   if (big_split(a1->layout, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
   if (n8_cb(a1->layout, a1->M, a1->N, a1->K, a1->epi)) return 1100;  // dgrad on gemm8n_kernel: own launch
-  if (a1->alpha == 1.f && a1->beta == 0.f && p8cb3_wanted(a1->layout, a1->M, a1->N, a1->K, a1->epi)) return 1100;
-  if (sk_wanted(a1->layout, a1->M, a1->N, a1->K) && a1->colsum == nullptr) return 1100;  // stream-K dgrad: own launch
   if (dmaw_plan(a1->layout, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
       dmaw_plan(2, a2->M, a2->N, a2->K, a2->epi, a2->c_f32 != 0, a2->colsum != nullptr).cfg != W_NONE)
     return 1100;  // the 8-wave kernels run these as two launches
@@ -3440,31 +2815,6 @@ int dtc_ce_dgrad(const bf16* logits, long ldl, const float* lse, const int* labe
   return 0;
 }
 
-// lm_head weight + bias gradient from the logits (ce_wgrad256_kernel): dw [V][D] fp32 (ldw), db [V] fp32
-// (optional), both = beta*old + new.  Token count K % 64 == 0, D % 8 == 0, V % 8 == 0.
-int dtc_ce_wgrad(const bf16* logits, long ldl, const float* lse, const int* labels, int vocab_start, int n_valid,
-                 float scale, const bf16* h, long ldh, float* dw, long lddw, float* db, float beta, int V, int D,
-                 int tokens, hipStream_t st) {
-  if (tokens % 64 || D % 8 || V % 8 || ldl % 8 || ldh % 8 || lddw % 4 || V < 8) return 1310;
-  CeWgradArgs a;
-  a.logits = logits; a.ldl = ldl; a.lse = lse; a.labels = labels; a.vocab_start = vocab_start; a.n_valid = n_valid;
-  a.scale = scale; a.h = h; a.ldh = ldh; a.dw = dw; a.lddw = lddw; a.db = db; a.beta = beta;
-  a.M = V; a.N = D; a.K = tokens;
-  a.tiles_m = (V + BIG - 1) / BIG;
-  a.tiles_n = (D + BIG - 1) / BIG;
-  const int ntiles = a.tiles_m * a.tiles_n;
-  a.gm = a.tiles_m;
-  if (a.tiles_n <= 16) a.gm = std::max(1, std::min(a.tiles_m, (ntiles / 8 + a.tiles_n - 1) / a.tiles_n));
-  hipLaunchKernelGGL(ce_wgrad256_kernel, dim3(ntiles), dim3(NT2), 0, st, a);
-  DTC_CHECK_LAUNCH();
-  return 0;
-}
-
-// Layer GEMM (NT, both operands K-major) with the LayerNorm that follows it fused into the epilogue:
-// a->bwd == 0: C = resid + A.B^T + bias, y = LN(C) (bf16), mean/rstd;  a->bwd == 1: dy = A.B^T (never
-// stored), C = dres + LN'(dy), y = bf16(C), column partials in `part`.  128x64 tiles on the 8-wave DMA
-// kernel (the plan the unfused fp32 forwards / dgrads of these shapes use).  Shapes: M % 128, N % 256,
-// N <= 1024, K % 64.
 int dtc_gemm_ln(const LnArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->M % 128 || a->N % 256 || a->N > 1024 || a->K <= 0 || a->K % 64) return 1400;
   if (a->lda % 8 || a->ldb % 8) return 1400;
@@ -3508,8 +2858,7 @@ int dtc_gemm_wgrad_split(int M, int N, int K, int has_db) {
 // 1 if the weight-gradient GEMM runs on the register-staged kernel, which can fuse the bias
 // gradient (GemmArgs.colsum); the 256^2 and DMA kernels cannot
 int dtc_gemm_wgrad_fuses_colsum(int M, int N, int K) {
-  static const int p8 = [] { const char* v = getenv("DTC_GEMM8P"); return v ? atoi(v) : 2; }();
-  if (big_split(2, M, N, K)) return (p8 == 2 && g_wgrad_cs256) ? 1 : 0;  // gemm8p_kernel sums it with MFMAs
+  if (big_split(2, M, N, K)) return g_wgrad_cs256 ? 1 : 0;  // gemm8p_kernel sums it with MFMAs
   const Plan p = make_plan(M, N, K, 1);
   if (p.bk != 64) return 1;
   return (gemm_dma_mask() & (p.bm == 64 ? 2 : 4)) ? 0 : 1;
@@ -3531,12 +2880,6 @@ int dtc_gemm_set_wgrad256(int on) {
 }
 
 // 256 x 192 gemm8p plans (DTC_GEMM8P3 at load time); returns the previous value
-int dtc_gemm_set_p8cb3(int on) {
-  const int old = g_p8cb3;
-  g_p8cb3 = on;
-  return old;
-}
-
 // gemm8n layout mask (DTC_GEMM8N at load time); returns the previous mask (tests / A/B)
 int dtc_gemm_set_n8(int mask) {
   const int old = g_n8_mask;
@@ -3545,12 +2888,6 @@ int dtc_gemm_set_n8(int mask) {
 }
 
 // stream-K layout mask (DTC_GEMM_SK at load time); returns the previous mask (tests / A/B)
-int dtc_gemm_set_sk(int mask) {
-  const int old = g_sk_mask;
-  g_sk_mask = mask;
-  return old;
-}
-
 int dtc_wg_entry_bytes() { return (int)sizeof(WgEntry); }
 int dtc_wg_max() { return WG_MAX; }
 
@@ -3585,23 +2922,6 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
       const int r = launch_n8_any(*a, cb, st);
       if (r >= 0) return r;
     }
-    if (p8cb3_wanted(a->layout, a->M, a->N, a->K, epi)) {
-      const int r = launch_p8cb3_any(*a, st);
-      if (r >= 0) return r;
-    }
-  }
-  if (a->layout <= 1 && !a->colsum && sk_wanted(a->layout, a->M, a->N, a->K)) {
-    int r = -2;
-    if (a->layout == 0) {
-      if (epi == EPI_STORE) r = f32 ? launch_sk<true, true, EPI_STORE, true>(*a, st) : launch_sk<true, true, EPI_STORE, false>(*a, st);
-      else if (epi == EPI_GELU && !f32) r = launch_sk<true, true, EPI_GELU, false>(*a, st);
-      else if (epi == EPI_RESID && f32) r = launch_sk<true, true, EPI_RESID, true>(*a, st);
-      else if (epi == EPI_DGELU && !f32) r = launch_sk<true, true, EPI_DGELU, false>(*a, st);
-    } else {
-      if (epi == EPI_STORE) r = f32 ? launch_sk<true, false, EPI_STORE, true>(*a, st) : launch_sk<true, false, EPI_STORE, false>(*a, st);
-      else if (epi == EPI_DGELU && !f32) r = launch_sk<true, false, EPI_DGELU, false>(*a, st);
-    }
-    if (r >= 0) return r;
   }
   if (a->layout <= 2 && !(a->layout == 2 && (a->bias || big_split(2, a->M, a->N, a->K)))) {
     const WPlan w = dmaw_plan(a->layout, a->M, a->N, a->K, epi, f32, a->colsum != nullptr);

@@ -56,12 +56,6 @@ def _ce_fused(tokens: int, d: int) -> bool:
     if _CE_FUSED_MODE == "auto":
         return tokens * d <= 4096 * 512
     return _CE_FUSED_MODE == "1"
-# lm_head weight/bias gradients recomputing dlogits from the logits (ops/xent.py ce_wgrad_fused): no
-# tokens x vocab dlogits tensor is written or read (-1.6 GB of HBM traffic per GPT-2 small step) and
-# the bias gradient is summed from fp32 values.  Off by default: the recompute (a second exp pass,
-# register-staged instead of DMA-staged operand) measured 14.57 vs 14.48 ms (GPT-2 small) and 4.73 vs
-# 4.70 ms (reference model), profiles/r3_ab_ce_wgrad.log
-_CE_WGRAD = _os.environ.get("DTC_CE_WGRAD", "0") == "1"
 # Vocab-chunked lm_head + cross-entropy (DTC_CE_CHUNK = vocab columns per chunk, a multiple of 256; 0 =
 # off): the forward keeps only each chunk's per-row (max, sum exp) and label logit (logits of one chunk
 # at a time), the backward recomputes a chunk's logits, turns them into dlogits in place and runs that
@@ -545,35 +539,26 @@ class GPTStage:
         wt = f.wt("lm_head.w")  # transposed mirror: NT split-K dgrad, both operands K-major
         red = self.red
         fused = _ce_fused(x.shape[0], x.shape[1])
-        if wt is not None and fused and logits.is_cuda and _CE_WGRAD and lab.shape[0] % 64 == 0:
-            # dx from the fused CE + dgrad kernel; dW / db from the fused CE + weight-gradient kernel:
-            # the logits are read twice, no dlogits anywhere
-            dyf, dlogits, _ = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt,
-                                               want_dlogits=False)
-            wg = lambda lg=logits, ls=lse, lb=lab, y=yf: X.ce_wgrad_fused(
-                lg, ls, lb, self.v_start, self.v_valid, grad_scale, y, f.g("lm_head.w"), f.g("lm_head.b"), beta)
-            keep = (logits, lse, lab, yf)
+        if wt is not None and fused and logits.is_cuda:
+            # CE backward fused into the dgrad's operand staging (no separate dlogits pass)
+            dyf, dlogits, colp = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt)
         else:
-            if wt is not None and fused and logits.is_cuda:
-                # CE backward fused into the dgrad's operand staging (no separate dlogits pass)
-                dyf, dlogits, colp = X.ce_dgrad_fused(logits, lse, lab, self.v_start, self.v_valid, grad_scale, wt)
-            else:
-                # one pass: dlogits in place + column partials of it (the bias gradient's input)
-                dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale,
-                                                      colpart=True)
-                # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
-                # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
-                dyf = (G.linear_resid(dlogits, wt, None, None) if wt is not None
-                       else G.matmul_nn(dlogits, f.w("lm_head.w")))
-            wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
-                                                    G.colsum(cp, f.g("lm_head.b"), beta, red=red))
-            keep = (dlogits, yf, colp)
-            if self._defer_wg and self.side.stream is None:
-                # the bias gradient from the CE pass's fp32 column partials now; the weight gradient joins
-                # the grouped launch (its 591 tiles at GPT-2 small fill the layers' last round)
-                G.colsum(colp, f.g("lm_head.b"), beta, red=red)
-                self.wg_queue.append((dlogits, yf, f.g("lm_head.w"), None))
-                wg = None
+            # one pass: dlogits in place + column partials of it (the bias gradient's input)
+            dlogits, colp = X.ce_backward_inplace(logits, lse, lab, self.v_start, self.v_valid, grad_scale,
+                                                  colpart=True)
+            # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
+            # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
+            dyf = (G.linear_resid(dlogits, wt, None, None) if wt is not None
+                   else G.matmul_nn(dlogits, f.w("lm_head.w")))
+        wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
+                                                G.colsum(cp, f.g("lm_head.b"), beta, red=red))
+        keep = (dlogits, yf, colp)
+        if self._defer_wg and self.side.stream is None:
+            # the bias gradient from the CE pass's fp32 column partials now; the weight gradient joins
+            # the grouped launch (its 591 tiles at GPT-2 small fill the layers' last round)
+            G.colsum(colp, f.g("lm_head.b"), beta, red=red)
+            self.wg_queue.append((dlogits, yf, f.g("lm_head.w"), None))
+            wg = None
         if wg is None:
             pass
         elif _LMHEAD_WGRAD_MAIN:

@@ -110,9 +110,7 @@ def _declare(lib):
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, i, vp], i),
         "dtc_gemm_wgrad_split": ([i, i, i, i], i),
-        "dtc_gemm_set_sk": ([i], i),
         "dtc_gemm_set_n8": ([i], i),
-        "dtc_gemm_set_p8cb3": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
         "dtc_wgrad_group": ([ctypes.POINTER(WgBatch), vp], i),
         "dtc_wg_entry_bytes": ([], i),
@@ -162,7 +160,6 @@ def _declare(lib):
         "dtc_ce_dgrad": ([vp, l, vp, vp, i, i, f, vp, l, vp, l, vp, vp, i, i, i, vp, l, vp], i),
         "dtc_ce_dgrad_workspace_bytes": ([i, i, i], l),
         "dtc_ce_dgrad_colpart_rows": ([i], i),
-        "dtc_ce_wgrad": ([vp, l, vp, vp, i, i, f, vp, l, vp, l, vp, f, i, i, i, vp], i),
         # exact-fp32 parity path (csrc/gemm_f32.hip, csrc/attention_f32.hip)
         "dtc_gemm_f32": ([ctypes.POINTER(GemmArgs), vp], i),
         "dtc_gemm_f32_workspace_bytes": ([i, i, i, i], l),

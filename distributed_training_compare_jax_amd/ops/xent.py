@@ -149,32 +149,3 @@ def ce_dgrad_fused(logits: torch.Tensor, lse: torch.Tensor, labels: torch.Tensor
     return dx, dl, cp
 
 
-def ce_wgrad_fused(logits: torch.Tensor, lse: torch.Tensor, labels: torch.Tensor, vocab_start: int, n_valid: int,
-                   grad_scale: float, h: torch.Tensor, dw: torch.Tensor, db: torch.Tensor | None, beta: float = 0.0):
-    """The lm_head weight and bias gradients straight from the logits (``csrc/gemm.hip``
-    ce_wgrad256_kernel): ``dw = beta*dw + dlogits^T h`` and ``db = beta*db + sum_rows dlogits`` with
-    ``dlogits = (softmax - onehot) * grad_scale`` recomputed on the fly — never stored (saves a write
-    and a read of tokens x vocab bf16 per step).  db is summed from the fp32 values (before the bf16
-    rounding the MFMA operand gets).  GPU bf16 path; CPU: the reference formula."""
-    M, Vl = logits.shape
-    if N.library_path(logits):
-        p = torch.exp(logits.float() - lse[:, None])
-        if n_valid < Vl:
-            p[:, n_valid:] = 0.0
-        loc = labels.long() - vocab_start
-        inside = (loc >= 0) & (loc < n_valid)
-        rows = torch.arange(M, device=logits.device)
-        p.index_put_((rows, loc.clamp(0, Vl - 1)), -inside.to(p.dtype), accumulate=True)
-        p = p * grad_scale
-        g = p.t() @ h.float()
-        dw.mul_(beta).add_(g) if beta != 0.0 else dw.copy_(g)
-        if db is not None:
-            db.mul_(beta).add_(p.sum(0)) if beta != 0.0 else db.copy_(p.sum(0))
-        return dw
-    D = h.shape[1]
-    assert logits.dtype == torch.bfloat16 and h.dtype == torch.bfloat16 and dw.dtype == torch.float32
-    assert tuple(dw.shape) == (Vl, D) and dw.is_contiguous() and h.shape[0] == M
-    N.check(N.lib().dtc_ce_wgrad(logits.data_ptr(), logits.stride(0), lse.data_ptr(), labels.data_ptr(), vocab_start,
-                                 n_valid, grad_scale, h.data_ptr(), h.stride(0), dw.data_ptr(), dw.stride(0), N.ptr(db),
-                                 beta, Vl, D, M, N.stream_ptr(logits.device)), "dtc_ce_wgrad")
-    return dw

@@ -125,36 +125,3 @@ def test_wgrad_split256(cuda, Nn, K, M):
         outs.append(dw)
     _close(outs[0], outs[1], 1e-4, "split256_vs_default")
 
-
-@pytest.mark.parametrize("M,Nn,K", [(8192, 3072, 768), (8100, 3072, 1024), (8192, 1536, 768)])
-def test_gemm8p_256x192(cuda, M, Nn, K):
-    """256 x 192 tiles on the phase-interleaved kernel (gemm8p_kernel CB = 3, DTC_GEMM8P3): fc1-forward
-    (GELU pair), bf16 / fp32 stores, fp32 residual and the fc2 dgrad (dGELU, NN and NT) against fp32 torch
-    and against the same calls with the plan off.  (8192, 1536): 512 tiles too; ragged M: 8100 rows."""
-    L = N.lib()
-    old8 = L.dtc_gemm_set_n8(3)
-    try:
-        x, w = _r(M, K, seed=21), _r(Nn, K, scale=0.05, seed=22)
-        b = _r(Nn, seed=23, dtype=torch.float32)
-        ref = x.float() @ w.float().t() + b
-        outs = {}
-        for on in (1, 0):
-            L.dtc_gemm_set_p8cb3(on)
-            u, g = G.linear_gelu(x, w, b)
-            _close(u, G.gelu_tanh_grad(ref), 1e-2, f"gelu_grad({on})")
-            _close(g, G.gelu_tanh(ref), 1e-2, f"gelu({on})")
-            _close(G.linear(x, w, b), ref, 1e-2, f"store_bf16({on})")
-            res = _r(M, Nn, seed=24, dtype=torch.float32)
-            yr = G.linear_resid(x, w, b, res)
-            _close(yr, ref + res, 2e-3, f"resid({on})")
-            # dgrad through this Dense's transpose: dX[M, Nn] = dY[M, K] . W^T... as fc2: dY [M, K], W [K, Nn]
-            dy, w2 = _r(M, K, seed=25), _r(K, Nn, scale=0.05, seed=26)
-            uu = _r(M, Nn, seed=27)
-            refd = (dy.float() @ w2.float()) * uu.float()
-            _close(G.matmul_nn_dgelu(dy, w2, uu), refd, 1e-2, f"nn_dgelu({on})")
-            _close(G.matmul_nt_dgelu(dy, w2.t().contiguous(), uu), refd, 1e-2, f"nt_dgelu({on})")
-            outs[on] = yr
-        _close(outs[1], outs[0], 1e-4, "p8cb3_vs_default")
-    finally:
-        L.dtc_gemm_set_p8cb3(0)
-        L.dtc_gemm_set_n8(old8)
