@@ -41,31 +41,34 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--shape", default="gpt2s", choices=["ref", "gpt2s"])
     a = ap.parse_args()
-    B, T, H, hd = 8, 512, 16, 32
+    B, T, H, hd = (8, 512, 16, 32) if a.shape == "ref" else (8, 1024, 12, 64)
     g = torch.Generator().manual_seed(0)
-    qkv = (torch.randn(B, T, 3 * H * hd, generator=g) * 0.5).cuda().bfloat16()
-    do = (torch.randn(B, T, H * hd, generator=g) * 0.5).cuda().bfloat16()
+    qkv = torch.randn(B, T, 3 * H * hd, generator=g).cuda().bfloat16()
+    do = torch.randn(B, T, H * hd, generator=g).cuda().bfloat16()
     o, lse = A.attn_fwd(qkv, H)
-    d_new = A.attn_bwd(qkv, o, lse, do, H)
-    d_old = A.attn_bwd(qkv, o, lse, do, H, flags=1)
-    torch.cuda.synchronize()
-    diff = (d_new.float() - d_old.float()).abs().max().item()
-    ref = d_old.float().abs().max().item()
-    print(f"max |fused - two-round| = {diff:.3e} (max |d| {ref:.3e})", flush=True)
-    o1, l1 = A.attn_fwd(qkv, H, flags=1)
-    torch.cuda.synchronize()
-    print(f"fwd zig vs plain order: max |do| {(o.float() - o1.float()).abs().max().item():.3e}, "
-          f"max |dlse| {(lse - l1).abs().max().item():.3e}", flush=True)
-    res = {"fwd": [], "fwd plain order": [], "bwd fused": [], "bwd two-round": []}
+    fwd_flops = 4.0 * B * H * T * T * hd / 2  # causal: half of QK^T and PV
+    if a.shape == "ref":
+        variants = {"fwd": lambda: A.attn_fwd(qkv, H), "fwd plain order": lambda: A.attn_fwd(qkv, H, flags=1),
+                    "bwd fused": lambda: A.attn_bwd(qkv, o, lse, do, H),
+                    "bwd two-round": lambda: A.attn_bwd(qkv, o, lse, do, H, flags=1)}
+    else:
+        o4, _ = A.attn_fwd(qkv, H, flags=4)
+        torch.cuda.synchronize()
+        print(f"fwd 32-row vs 16-row kernel: max |do| {(o.float() - o4.float()).abs().max().item():.3e}", flush=True)
+        variants = {"fwd (32 q/wave, 32x32x16)": lambda: A.attn_fwd(qkv, H),
+                    "fwd (16 q/wave chunk)": lambda: A.attn_fwd(qkv, H, flags=4),
+                    "bwd": lambda: A.attn_bwd(qkv, o, lse, do, H)}
+    res = {k: [] for k in variants}
     for _ in range(a.rounds):
-        res["fwd"].append(timeit(lambda: A.attn_fwd(qkv, H), a.reps))
-        res["fwd plain order"].append(timeit(lambda: A.attn_fwd(qkv, H, flags=1), a.reps))
-        res["bwd fused"].append(timeit(lambda: A.attn_bwd(qkv, o, lse, do, H), a.reps))
-        res["bwd two-round"].append(timeit(lambda: A.attn_bwd(qkv, o, lse, do, H, flags=1), a.reps))
+        for k, fn in variants.items():
+            res[k].append(timeit(fn, a.reps))
     for k, v in res.items():
         v = sorted(v)
-        print(f"{k:15s} median {v[len(v) // 2]:7.2f} us  min {v[0]:7.2f} us", flush=True)
+        fl = fwd_flops * (2.5 if k.startswith("bwd") else 1.0)
+        print(f"{k:28s} median {v[len(v) // 2]:7.2f} us  min {v[0]:7.2f} us  ({fl / v[len(v) // 2] / 1e6:6.1f} TF/s)",
+              flush=True)
 
 
 if __name__ == "__main__":

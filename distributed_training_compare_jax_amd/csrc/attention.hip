@@ -644,6 +644,154 @@ __global__ void __launch_bounds__(CH_THREADS) attn_fwd_chunk_kernel(const bf16* 
   }
 }
 
+// ============================================================================ forward, 32 queries per wave
+// v_mfma_f32_32x32x16_bf16 with the score tile computed TRANSPOSED (S^T = K Q^T: 32 keys x 32 queries,
+// query on the lane) so softmax is lane-local: lane (r, h) holds 16 keys {(i&3) + 8(i>>2) + 4h} of
+// query r per 32-key block, and its partner lane r + 32 the other 16 (one shfl_xor 32 per max).  The
+// accumulator is directly the B operand of PV (O^T = V^T P^T: registers 8s..8s+7 = the k-step s
+// fragment, keys in the permuted order 16s + 8(j>>2) + 4h + (j&3), cdna_hip_programming.md §3), so P
+// never leaves registers; V^T fragments come from a row-major [key][hd] LDS image by
+// ds_read_b64_tr_b16.  Per 64-key tile a wave does 16 MFMAs of 32 cycles and reads 8 K fragments + 16
+// transposed V halves (2x the queries per K/V byte of the 16-row kernel above, which was LDS-bound at
+// 16 rows per wave); the softmax VALU fills the MFMAs' issue gaps across the 3 waves per SIMD.
+// Max tracking is deferred (T13): the running max m moves only when a tile's max exceeds it by
+// FW_THR (log2 units), so the O / l rescale runs on a few early tiles instead of on every tile; P
+// stays <= 2^FW_THR (exact in bf16 range, fp32 sums).  Block = 4 waves = 128 queries of one (b, h);
+// K/V stream through 2 LDS + 2 register stages (pipelined_tiles), one barrier per 64 keys; heavy
+// (late) query blocks first across the grid.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+constexpr int FW_THREADS = 256, FW_QROWS = 128, FW_KEYS = 64;
+constexpr float FW_THR = 8.f;
+template <int HD>
+struct FwLds {
+  // K image [key][KLD]: ds_read_b128 rows r = lane & 31 at a fixed 16-B chunk; row strides of 36 / 20
+  // dwords put the 16 rows of every 16-lane read group on distinct 4-bank windows.  V image [key][VLD]:
+  // ds_read_b64_tr_b16 reads 4 rows x 32 lanes; a row stride = 16 (mod 64) dwords makes them disjoint.
+  static constexpr int KLD = HD + 8;
+  static constexpr int VLD = HD == 32 ? 32 : 96;
+  static constexpr int STAGE = FW_KEYS * (KLD + VLD);
+};
+template <int HD>
+__host__ __device__ constexpr int fw_lds_bytes() { return 2 * FwLds<HD>::STAGE * 2; }
+
+// A fragment of V^T (32 hd rows x 16 keys, permuted k order) from the [key][VLD] image: keys
+// k0 + 4h + (0..3) and k0 + 8 + 4h + (0..3) of hd column c0 + (lane & 31)
+__device__ __forceinline__ bf16x8 vt_frag32(const bf16* sv, int vld, int k0, int c0, int lane) {
+  const int G = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+  const bf16* p0 = sv + (k0 + 4 * (G >> 1) + qq) * vld + c0 + 16 * (G & 1) + 4 * p;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0 + 8 * vld));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = f2bf(x[8 * s + e]);
+  return r;
+}
+
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS) attn_fwd32_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+                                                              float* __restrict__ lse, int B, int T, int H,
+                                                              float scale) {
+  constexpr int HC = HD / 16, HB = HD / 32;
+  using L = FwLds<HD>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (T + FW_QROWS - 1) / FW_QROWS, nbh = B * H;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);
+  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  DTC_ASSERT(qblk >= 0 && b < B && h < H);
+  const long ts = 3L * H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const int q0 = qblk * FW_QROWS + 32 * w;  // this wave's queries q0 .. q0 + 31
+  const int q = q0 + r;
+  bf16x8 qf[HC];  // B operand of S^T = K Q^T: lane (r, h) holds Q[q][16c + 8h .. +7]
+#pragma unroll
+  for (int c = 0; c < HC; ++c) qf[c] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + 16 * c + 8 * hh) : bf16x8{};
+  const float cs = scale * LOG2E;
+  float m = -1e30f, l = 0.f;  // m: running max of s * cs (finite start: masked scores give exp2(-inf) = 0)
+  f32x16 acc[HB];
+#pragma unroll
+  for (int i = 0; i < HB; ++i) acc[i] = f32x16{};
+
+  auto body = [&](const bf16* sK, const bf16* sV, int it) {
+    const int kb = it * FW_KEYS;
+    if (kb > q0 + 31 || q0 >= T) return;  // wave-uniform: the whole tile lies past this wave's queries
+    const bool diag = kb + FW_KEYS - 1 > q0;
+    f32x16 sc[2];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      sc[k2] = f32x16{};
+#pragma unroll
+      for (int c = 0; c < HC; ++c)
+        sc[k2] = mfma32(*(const bf16x8*)(sK + (k2 * 32 + r) * L::KLD + 16 * c + 8 * hh), qf[c], sc[k2]);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float x = sc[k2][i];
+        if (diag) {
+          const int key = kb + 32 * k2 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          x = (key <= q && key < T) ? x : -INFINITY;
+        }
+        sc[k2][i] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * cs;  // the partner lane holds the query's other keys
+    if (__builtin_amdgcn_ballot_w64(mt > m + FW_THR)) {  // deferred max: rare after the first tiles
+      const float mn = mt > m + FW_THR ? mt : m;
+      const float alpha = fast_exp2(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < HB; ++i) acc[i] *= alpha;
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = fast_exp2(fmaf(sc[k2][i], cs, -m));
+        sc[k2][i] = pv;
+        ls += pv;
+      }
+    l += ls;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = pack8(sc[k2], s2);
+#pragma unroll
+        for (int i = 0; i < HB; ++i) acc[i] = mfma32(vt_frag32(sV, L::VLD, 32 * k2 + 16 * s2, 32 * i, lane), pf, acc[i]);
+      }
+  };
+  const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + FW_KEYS - 1) / FW_KEYS;
+  pipelined_tiles<HD, FW_KEYS, FW_THREADS>(nkt, [](int it) { return it * FW_KEYS; }, Kb, ts, Vb, ts, T, lds, L::KLD,
+                                           L::VLD, tid, body);
+  l += __shfl_xor(l, 32, 64);
+  if (q < T) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long)b * T + q) * H * HD + h * HD;
+#pragma unroll
+    for (int i = 0; i < HB; ++i)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *(bf16x4*)(orow + 32 * i + 8 * g4 + 4 * hh) =
+            bf16x4{f2bf(acc[i][4 * g4] * inv), f2bf(acc[i][4 * g4 + 1] * inv), f2bf(acc[i][4 * g4 + 2] * inv),
+                   f2bf(acc[i][4 * g4 + 3] * inv)};
+    if (hh == 0) lse[((long)b * H + h) * T + q] = (m + __log2f(l)) * LN2;
+  }
+}
+
 // Chunked backward for T > RES_MAXT / head_dim 64 (the tiled kernels above with 16 waves = 256
 // rows per block, 128-row Q/dO or K/V chunks, wave-uniform tile skips, diagonal-only masks and a
 // grid-wide heavy-first block order; see attn_fwd_chunk_kernel).
@@ -1352,6 +1500,14 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
     // flags bit 0: plain wave -> query-group order (A/B of the SIMD-balanced order)
     hipLaunchKernelGGL(attn_fwd_res_kernel<32>, dim3(B * H * 2), dim3(RES_THREADS), res_lds_fwd(T, HD), st, qkv, o,
                        lse, B, T, H, scale, (int)!(flags & 1));
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
+  // flags bit 2: the 16-query-row chunked kernel instead of the 32-row one (A/B)
+  if (HD == 64 && !(flags & 4) && attn_chunk_enabled()) {
+    allow_lds(attn_fwd32_kernel<64>, fw_lds_bytes<64>());
+    hipLaunchKernelGGL(attn_fwd32_kernel<64>, dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
+                       fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale);
     DTC_CHECK_LAUNCH();
     return 0;
   }

@@ -5,10 +5,11 @@ set -u
 mkdir -p gpurun_out
 T="timeout -k 10"
 echo "GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-unset}"
-$T 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_wgrad_group_gpu.py tests/test_gemm_n8_gpu.py > gpurun_out/r4_wg_tests.log 2>&1; rc=$?
+$T 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_wgrad_group_gpu.py tests/test_gemm_n8_gpu.py tests/test_kernels_gpu.py -k "wgrad or n8 or split256 or attention" > gpurun_out/r4_wg_tests.log 2>&1; rc=$?
 tail -n 3 gpurun_out/r4_wg_tests.log; [ $rc -ne 0 ] && exit $rc
 $T 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_engine_gpu.py > gpurun_out/r4_wg_engine.log 2>&1; rc=$?
 tail -n 3 gpurun_out/r4_wg_engine.log; [ $rc -ne 0 ] && exit $rc
+$T 300 python benchmarks/attn_ab.py --rounds 5 > gpurun_out/r4_attn_ab.log 2>&1; tail -n 6 gpurun_out/r4_attn_ab.log
 for arm in 0 -1 0; do
   $T 300 python bench.py --steps 30 --warmup 5 --set wgrad_group=$arm > gpurun_out/r4_wg_bench_$arm.log 2>&1 || exit $?
   echo "wgrad_group=$arm"; tail -n 1 gpurun_out/r4_wg_bench_$arm.log

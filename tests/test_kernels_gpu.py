@@ -225,6 +225,27 @@ def test_attention(cuda, B, T, H, hd):
         _close(d3[:, :, i], r3[:, :, i], 3e-2, f"attn_d{n}")
 
 
+@pytest.mark.parametrize("spike", [False, True])
+@pytest.mark.parametrize("B,T,H", [(2, 1024, 3), (1, 777, 2)])
+def test_attention_fwd32_vs_chunk_and_reference(cuda, B, T, H, spike):
+    """head_dim 64 forward on the 32-query-per-wave 32x32x16 kernel (default) against the 16-row chunked
+    kernel (flags bit 2) and the fp32 reference.  ``spike``: one key scaled up mid-sequence so the
+    running max jumps by far more than the deferred-max threshold (2^8) at a late tile -- the rescale
+    branch runs on most rows (cdna_hip_programming.md §5.4 rule 26)."""
+    hd = 64
+    qkv = _r(B, T, 3 * H * hd, seed=40)
+    if spike:
+        v = qkv.view(B, T, 3, H, hd)
+        v[:, T // 2 + 5, 1] *= 12.0  # key row T/2+5 of every head: its scores dominate later queries
+    o, lse = A.attn_fwd(qkv, H)
+    o4, lse4 = A.attn_fwd(qkv, H, flags=4)
+    oc, lsec = A.attn_fwd(qkv.cpu().float(), H)
+    _close(o.cpu(), oc, 2e-2, "attn32_o")
+    _close(lse.cpu(), lsec, 1e-3, "attn32_lse")
+    _close(o.float(), o4.float(), 2e-2, "attn32_vs_chunk")
+    assert torch.equal(o, A.attn_fwd(qkv, H)[0])  # deterministic
+
+
 @pytest.mark.parametrize("B,T,H", [(2, 512, 4), (1, 200, 3), (2, 64, 2)])
 def test_attention_bwd_fused_matches_two_round(cuda, B, T, H):
     """The fused single-round backward and the two-round resident kernels compute the same
