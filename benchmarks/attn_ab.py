@@ -59,7 +59,8 @@ def main():
         print(f"fwd 32-row vs 16-row kernel: max |do| {(o.float() - o4.float()).abs().max().item():.3e}", flush=True)
         variants = {"fwd (32 q/wave, 32x32x16)": lambda: A.attn_fwd(qkv, H),
                     "fwd (16 q/wave chunk)": lambda: A.attn_fwd(qkv, H, flags=4),
-                    "bwd": lambda: A.attn_bwd(qkv, o, lse, do, H)}
+                    "bwd (32 rows/wave)": lambda: A.attn_bwd(qkv, o, lse, do, H),
+                    "bwd (16-row chunk)": lambda: A.attn_bwd(qkv, o, lse, do, H, flags=4)}
     res = {k: [] for k in variants}
     for _ in range(a.rounds):
         for k, fn in variants.items():

@@ -792,6 +792,275 @@ __global__ void __launch_bounds__(FW_THREADS) attn_fwd32_kernel(const bf16* __re
   }
 }
 
+// ============================================================================ backward, 32 rows per wave
+// The 32x32x16 forms of the two chunked backward kernels (head_dim 64).  Every 64-row tile they read
+// both ways -- row fragments (ds_read_b128) for one product and transposed fragments
+// (ds_read_b64_tr_b16) for another -- sits in ONE swizzled image: 64 rows x 64 bf16 (128-B rows), 16-B
+// chunk c of row r at chunk position c ^ sw8(r), sw8(r) = ((r >> 1) & 1) << 2 | ((r >> 2) & 3).  The row
+// reads (rows lane & 31 of one chunk) then hit 16 distinct 4-bank windows per 16-lane read group, and a
+// transposed read (4 consecutive rows x 4 chunks per 32 lanes) all 64 banks once.
+__device__ __forceinline__ int sw8(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ bf16x8 sw_row(const bf16* t, int row, int ch) {
+  return *(const bf16x8*)(t + row * 64 + ((ch ^ sw8(row)) << 3));
+}
+// A fragment of X^T (32 columns c0.. of the tile as rows, 16 tile rows k0.. as k, permuted order)
+__device__ __forceinline__ bf16x8 sw_tr(const bf16* t, int k0, int c0, int lane) {
+  const int G = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+  const int r0 = k0 + 4 * (G >> 1) + qq, r1 = r0 + 8, col = c0 + 16 * (G & 1) + 4 * p;
+  const bf16* p0 = t + r0 * 64 + (((col >> 3) ^ sw8(r0)) << 3) + (col & 7);
+  const bf16* p1 = t + r1 * 64 + (((col >> 3) ^ sw8(r1)) << 3) + (col & 7);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DTC_LDS s16x4*)(DTC_LDS void*)(p1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// Two [64][64] bf16 tiles (rows t0.., two operands) + optionally two fp32 row vectors [64] (lse, delta),
+// register-staged: load() issues the global loads, store() writes the swizzled images.
+template <int NTH, bool VEC>
+struct SwStage {
+  static constexpr int CPT = 64 * 8 / NTH;
+  u32x4 x[CPT], y[CPT];
+  f32x4 v;
+  __device__ __forceinline__ void load(const bf16* __restrict__ bx, long sx, const bf16* __restrict__ by, long sy,
+                                       const float* __restrict__ va, const float* __restrict__ vb, int t0, int T,
+                                       int tid) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + NTH * i, r = c >> 3, ch = c & 7, t = t0 + r;
+      x[i] = t < T ? *(const u32x4*)(bx + (long)t * sx + ch * 8) : u32x4{0, 0, 0, 0};
+      y[i] = t < T ? *(const u32x4*)(by + (long)t * sy + ch * 8) : u32x4{0, 0, 0, 0};
+    }
+    if (VEC && tid < 32) {
+      const float* src = tid < 16 ? va : vb;
+      const int r = 4 * (tid & 15), t = t0 + r;
+      if (t + 4 <= T) v = *(const f32x4*)(src + t);
+      else for (int e = 0; e < 4; ++e) v[e] = t + e < T ? src[t + e] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(bf16* lx, bf16* ly, float* lv, int tid) const {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + NTH * i, r = c >> 3, ch = c & 7;
+      *(u32x4*)(lx + r * 64 + ((ch ^ sw8(r)) << 3)) = x[i];
+      *(u32x4*)(ly + r * 64 + ((ch ^ sw8(r)) << 3)) = y[i];
+    }
+    if (VEC && tid < 32) *(f32x4*)(lv + (tid < 16 ? 0 : 64) + 4 * (tid & 15)) = v;
+  }
+};
+constexpr int SW_STAGE = 2 * 64 * 64 + 2 * 64 * 2;  // bf16 elements per stage (2 images + 2 fp32 vectors)
+
+// body(sX, sY, sVec, it) over tiles t0_of(it), two LDS + two register stages, one barrier per tile
+template <int NTH, bool VEC, typename T0, typename Body>
+__device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, const bf16* bx, long sx, const bf16* by, long sy,
+                                                   const float* va, const float* vb, int T, bf16* lds, int tid,
+                                                   Body body) {
+  if (n <= 0) return;
+  bf16* X[2] = {lds, lds + SW_STAGE};
+  SwStage<NTH, VEC> p0, p1;
+  auto Y = [&](int k) { return X[k] + 64 * 64; };
+  auto Vv = [&](int k) { return (float*)(X[k] + 2 * 64 * 64); };
+  p0.load(bx, sx, by, sy, va, vb, t0_of(0), T, tid);
+  if (n > 1) p1.load(bx, sx, by, sy, va, vb, t0_of(1), T, tid);
+  p0.store(X[0], Y(0), Vv(0), tid);
+  __syncthreads();
+  for (int it = 0; it < n; it += 2) {
+    if (it + 2 < n) p0.load(bx, sx, by, sy, va, vb, t0_of(it + 2), T, tid);
+    body(X[0], Y(0), Vv(0), it);
+    if (it + 1 < n) p1.store(X[1], Y(1), Vv(1), tid);
+    __syncthreads();
+    if (it + 1 >= n) break;
+    if (it + 3 < n) p1.load(bx, sx, by, sy, va, vb, t0_of(it + 3), T, tid);
+    body(X[1], Y(1), Vv(1), it + 1);
+    if (it + 2 < n) p0.store(X[0], Y(0), Vv(0), tid);
+    __syncthreads();
+  }
+}
+
+// dQ (+ delta = rowsum(dO * O) for the dK/dV kernel): block = 4 waves = 128 queries of one (b, h); wave
+// = 32 queries on the lane.  Per 32-key block: S^T = K Q^T and dP^T = V dO^T (K / V row fragments, Q /
+// dO stationary in registers), dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K transposed
+// fragments, dS^T straight from the accumulators).
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS) attn_bwd_dq32_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
+    float scale) {
+  static_assert(HD == 64, "swizzled 64-wide images");
+  constexpr int HC = HD / 16, HB = HD / 32;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (T + FW_QROWS - 1) / FW_QROWS, nbh = B * H;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);
+  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  DTC_ASSERT(qblk >= 0 && b < B && h < H);
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const int q0 = qblk * FW_QROWS + 32 * w, q = q0 + r;
+  bf16x8 qf[HC], df[HC];
+  float dpart = 0.f;
+#pragma unroll
+  for (int c = 0; c < HC; ++c) {
+    qf[c] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + 16 * c + 8 * hh) : bf16x8{};
+    df[c] = q < T ? *(const bf16x8*)(dOb + (long)q * dts + 16 * c + 8 * hh) : bf16x8{};
+    const bf16x8 of = q < T ? *(const bf16x8*)(o + ((long)b * T + q) * dts + h * HD + 16 * c + 8 * hh) : bf16x8{};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dpart += (float)of[e] * (float)df[c][e];
+  }
+  const float dlt = dpart + __shfl_xor(dpart, 32, 64);
+  if (hh == 0 && q < T) delta[((long)b * H + h) * T + q] = dlt;
+  const float lq = q < T ? lse[((long)b * H + h) * T + q] * LOG2E : 0.f;
+  const float cs = scale * LOG2E;
+  f32x16 acc[HB];
+#pragma unroll
+  for (int i = 0; i < HB; ++i) acc[i] = f32x16{};
+  auto body = [&](const bf16* sK, const bf16* sV, const float*, int it) {
+    const int kb = it * 64;
+    if (kb > q0 + 31 || q0 >= T) return;
+    const bool diag = kb + 63 > q0;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      if (kb + 32 * k2 > q0 + 31) break;  // wave-uniform: the second 32 keys lie past every query
+      f32x16 st = f32x16{}, dp = f32x16{};
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+        st = mfma32(sw_row(sK, 32 * k2 + r, 2 * c + hh), qf[c], st);
+        dp = mfma32(sw_row(sV, 32 * k2 + r, 2 * c + hh), df[c], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pv = fast_exp2(fmaf(st[i], cs, -lq));
+        if (diag) {
+          const int key = kb + 32 * k2 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          pv = (key <= q && key < T && q < T) ? pv : 0.f;
+        }
+        st[i] = pv * (dp[i] - dlt);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 dsb = pack8(st, s2);
+#pragma unroll
+        for (int i = 0; i < HB; ++i) acc[i] = mfma32(sw_tr(sK, 32 * k2 + 16 * s2, 32 * i, lane), dsb, acc[i]);
+      }
+    }
+  };
+  const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + 63) / 64;
+  sw_pipelined_tiles<FW_THREADS, false>(nkt, [](int it) { return it * 64; }, Kb, ts, Vb, ts, nullptr, nullptr, T, lds,
+                                        tid, body);
+  if (q < T) {
+    bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
+#pragma unroll
+    for (int i = 0; i < HB; ++i)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *(bf16x4*)(pq + 32 * i + 8 * g4 + 4 * hh) =
+            bf16x4{f2bf(acc[i][4 * g4] * scale), f2bf(acc[i][4 * g4 + 1] * scale), f2bf(acc[i][4 * g4 + 2] * scale),
+                   f2bf(acc[i][4 * g4 + 3] * scale)};
+  }
+}
+
+// dK, dV: block = 4 waves = 128 keys of one (b, h); wave = 32 keys on the lane.  Per 32-query block:
+// S = Q K^T and dP = dO V^T (Q / dO row fragments, K / V stationary), P and dS = P (dP - delta) with the
+// key on the lane, dV^T += dO^T P and dK^T += Q^T dS (Q / dO transposed fragments of the same images,
+// P / dS straight from the accumulators).  The heaviest key block (0: every query) goes first.
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dkdv32_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  static_assert(HD == 64, "swizzled 64-wide images");
+  constexpr int HC = HD / 16, HB = HD / 32;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbh = B * H;
+  const int kblk = (int)(blockIdx.x / nbh);
+  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  DTC_ASSERT(kblk * FW_QROWS < T && b < B && h < H);
+  const long ts = 3L * H * HD, dts = (long)H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
+  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const bf16* dOb = dout + (long)b * T * dts + h * HD;
+  const float* lseb = lse + ((long)b * H + h) * T;
+  const float* delb = delta + ((long)b * H + h) * T;
+  const int k0w = kblk * FW_QROWS + 32 * w, key = k0w + r;  // this wave's keys k0w .. k0w + 31
+  bf16x8 kf[HC], vf[HC];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) {
+    kf[c] = key < T ? *(const bf16x8*)(Kb + (long)key * ts + 16 * c + 8 * hh) : bf16x8{};
+    vf[c] = key < T ? *(const bf16x8*)(Vb + (long)key * ts + 16 * c + 8 * hh) : bf16x8{};
+  }
+  const float cs = scale * LOG2E;
+  f32x16 dk[HB], dv[HB];
+#pragma unroll
+  for (int i = 0; i < HB; ++i) dk[i] = dv[i] = f32x16{};
+  const int qt0 = kblk * FW_QROWS / 64;  // first 64-query tile (queries >= the block's keys)
+  auto body = [&](const bf16* sQ, const bf16* sD, const float* sv, int it) {
+    const int qb = (qt0 + it) * 64;
+    if (qb + 63 < k0w || k0w >= T) return;  // wave-uniform: every query of the tile before the keys
+    const float* sl = sv;
+    const float* sd = sv + 64;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const int qs = qb + 32 * k2;
+      if (qs + 31 < k0w || qs >= T) continue;  // wave-uniform
+      const bool diag = qs < k0w + 31 || qs + 32 > T;
+      f32x16 sc = f32x16{}, dp = f32x16{};
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+        sc = mfma32(sw_row(sQ, 32 * k2 + r, 2 * c + hh), kf[c], sc);
+        dp = mfma32(sw_row(sD, 32 * k2 + r, 2 * c + hh), vf[c], dp);
+      }
+      f32x16 ds;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int qr = 32 * k2 + 8 * g4 + 4 * hh;  // tile rows of registers 4 g4 .. 4 g4 + 3
+        const f32x4 l4 = *(const f32x4*)(sl + qr), d4 = *(const f32x4*)(sd + qr);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          float pv = fast_exp2(fmaf(sc[i], cs, -l4[e] * LOG2E));
+          if (diag) {
+            const int qq = qb + qr + e;
+            pv = (key <= qq && qq < T && key < T) ? pv : 0.f;
+          }
+          sc[i] = pv;
+          ds[i] = pv * (dp[i] - d4[e]);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pb = pack8(sc, s2), dsb = pack8(ds, s2);
+#pragma unroll
+        for (int i = 0; i < HB; ++i) {
+          dv[i] = mfma32(sw_tr(sD, 32 * k2 + 16 * s2, 32 * i, lane), pb, dv[i]);
+          dk[i] = mfma32(sw_tr(sQ, 32 * k2 + 16 * s2, 32 * i, lane), dsb, dk[i]);
+        }
+      }
+    }
+  };
+  const int nqt = (T - qt0 * 64 + 63) / 64;
+  sw_pipelined_tiles<FW_THREADS, true>(nqt, [qt0](int it) { return (qt0 + it) * 64; }, Qb, ts, dOb, dts, lseb, delb, T,
+                                       lds, tid, body);
+  if (key < T) {
+    bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
+    bf16* pv = dqkv + ((long)b * T + key) * ts + (2 * H + h) * HD;
+#pragma unroll
+    for (int i = 0; i < HB; ++i)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * i + 8 * g4 + 4 * hh;
+        *(bf16x4*)(pk + d0) = bf16x4{f2bf(dk[i][4 * g4] * scale), f2bf(dk[i][4 * g4 + 1] * scale),
+                                     f2bf(dk[i][4 * g4 + 2] * scale), f2bf(dk[i][4 * g4 + 3] * scale)};
+        *(bf16x4*)(pv + d0) = bf16x4{f2bf(dv[i][4 * g4]), f2bf(dv[i][4 * g4 + 1]), f2bf(dv[i][4 * g4 + 2]),
+                                     f2bf(dv[i][4 * g4 + 3])};
+      }
+  }
+}
+
 // Chunked backward for T > RES_MAXT / head_dim 64 (the tiled kernels above with 16 waves = 256
 // rows per block, 128-row Q/dO or K/V chunks, wave-uniform tile skips, diagonal-only masks and a
 // grid-wide heavy-first block order; see attn_fwd_chunk_kernel).
@@ -1562,7 +1831,17 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
                        dqkv, B, T, H, scale);
   } else if (attn_chunk_enabled() && (HD == 32 || HD == 64)) {
     const dim3 g(B * H * ((T + CH_QROWS - 1) / CH_QROWS)), gk(B * H * ((T + CHB_KROWS - 1) / CHB_KROWS));
-    if (HD == 64) {
+    if (HD == 64 && !(flags & 4)) {
+      // 32x32x16 kernels (flags bit 2: the 16-row chunked ones); dQ first: it writes delta
+      constexpr int lb = 2 * SW_STAGE * 2;
+      allow_lds(attn_bwd_dq32_kernel<64>, lb);
+      allow_lds(attn_bwd_dkdv32_kernel<64>, lb);
+      const dim3 g32(B * H * ((T + FW_QROWS - 1) / FW_QROWS));
+      hipLaunchKernelGGL(attn_bwd_dq32_kernel<64>, g32, dim3(FW_THREADS), lb, st, qkv, o, dout, lse, ws, dqkv, B, T, H,
+                         scale);
+      hipLaunchKernelGGL(attn_bwd_dkdv32_kernel<64>, g32, dim3(FW_THREADS), lb, st, qkv, dout, lse, ws, dqkv, B, T, H,
+                         scale);
+    } else if (HD == 64) {
       allow_lds(attn_bwd_dkdv_chunk_kernel<64>, ch_lds_bwd<64>());
       allow_lds(attn_bwd_dq_chunk_kernel<64>, ch_lds_bwd<64>());
       // dQ first: it writes delta (ws) for the dK/dV kernel

@@ -244,6 +244,16 @@ def test_attention_fwd32_vs_chunk_and_reference(cuda, B, T, H, spike):
     _close(lse.cpu(), lsec, 1e-3, "attn32_lse")
     _close(o.float(), o4.float(), 2e-2, "attn32_vs_chunk")
     assert torch.equal(o, A.attn_fwd(qkv, H)[0])  # deterministic
+    # backward: the 32x32x16 dQ and dK/dV kernels (default) vs the 16-row chunked ones vs fp32
+    do = _r(B, T, H * hd, seed=41)
+    d = A.attn_bwd(qkv, o, lse, do, H)
+    d4 = A.attn_bwd(qkv, o, lse, do, H, flags=4)
+    dref = A.attn_bwd(qkv.cpu().float(), o.cpu().float(), lse.cpu(), do.cpu().float(), H)
+    d3, r3, o3 = d.cpu().float().view(B, T, 3, -1), dref.view(B, T, 3, -1), d4.cpu().float().view(B, T, 3, -1)
+    for i, n in enumerate("qkv"):
+        _close(d3[:, :, i], r3[:, :, i], 3e-2, f"attn32_d{n}")
+        _close(d3[:, :, i], o3[:, :, i], 3e-2, f"attn32_vs_chunk_d{n}")
+    assert torch.equal(d, A.attn_bwd(qkv, o, lse, do, H))  # deterministic
 
 
 @pytest.mark.parametrize("B,T,H", [(2, 512, 4), (1, 200, 3), (2, 64, 2)])
