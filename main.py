@@ -39,6 +39,32 @@ def _run(train_config_path: str, model_config_path: str, optim_config_path: str,
         destroy()
 
 
+def _parse_sets(items) -> dict:
+    """KEY=VALUE strings -> TrainConfig overrides, each value parsed as its field's type."""
+    import dataclasses
+
+    from distributed_training_compare_jax_amd.config.schema import TrainConfig
+
+    types = {f.name: str(f.type) for f in dataclasses.fields(TrainConfig)}
+    out = {}
+    for it in items:
+        k, v = it.split("=", 1)
+        if k not in types:
+            raise click.BadParameter(f"unknown TrainConfig field {k!r}", param_hint="--set")
+        t = types[k]
+        if v.lower() in ("none", "null") and "Optional" in t:
+            out[k] = None
+        elif "bool" in t:
+            out[k] = v.lower() in ("1", "true", "yes")
+        elif "int" in t:
+            out[k] = int(v)
+        elif "float" in t:
+            out[k] = float(v)
+        else:
+            out[k] = v
+    return out
+
+
 def _spawn_target(args):
     _run(*args)
 
@@ -57,9 +83,11 @@ def _spawn_target(args):
               help="roctx ranges + device step times + Chrome trace in <output_dir>/trace/")
 @click.option("--dtype", type=click.Choice(["bf16", "fp32"]), default=None,
               help="compute precision (default bf16; fp32 = the reference's precision on the exact-fp32 kernels)")
+@click.option("--set", "sets", multiple=True, metavar="KEY=VALUE",
+              help="any other TrainConfig field, e.g. --set tp_comm=p2p --set pp_schedule=1f1b")
 def main(train_config_path: str, model_config_path: str, optim_config_path: str, nproc, steps, device, log_every,
-         warmup_steps, output_dir, profile, dtype):
-    overrides = {}
+         warmup_steps, output_dir, profile, dtype, sets):
+    overrides = _parse_sets(sets)
     if dtype is not None:
         overrides["dtype"] = dtype
     if output_dir is not None:

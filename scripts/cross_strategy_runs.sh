@@ -1,0 +1,21 @@
+#!/bin/bash
+# Long cross-strategy loss curves on ONE GPU: the reference model, same data and
+# canonical init, STEPS timed steps each:
+#   dp1 (1 process), tp2 (2 processes, P2P all-reduce kernels), pp2 (2 processes, 1F1B, 8 microbatches)
+# The 2-process runs share cuda:0 over gloo (RCCL refuses two ranks on one device).
+#   -> gpurun_out/curves/{dp,tp,pp}/log.csv ; report: python scripts/cross_strategy_report.py gpurun_out/curves
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+STEPS=${STEPS:-2000}
+OUT=gpurun_out/curves
+mkdir -p $OUT
+T="timeout -k 10"
+$T 400 python main.py --train_config_path configs/train_config_dp.yaml --nproc 1 --steps $STEPS --log_every 250 \
+    --output_dir $OUT/dp > $OUT/dp.log 2>&1 || exit $?
+tail -n 2 $OUT/dp.log
+DTC_DIST_BACKEND=gloo $T 600 python main.py --train_config_path configs/train_config_tp.yaml --nproc 2 --steps $STEPS \
+    --log_every 250 --output_dir $OUT/tp --set tp_comm=p2p > $OUT/tp.log 2>&1 || exit $?
+tail -n 2 $OUT/tp.log
+DTC_DIST_BACKEND=gloo $T 900 python main.py --train_config_path configs/train_config_pp_1f1b.yaml --nproc 2 --steps $STEPS \
+    --log_every 250 --output_dir $OUT/pp > $OUT/pp.log 2>&1 || exit $?
+tail -n 2 $OUT/pp.log
