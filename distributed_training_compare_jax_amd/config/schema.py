@@ -34,8 +34,9 @@ are optional and default to the reference behaviour:
   dp = 1, 2 under DP so each group's buckets overlap the rest of the backward), ``pp_split``
   (``cost``: the contiguous layer split minimising the most expensive stage, counting lm_head + CE as
   ``pp_head_cost`` blocks on the last stage -- default from FLOPs, ``parallel/mesh.py``; ``even``: the
-  remainder layers to the earliest stages), ``dp_grad_dtype`` / ``pp_comm_dtype`` (``bf16``: the DP
-  gradient buckets / PP stage messages travel as bf16 and are summed in fp32, ``ops/payload.py``).
+  remainder layers to the earliest stages), ``dp_grad_dtype`` / ``pp_comm_dtype`` / ``tp_comm_dtype`` (``bf16``: the DP
+  gradient buckets / PP stage messages / TP partial sums travel as bf16 and are summed in fp32,
+  ``ops/payload.py``, ``parallel/tp.py reduce_to``; the TP residual is added after the sum, unrounded).
 """
 
 from __future__ import annotations
@@ -134,6 +135,7 @@ class TrainConfig:
     pp_split: str = "cost"  # cost | even: PP layer split (parallel/mesh.py split_layers)
     dp_grad_dtype: str = "fp32"  # fp32 | bf16: DP gradient payload (bf16: all-to-all + fp32 shard sums)
     pp_comm_dtype: str = "fp32"  # fp32 | bf16: PP activation / gradient messages
+    tp_comm_dtype: str = "fp32"  # fp32 | bf16: TP row-parallel / input-gradient partials (fp32 sums)
     pp_head_cost: Optional[float] = None  # lm_head + CE in blocks (None: parallel/mesh.py head_cost_blocks)
     warmup_steps: int = 5
     ckpt_every: int = 0

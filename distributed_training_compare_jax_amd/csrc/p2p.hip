@@ -108,6 +108,82 @@ __global__ void p2p_oneshot_kernel(PeerTable t, int world, long n4, long half_by
   }
 }
 
+// ---------------------------------------------------------------- bf16 payload (tp_comm_dtype: bf16)
+// Row-parallel partials travel as bf16 (half the xGMI bytes of the fp32 residual), are summed in fp32
+// in rank order, and the LAST kernel adds the fp32 residual and the bias:
+//   out[i] = resid[i] + bias[i % ncols] + sum_p partial_p[i]
+// so the residual stream itself is never rounded (only the layer's delta is, once, to bf16).  The
+// two-shot reduce-scatter stores its reduced slice in bf16 (the all-gather reads half the bytes).
+__global__ void p2p_stage_bf16_kernel(const bf16x8* __restrict__ x, PeerTable t, int rank, long n8, long half_bytes,
+                                      const uint32_t* __restrict__ epoch) {
+  const int h = (epoch[0] >> 1) & 1;
+  bf16x8* dst = (bf16x8*)(t.base[rank] + FLAG_BYTES + h * half_bytes);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) dst[i] = x[i];
+}
+
+__device__ __forceinline__ void add8(float (&a)[8], const bf16x8& v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] += (float)v[e];
+}
+
+// out (fp32) = resid + bias + the 8 values a, for elements 8i .. 8i+7
+__device__ __forceinline__ void finish8(float (&a)[8], long i, float* __restrict__ out, const float* __restrict__ resid,
+                                        const float* __restrict__ bias, int ncols) {
+  if (resid) {
+    const f32x4 r0 = ((const f32x4*)resid)[2 * i], r1 = ((const f32x4*)resid)[2 * i + 1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { a[e] += r0[e]; a[e + 4] += r1[e]; }
+  }
+  if (bias) {
+    const int c0 = (int)((8 * i) % ncols);  // ncols % 8 == 0: the 8 columns share a row
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += bias[c0 + e];
+  }
+  ((f32x4*)out)[2 * i] = f32x4{a[0], a[1], a[2], a[3]};
+  ((f32x4*)out)[2 * i + 1] = f32x4{a[4], a[5], a[6], a[7]};
+}
+
+__global__ void p2p_oneshot_bf16_kernel(PeerTable t, int world, long n8, long half_bytes, float* __restrict__ out,
+                                        const float* __restrict__ resid, const float* __restrict__ bias, int ncols,
+                                        const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 2) >> 1) & 1;
+  const long off = FLAG_BYTES + h * half_bytes;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < world; ++p) add8(a, ((const bf16x8*)(t.base[p] + off))[i]);
+    finish8(a, i, out, resid, bias, ncols);
+  }
+}
+
+__global__ void p2p_reduce_scatter_bf16_kernel(PeerTable t, int rank, int world, long n8, long half_bytes,
+                                               const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 1) >> 1) & 1;
+  const long chunk = (n8 + world - 1) / world;
+  const long lo = rank * chunk, hi = min(n8, lo + chunk);
+  const long off = FLAG_BYTES + h * half_bytes;
+  for (long i = lo + (long)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (long)gridDim.x * blockDim.x) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < world; ++p) add8(a, ((const bf16x8*)(t.base[p] + off))[i]);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(a[e]);
+    ((bf16x8*)(t.base[rank] + off))[i] = o;
+  }
+}
+
+__global__ void p2p_all_gather_bf16_kernel(PeerTable t, int world, long n8, long half_bytes, float* __restrict__ out,
+                                           const float* __restrict__ resid, const float* __restrict__ bias, int ncols,
+                                           const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 2) >> 1) & 1;
+  const long chunk = (n8 + world - 1) / world;
+  const long off = FLAG_BYTES + h * half_bytes;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    add8(a, ((const bf16x8*)(t.base[(int)(i / chunk)] + off))[i]);
+    finish8(a, i, out, resid, bias, ncols);
+  }
+}
+
 // ---------------------------------------------------------------- intra-device stream flags
 // Cross-stream dependencies between two separately captured hipGraphs (main / side) on the SAME
 // device: a producer stream bumps flags[k] to its replay epoch (agent-scope release, after all of
@@ -233,6 +309,42 @@ int dtc_p2p_allreduce(const float* x, float* out, long n, void* const* bases, in
   DTC_CHECK_LAUNCH();
   hipLaunchKernelGGL(p2p_all_gather_kernel, dim3(blocks), dim3(256), 0, st, t, world, n4, half_bytes, (f32x4*)out,
                      epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// out (fp32) = resid + bias + sum over ranks of x (bf16, n % 8 == 0, n * 2 <= half_bytes); resid / bias
+// optional (null), bias indexed by column (ncols % 8 == 0).  mode as dtc_p2p_allreduce; x may not alias out.
+int dtc_p2p_allreduce_bf16(const bf16* x, float* out, long n, void* const* bases, int rank, int world, long half_bytes,
+                           uint32_t* epoch, int* err, int mode, const float* resid, const float* bias, int ncols,
+                           hipStream_t st) {
+  if (world < 1 || world > P2P_MAX || n % 8 || n * 2 > half_bytes || (bias && (ncols <= 0 || ncols % 8))) return 4001;
+  PeerTable t;
+  for (int p = 0; p < P2P_MAX; ++p) t.base[p] = (unsigned char*)(p < world ? bases[p] : nullptr);
+  const long n8 = n / 8;
+  const int blocks = (int)std::min(1024L, std::max(1L, (n8 + 255) / 256));
+  const bool one = mode == 2 || (mode == 0 && oneshot_auto(n * 2, world));
+  hipLaunchKernelGGL(p2p_stage_bf16_kernel, dim3(blocks), dim3(256), 0, st, (const bf16x8*)x, t, rank, n8, half_bytes,
+                     epoch);
+  DTC_CHECK_LAUNCH();
+  if (one) {
+    hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 2);
+    DTC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(p2p_oneshot_bf16_kernel, dim3(blocks), dim3(256), 0, st, t, world, n8, half_bytes, out, resid,
+                       bias, ncols, epoch);
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 1);
+  DTC_CHECK_LAUNCH();
+  const int rs_blocks = (int)std::min(1024L, std::max(1L, (n8 / world + 255) / 256));
+  hipLaunchKernelGGL(p2p_reduce_scatter_bf16_kernel, dim3(rs_blocks), dim3(256), 0, st, t, rank, world, n8, half_bytes,
+                     epoch);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 1);
+  DTC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(p2p_all_gather_bf16_kernel, dim3(blocks), dim3(256), 0, st, t, world, n8, half_bytes, out, resid,
+                     bias, ncols, epoch);
   DTC_CHECK_LAUNCH();
   return 0;
 }

@@ -164,6 +164,9 @@ class GPTStage:
         self.seed = int(dropout_seed)
         self.act_dtype = act_dtype
         D, H = cfg.d_model, cfg.n_heads
+        # tp_comm_dtype: bf16 -> row-parallel partials and input-gradient partials travel as bf16
+        # (TPComm.reduce_to; residual + bias added after the fp32 sum), set by the engine
+        self.tp_bf16 = False
         assert D % H == 0
         # whole heads per TP rank, uneven when tp does not divide H (models/params.py head_split)
         self.heads_local = head_split(H, self.tp.size)[self.tp.rank][1]
@@ -289,6 +292,9 @@ class GPTStage:
         if self._fuse_fwd:
             x2, (y2, mu2, rs2) = LF.linear_resid_ln(o, f.w(p + "out.w"), f.p(p + "out.b"), x, f.p(p + "ln2.g"),
                                                     f.p(p + "ln2.b"), self.eps, self.ln_sync, self._ln_site(l, 0, False))
+        elif self.tp_bf16:
+            x2 = tp.reduce_to(G.linear(o, f.w(p + "out.w"), None, out_dtype=torch.bfloat16), resid=x, bias=f.p(p + "out.b"))
+            y2, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
         else:
             x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
             tp.all_reduce_(x2)
@@ -300,6 +306,9 @@ class GPTStage:
             x3, pre_next = LF.linear_resid_ln(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b"), x2, f.p(nxt + ".g"),
                                               f.p(nxt + ".b"), self.eps, self.ln_sync, self._ln_site(l, 1, False))
             ctx[("ln1", l + 1) if nxt != "lnf" else "lnf_pre"] = pre_next
+        elif self.tp_bf16:
+            x3 = tp.reduce_to(G.linear(gact, f.w(p + "fc2.w"), None, out_dtype=torch.bfloat16), resid=x2,
+                              bias=f.p(p + "fc2.b"))
         else:
             x3 = G.linear_resid(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b") if lead else None, x2 if lead else None)
             tp.all_reduce_(x3)
@@ -348,8 +357,7 @@ class GPTStage:
                                              sync=self.ln_sync, site=self._ln_site(l, 0, True))
                 self._wg(du, y2, p + "fc1", bias=True)
             else:
-                dy2 = self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False)
-                tp.all_reduce_(dy2)
+                dy2 = self._tp_reduce(self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False))
                 dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
             wto = f.wt(p + "out.w")
             if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
@@ -373,8 +381,7 @@ class GPTStage:
                     dx_hook(out[0])
                 self._wg(dqkv, y1, p + "qkv", bias=True)
                 return out
-            dy1 = self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True)
-            tp.all_reduce_(dy1)
+            dy1 = self._tp_reduce(self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True))
             out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
             if dx_hook is not None:
                 dx_hook(out[0])
@@ -409,6 +416,15 @@ class GPTStage:
             dx_hook(out[0])
         return out
 
+    def _tp_reduce(self, d):
+        """All-reduce an input-gradient partial over the TP group (in place for fp32 payloads; with
+        ``tp_bf16`` ``d`` is the bf16 partial and a new fp32 sum comes back)."""
+        if self.tp.size == 1:
+            return d
+        if d.dtype == torch.bfloat16 and self.tp_bf16:
+            return self.tp.reduce_to(d)
+        return self.tp.all_reduce_(d)
+
     def _dgrad_wgrad(self, dy, dense: str, x, beta, red, pair: bool):
         """dX = dY·W (fp32) and dW/db of a Dense with a bias.  With the transposed weight mirror
         (``flat.wt``) the dgrad is an NT GEMM on W^T followed by the weight gradient; otherwise the
@@ -416,7 +432,11 @@ class GPTStage:
         f = self.flat
         wt = f.wt(dense + ".w")
         if self._defer_wg:
-            dx = G.linear_resid(dy, wt, None, None) if wt is not None else G.matmul_nn(dy, f.w(dense + ".w"))
+            if self.tp_bf16 and self.tp.size > 1:  # bf16 partial for the bf16-payload all-reduce
+                dx = (G.linear(dy, wt, out_dtype=torch.bfloat16) if wt is not None
+                      else G.matmul_nn(dy, f.w(dense + ".w"), out_dtype=torch.bfloat16))
+            else:
+                dx = G.linear_resid(dy, wt, None, None) if wt is not None else G.matmul_nn(dy, f.w(dense + ".w"))
             self._wg(dy, x, dense, bias=True)
             return dx
         if wt is None:

@@ -119,6 +119,20 @@ class P2PAllReduce:
                                           N.stream_ptr(t.device)), "dtc_p2p_allreduce")
         return t
 
+    def supports_bf16(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
+                and x.numel() * 2 <= self.half)
+
+    def all_reduce_bf16(self, x: torch.Tensor, out: torch.Tensor, resid=None, bias=None, mode: int = 0) -> torch.Tensor:
+        """out (fp32) = resid + bias + Σ_ranks x, x bf16 (the payload), fp32 sums in rank order; ``bias``
+        indexed by the last dimension of ``out``.  Same barrier / buffer-half protocol as all_reduce_."""
+        ncols = out.shape[-1] if bias is not None else 0
+        N.check(N.lib().dtc_p2p_allreduce_bf16(x.data_ptr(), out.data_ptr(), x.numel(), self._bases_ptr, self.rank,
+                                               self.world, self.half, self.epoch.data_ptr(), self.err.data_ptr(),
+                                               int(mode), N.ptr(resid), N.ptr(bias), ncols, N.stream_ptr(x.device)),
+                "dtc_p2p_allreduce_bf16")
+        return out
+
     def check(self):
         """Raise if a barrier timed out (a peer never arrived); call at a host sync point."""
         e = int(self.err.item())

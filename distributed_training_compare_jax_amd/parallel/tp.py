@@ -50,6 +50,23 @@ class TPComm:
         self.program.comm(lambda: dist.all_reduce(t, group=g), sig=csig("all_reduce", g, t))
         return t
 
+    def reduce_to(self, part: torch.Tensor, resid=None, bias=None) -> torch.Tensor:
+        """fp32 ``resid + bias + Σ_ranks part`` for a bf16 partial (``tp_comm_dtype: bf16``): the partial
+        travels as bf16 and is summed in fp32; the residual and the bias are added once, after the sum, on
+        every rank (the residual stream is never rounded).  P2P kernels on GPU; otherwise an fp32
+        all-reduce of the bf16-rounded partial (same arithmetic up to summation order)."""
+        out = torch.empty(part.shape, dtype=torch.float32, device=part.device)
+        if self.size > 1 and self.p2p is not None and self.p2p.supports_bf16(part) and \
+                (bias is None or part.shape[-1] % 8 == 0):
+            return self.p2p.all_reduce_bf16(part, out, resid, bias)
+        out.copy_(part)
+        self.all_reduce_(out)
+        if resid is not None:
+            out.add_(resid)
+        if bias is not None:
+            out.add_(bias)
+        return out
+
     def all_gather_stack(self, t: torch.Tensor) -> torch.Tensor:
         """[...] → [size, ...] (shard-major).  With the P2P path: every rank writes its slot of a
         zeroed [size, ...] buffer and the buffer is summed (x + 0 = x exactly, so it IS the gather),

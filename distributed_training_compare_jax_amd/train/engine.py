@@ -92,6 +92,9 @@ class Engine:
         self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
                               act_dtype=self.act_dtype,
                               side_stream=on_gpu and os.environ.get("DTC_SIDE_STREAM", "0") == "1")
+        if train_cfg.tp_comm_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"tp_comm_dtype={train_cfg.tp_comm_dtype!r}: expected 'fp32' or 'bf16'")
+        self.stage.tp_bf16 = bool(tp > 1 and train_cfg.tp_comm_dtype == "bf16")
         self.program.before_comm.append(self.stage.side.join)
         # deferred grouped weight gradients (models/gpt.py set_wgrad_group): all layers + the lm_head in
         # one launch when no collective waits on per-layer grads (dp == 1), else groups of wgrad_group

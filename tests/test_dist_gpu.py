@@ -133,6 +133,8 @@ HEADS12 = {"d_model": 384, "n_heads": 12, "d_ff": 512, "n_layers": 2}
 @pytest.mark.parametrize("world,kw", [
     (8, {"parallel": "tp", "tp_comm": "p2p"}),
     (4, {"parallel": "dp", "tp": 2, "tp_comm": "p2p"}),  # dp2 x tp2 at the box's default HW queue count
+    (2, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16"}),  # bf16 payload P2P kernels
+    (4, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16"}),  # ... two-shot at W = 4 (12 heads: 3 each)
 ])
 def test_uneven_heads_and_hybrid_one_gpu(world, kw):
     """TP=8 with 12 heads and dp2 x tp2, 8 / 4 processes on one GPU through the P2P all-reduce kernels,
@@ -189,6 +191,13 @@ def _p2p_worker(out_dir):
         torch.cuda.synchronize()
         outs.append(t.cpu().clone())
     res["graph"] = outs
+    # bf16 payload with the fused residual + bias: forced two-shot (1) and one-shot (2), 3 x 256 rows x 64
+    xb = torch.randn(d.world, 3 * 256, 64, generator=g).to(torch.bfloat16)
+    rs, bs = torch.randn(3 * 256, 64, generator=g), torch.randn(64, generator=g)
+    for mode in (1, 2):
+        out = torch.empty(3 * 256, 64, device=d.device)
+        ar.all_reduce_bf16(xb[d.rank].to(d.device).contiguous(), out, rs.to(d.device), bs.to(d.device), mode=mode)
+        res[f"bf16_{mode}"] = out.cpu()
     ar.check()
     torch.save(res, os.path.join(out_dir, f"p2p{d.rank}.pt"))
     ar.close()
@@ -212,3 +221,11 @@ def test_p2p_allreduce_two_ranks_one_gpu():
         exp = float(1 + it) + float(2 + it)
         for i in range(world):
             assert torch.all(r[i]["graph"][it] == exp), (i, it)
+    xb = torch.randn(world, 3 * 256, 64, generator=g).to(torch.bfloat16)
+    rs, bs = torch.randn(3 * 256, 64, generator=g), torch.randn(64, generator=g)
+    exp = rs + bs + xb.float().sum(0)
+    for mode in (1, 2):  # fp32 sum of the bf16 payload (two-shot rounds the reduced slice to bf16 once)
+        for i in range(world):
+            tol = 2e-2 if mode == 1 else 1e-5
+            assert torch.allclose(r[i][f"bf16_{mode}"], exp, atol=tol, rtol=tol), (mode, i)
+        assert torch.equal(r[0][f"bf16_{mode}"], r[1][f"bf16_{mode}"])

@@ -149,6 +149,8 @@ def test_uneven_heads_match_single_process(parallel, world, kw):
     ("dp", 2, {"dp_grad_dtype": "bf16"}),
     ("dp", 4, {"dp_grad_dtype": "bf16"}),
     ("dp", 4, {"dp_grad_dtype": "bf16", "tp": 2}),
+    ("tp", 2, {"tp_comm_dtype": "bf16"}),
+    ("dp", 4, {"tp": 2, "tp_comm_dtype": "bf16", "dp_grad_dtype": "bf16"}),
     ("pp", 2, {"pp_comm_dtype": "bf16", "pp_microbatches": 2, "pp_clip": "global"}),
     ("pp", 4, {"pp_comm_dtype": "bf16", "pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
 ])
