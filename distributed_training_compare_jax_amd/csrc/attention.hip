@@ -567,6 +567,7 @@ __global__ void __launch_bounds__(CH_THREADS) attn_fwd_chunk_kernel(const bf16* 
   const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
   const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
   const int qbase = qblk * CH_QROWS + 16 * w;  // this wave's rows qbase .. qbase + 15
+  DTC_ASSERT(qblk >= 0 && b < B && qbase < T + CH_QROWS);
   const int q = qbase + j;
   bf16x8 qf[KC];
 #pragma unroll
@@ -1090,6 +1091,7 @@ __global__ void __launch_bounds__(CHB_THREADS) attn_bwd_dkdv_chunk_kernel(
   const float* lseb = lse + ((long)b * H + h) * T;
   const float* delb = delta + ((long)b * H + h) * T;
   const int kb0 = kblk * CHB_KROWS, kmin = kb0 + 16 * w;  // this wave's keys kmin .. kmin + 15
+  DTC_ASSERT(b < B && h < H && kb0 < T);
   const int key = kmin + j;
   bf16x8 kf[KC], vf[KC];
 #pragma unroll
@@ -1182,6 +1184,7 @@ __global__ void __launch_bounds__(CH_THREADS) attn_bwd_dq_chunk_kernel(
   const bf16* dOb = dout + (long)b * T * dts + h * HD;
   const int qbase = qblk * CH_QROWS + 16 * w;
   const int q = qbase + j;
+  DTC_ASSERT(qblk >= 0 && b < B && h < H);
   bf16x8 qf[KC], df[KC];
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc) {

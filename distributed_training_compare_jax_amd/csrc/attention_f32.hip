@@ -126,6 +126,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_fwd_kernel(AttnFArgs a) {
   const int nqb = (a.T + QB - 1) / QB;
   const int bh = blockIdx.x / nqb, qb = nqb - 1 - blockIdx.x % nqb;  // longest (last) query blocks first
   const int b = bh / a.H, h = bh % a.H;
+  DTC_ASSERT(b < a.B && h < a.H);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
   const long rs = 3L * a.H * HD;  // qkv row stride
   const float* qg = a.qkv + (long)b * a.T * rs + (long)h * HD;
@@ -236,6 +237,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_dkdv_kernel(AttnFArgs a) {
   const int nkb = (a.T + QB - 1) / QB;
   const int bh = blockIdx.x / nkb, kbk = blockIdx.x % nkb;  // first key blocks have the most queries
   const int b = bh / a.H, h = bh % a.H;
+  DTC_ASSERT(b < a.B && h < a.H);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
   const long rs = 3L * a.H * HD, ors = (long)a.H * HD;
   const float* qg = a.qkv + (long)b * a.T * rs + (long)h * HD;
@@ -331,6 +333,7 @@ __global__ void __launch_bounds__(AT, 2) attn_f32_dq_kernel(AttnFArgs a) {
   const int nqb = (a.T + QB - 1) / QB;
   const int bh = blockIdx.x / nqb, qb = nqb - 1 - blockIdx.x % nqb;
   const int b = bh / a.H, h = bh % a.H;
+  DTC_ASSERT(b < a.B && h < a.H);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
   const long rs = 3L * a.H * HD, ors = (long)a.H * HD;
   const float* qg = a.qkv + (long)b * a.T * rs + (long)h * HD;

@@ -37,6 +37,7 @@ __global__ void embed_fwd_kernel(const int* __restrict__ ids, const float* __res
   int d = (int)(i % D4) * 4;
   int t = (int)(tok % T);
   int id = ids[tok];
+  DTC_ASSERT(id >= 0 && t < T && d + 4 <= D);
   f32x4 v = *(const f32x4*)(wte + (long)id * D + d) + *(const f32x4*)(wpe + (long)t * D + d);
   if (p > 0.f) {
     long gtok = (row0 + tok / T) * T + t;
@@ -101,6 +102,7 @@ __global__ void __launch_bounds__(64) embed_piece_sums(const uint32_t* __restric
   const int d = (blockIdx.y * 64 + threadIdx.x) * 4;
   if (d >= D) return;
   const int q_beg = blockIdx.x * piece, q_end = min(n, q_beg + piece);
+  DTC_ASSERT(q_beg < n && nb >= 1 && nb < 32 && d + 4 <= D);
   const uint32_t tmask = (1u << nb) - 1;
   const uint32_t thr = drop_threshold(p), stp = (uint32_t)step[0];
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -140,6 +142,7 @@ __global__ void __launch_bounds__(64) embed_segment_sum(const uint32_t* __restri
                                                         int accumulate) {
   const int s = blockIdx.x;
   const uint32_t id = keys[s] >> nb;
+  DTC_ASSERT(s < n && piece >= 1);
   if (s > 0 && (keys[s - 1] >> nb) == id) return;  // not the first occurrence of this id
   const int d = (blockIdx.y * 64 + threadIdx.x) * 4;
   if (d >= D) return;
@@ -257,6 +260,7 @@ __global__ void ce_bwd_kernel(bf16* __restrict__ logits, long ld, const float* _
   if (i >= (long)M * V8) return;
   int m = (int)(i / V8);
   int n = (int)(i % V8) * 8;
+  DTC_ASSERT(m < M && n + 8 <= V && labels[m] >= 0);
   bf16x8* p = (bf16x8*)(logits + (long)m * ld + n);
   const bf16x8 v = *p;
   float g[8];
@@ -281,6 +285,7 @@ __global__ void __launch_bounds__(256) ce_bwd_colsum_kernel(bf16* __restrict__ l
   const int m0 = blockIdx.y * CE_ROWS, m1 = min(M, m0 + CE_ROWS);
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
+  DTC_ASSERT(m0 < M && n + 8 <= V);
   for (int m = m0; m < m1; ++m) {
     bf16x8* p = (bf16x8*)(logits + (long)m * ld + n);
     const bf16x8 v = *p;
@@ -477,6 +482,7 @@ __global__ void __launch_bounds__(256) transpose_batch_kernel(TrBatch batch) {
   const TrTask& T = batch.t[t];
   const int b = blockIdx.x - T.blk0;
   const int tcols = (T.cols + 63) / 64;
+  DTC_ASSERT(b >= 0 && b < ((T.rows + 63) / 64) * tcols && (int)blockIdx.x < batch.nblocks);
   const int r0 = (b / tcols) * 64, c0 = (b % tcols) * 64;
   // row length 65: a column read (8 lanes per row group, rows 8 apart) lands rows 4 banks apart -> the 64
   // lanes cover 32 distinct banks (+8 padding: ~6 bank conflicts per LDS instruction under PMC).  Time-neutral

@@ -715,6 +715,7 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
   const int gm_eff = min(gm, tiles_m - grp * gm);
   const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
   const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  DTC_ASSERT(tm_idx >= 0 && tn_idx >= 0 && z >= 0 && m0 < M && n0 < N);
   const int kbeg = z * k_per_split;
   const int nk = min(k_per_split, K - kbeg) / BK;
 
@@ -1222,6 +1223,7 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;  // M half (= wave group), 64-column slice
   const int m0 = tm_idx * BIG, n0 = tn_idx * (64 * CB);
+  DTC_ASSERT(tm_idx >= 0 && tn_idx >= 0 && z >= 0 && z < split && m0 < M && n0 < N);
   const int kbeg = z * k_per_split;
   const int nk = min(k_per_split, K - kbeg) / 64;
   DTC_ASSERT(nk >= 1);
@@ -1771,6 +1773,7 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
   const int gm_eff = min(a.gm, a.tiles_m - grp * a.gm);
   const int tm_idx = grp * a.gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
   const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
+  DTC_ASSERT(tm_idx >= 0 && tn_idx >= 0 && z >= 0 && m0 < a.M && n0 < a.N);
   const int kbeg = z * a.kps;
   const int nk = min(a.kps, a.K - kbeg) / 64;
   // the dlogits stores + column sums of k-step kt go to n-tile kt % 2 (the two n-tiles share them)
@@ -2017,6 +2020,7 @@ gemm_dma_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B
   const int gm_eff = min(gm, tiles_m - grp * gm);
   const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
   const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  DTC_ASSERT(tm_idx >= 0 && tn_idx >= 0 && z >= 0 && m0 < M && n0 < N);
   const int kbeg = z * k_per_split;
   const int nk = min(k_per_split, K - kbeg) / 64;
 

@@ -294,6 +294,7 @@ __global__ void splitk_reduce_f32(const float* __restrict__ slab, int split, int
   const long MN = (long)M * N;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= MN) return;
+  DTC_ASSERT(split >= 1 && ldc >= N);
   float s = slab[i];
   for (int z = 1; z < split; ++z) s += slab[z * MN + i];
   const long m = i / N, n = i % N;

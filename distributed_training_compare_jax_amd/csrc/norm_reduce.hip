@@ -20,6 +20,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   if (row0 >= M) return;
+  DTC_ASSERT(D % 4 == 0 && D / 4 <= NV * 64);
   const int D4 = D / 4;
   f32x4 v[RPW][NV], gv[NV], bv[NV];
   // gamma/beta are issued with the row loads so their latency hides under the row reductions
@@ -92,6 +93,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
 #pragma unroll
   for (int i = 0; i < NV; ++i) { ag[i] = f32x4{0.f, 0.f, 0.f, 0.f}; ab[i] = ag[i]; ao[i] = ag[i]; }
   const int r0 = blockIdx.x * LN_BWD_ROWS + wave * LN_RPW;
+  DTC_ASSERT(D % 4 == 0 && D / 4 <= NV * 64 && (long)blockIdx.x * LN_BWD_ROWS < M + LN_BWD_ROWS);
   f32x4 xh[LN_RPW][NV], d[LN_RPW][NV], rv[LN_RPW][NV], gv[NV];
   float s1[LN_RPW] = {}, s2[LN_RPW] = {}, rsv[LN_RPW] = {};
   // every global load of the block (x, dy, the residual gradient, gamma) is issued before the first
@@ -254,6 +256,8 @@ __global__ void __launch_bounds__(256) reduce_tasks_kernel(RedBatch batch) {
   while (t + 1 < batch.ntasks && (int)blockIdx.x >= batch.t[t + 1].blk0) ++t;
   const RedTask& T = batch.t[t];
   const int b = blockIdx.x - T.blk0;
+  DTC_ASSERT(t < batch.ntasks && b >= 0 && b < T.nblk && (int)blockIdx.x < batch.nblocks);
+  DTC_ASSERT(T.mode == RED_SUMSQ ? (T.part != nullptr) : (T.dst != nullptr && T.P >= 1));
   const int tid = threadIdx.x;
   if (T.mode == RED_WIDE) {
     const long c = ((long)b * 256 + tid) * 4;

@@ -42,6 +42,7 @@ __device__ __forceinline__ uint64_t wall_clock() { return __builtin_amdgcn_s_mem
 __global__ void p2p_barrier_kernel(PeerTable t, int rank, int world, uint32_t* __restrict__ epoch,
                                    int* __restrict__ err, int inc) {
   const int p = threadIdx.x;
+  DTC_ASSERT(world >= 1 && world <= P2P_MAX && rank >= 0 && rank < world && (inc == 1 || inc == 2));
   const uint32_t e = epoch[0] + inc;
   __threadfence_system();  // this rank's prior writes (its buffer half) before the signal
   if (p < world && p != rank) {
@@ -75,6 +76,7 @@ __global__ void p2p_reduce_scatter_kernel(PeerTable t, int rank, int world, long
   const long chunk = (n4 + world - 1) / world;
   const long lo = rank * chunk, hi = min(n4, lo + chunk);
   const long off = FLAG_BYTES + h * half_bytes;
+  DTC_ASSERT(16 * n4 <= half_bytes && rank < world);
   for (long i = lo + (long)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (long)gridDim.x * blockDim.x) {
     f32x4 s = ((const f32x4*)(t.base[0] + off))[i];
     for (int p = 1; p < world; ++p) s += ((const f32x4*)(t.base[p] + off))[i];
@@ -89,6 +91,7 @@ __global__ void p2p_all_gather_kernel(PeerTable t, int world, long n4, long half
   const long off = FLAG_BYTES + h * half_bytes;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const int q = (int)(i / chunk);
+    DTC_ASSERT(q < world);
     out[i] = ((const f32x4*)(t.base[q] + off))[i];
   }
 }

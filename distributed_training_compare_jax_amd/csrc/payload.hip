@@ -15,6 +15,7 @@ __global__ void __launch_bounds__(256) shard_sum_bf16_kernel(const bf16* __restr
                                                              bf16* __restrict__ out) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < s8; i += (long)gridDim.x * blockDim.x) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    DTC_ASSERT(nshards >= 1);
     for (int j = 0; j < nshards; ++j) {
       const bf16x8 v = ((const bf16x8*)in)[(long)j * s8 + i];
 #pragma unroll

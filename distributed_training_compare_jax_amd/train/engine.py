@@ -10,8 +10,10 @@ segments after the first eager warmup step.
 
 from __future__ import annotations
 
+import math
 import os
 import warnings
+from dataclasses import replace
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -38,6 +40,15 @@ class Engine:
         self.dinfo = dinfo
         self.device = dinfo.device
         dp, tp, pp = resolve_degrees(train_cfg.parallel, dinfo.world, train_cfg.dp, train_cfg.tp, train_cfg.pp)
+        if tp > 1:
+            # every TP rank's vocab shard a multiple of 64 columns (the GEMM K-steps of the lm_head dgrad and
+            # the 64-wide CE tiles): pad the vocab to a multiple of 64 * tp (GPT-2 at tp = 8: 50688 instead
+            # of 50304 = 8 x 6288).  Pad rows are zero and masked, and the valid rows' canonical init does not
+            # depend on the padded length, so every layout still trains the same model.
+            mult = math.lcm(max(1, int(model_cfg.vocab_pad_multiple)), 64 * tp)
+            if mult != model_cfg.vocab_pad_multiple:
+                model_cfg = replace(model_cfg, vocab_pad_multiple=mult)
+                self.mcfg = model_cfg
         self.mesh: Mesh = build_mesh(dinfo.rank, dinfo.world, dp, tp, pp)
         m = self.mesh
         on_gpu = self.device.type == "cuda"
