@@ -284,8 +284,8 @@ __global__ void __launch_bounds__(256) ce_bwd_colsum_kernel(bf16* __restrict__ l
   if (n >= V) return;
   const int m0 = blockIdx.y * CE_ROWS, m1 = min(M, m0 + CE_ROWS);
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
   DTC_ASSERT(m0 < M && n + 8 <= V);
+#pragma unroll 4
   for (int m = m0; m < m1; ++m) {
     bf16x8* p = (bf16x8*)(logits + (long)m * ld + n);
     const bf16x8 v = *p;
