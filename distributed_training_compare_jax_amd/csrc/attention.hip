@@ -17,6 +17,7 @@
 #include "common.h"
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -694,8 +695,30 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
   return r;
 }
 
+// One register stage of a [64 rows][HD] tile pair (K & V, Q & dO, ...) read through buffer resources
+// (32-bit offsets from a per-(b, h) base: no 64-bit address registers per load), rows >= T read as 0 by
+// the hardware range check.  The pipelines below keep ONE register set: tile t+1 is loaded before tile
+// t's compute and written to the other LDS buffer after it (T14), one barrier per tile.
+template <int HD, int NTH>
+struct RegStage {
+  static constexpr int CPT = 64 * HD / 8 / NTH;  // 16-B chunks per thread per operand
+  u32x4 x[CPT], y[CPT];
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rx, long sx, __amdgpu_buffer_rsrc_t ry, long sy, int t0,
+                                       int tid) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + NTH * i, r = c / (HD / 8), col = (c % (HD / 8)) * 8;
+      x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((long)(t0 + r) * sx + col) * 2), 0, 0));
+      y[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, (int)(((long)(t0 + r) * sy + col) * 2), 0, 0));
+    }
+  }
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const bf16* base, long stride, int T, int width) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(((long)(T - 1) * stride + width) * 2), 0x00020000);
+}
+
 template <int HD>
-__global__ void __launch_bounds__(FW_THREADS) attn_fwd32_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd32_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
                                                               float* __restrict__ lse, int B, int T, int H,
                                                               float scale) {
   constexpr int HC = HD / 16, HB = HD / 32;
@@ -709,8 +732,8 @@ __global__ void __launch_bounds__(FW_THREADS) attn_fwd32_kernel(const bf16* __re
   DTC_ASSERT(qblk >= 0 && b < B && h < H);
   const long ts = 3L * H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
-  const bf16* Kb = qkv + (long)b * T * ts + (1 * H + h) * HD;
-  const bf16* Vb = qkv + (long)b * T * ts + (2 * H + h) * HD;
+  const __amdgpu_buffer_rsrc_t rK = rows_rsrc(qkv + (long)b * T * ts + (1 * H + h) * HD, ts, T, HD);
+  const __amdgpu_buffer_rsrc_t rV = rows_rsrc(qkv + (long)b * T * ts + (2 * H + h) * HD, ts, T, HD);
   const int q0 = qblk * FW_QROWS + 32 * w;  // this wave's queries q0 .. q0 + 31
   const int q = q0 + r;
   bf16x8 qf[HC];  // B operand of S^T = K Q^T: lane (r, h) holds Q[q][16c + 8h .. +7]
@@ -721,11 +744,10 @@ __global__ void __launch_bounds__(FW_THREADS) attn_fwd32_kernel(const bf16* __re
   f32x16 acc[HB];
 #pragma unroll
   for (int i = 0; i < HB; ++i) acc[i] = f32x16{};
+  const int qlim = min(q, T - 1);  // last key this lane's query may see
 
-  auto body = [&](const bf16* sK, const bf16* sV, int it) {
-    const int kb = it * FW_KEYS;
-    if (kb > q0 + 31 || q0 >= T) return;  // wave-uniform: the whole tile lies past this wave's queries
-    const bool diag = kb + FW_KEYS - 1 > q0;
+  // one 64-key tile; MASK: the tile crosses this wave's diagonal (or the sequence end)
+  auto tile = [&](const bf16* sK, const bf16* sV, int kb, auto MASK) {
     f32x16 sc[2];
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
@@ -734,38 +756,38 @@ __global__ void __launch_bounds__(FW_THREADS) attn_fwd32_kernel(const bf16* __re
       for (int c = 0; c < HC; ++c)
         sc[k2] = mfma32(*(const bf16x8*)(sK + (k2 * 32 + r) * L::KLD + 16 * c + 8 * hh), qf[c], sc[k2]);
     }
-    float mt = -INFINITY;
+    if constexpr (decltype(MASK)::value) {
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int lim = qlim - (kb + 32 * k2 + 4 * hh);  // keep key offset (i&3) + 8(i>>2) <= lim
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[k2][i] = ((i & 3) + 8 * (i >> 2) <= lim) ? sc[k2][i] : -INFINITY;
+      }
+    }
+    float mt = sc[0][0];
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = sc[k2][i];
-        if (diag) {
-          const int key = kb + 32 * k2 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          x = (key <= q && key < T) ? x : -INFINITY;
-        }
-        sc[k2][i] = x;
-        mt = fmaxf(mt, x);
-      }
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sc[k2][i]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * cs;  // the partner lane holds the query's other keys
-    if (__builtin_amdgcn_ballot_w64(mt > m + FW_THR)) {  // deferred max: rare after the first tiles
+    if (__builtin_amdgcn_ballot_w64(mt > m + FW_THR) != 0) {  // deferred max: rare after the first tiles
       const float mn = mt > m + FW_THR ? mt : m;
       const float alpha = fast_exp2(m - mn);
       m = mn;
       l *= alpha;
 #pragma unroll
-      for (int i = 0; i < HB; ++i) acc[i] *= alpha;
+      for (int i = 0; i < HB; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] *= alpha;
     }
-    float ls = 0.f;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float pv = fast_exp2(fmaf(sc[k2][i], cs, -m));
         sc[k2][i] = pv;
-        ls += pv;
+        l += pv;
       }
-    l += ls;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
@@ -776,8 +798,31 @@ __global__ void __launch_bounds__(FW_THREADS) attn_fwd32_kernel(const bf16* __re
       }
   };
   const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + FW_KEYS - 1) / FW_KEYS;
-  pipelined_tiles<HD, FW_KEYS, FW_THREADS>(nkt, [](int it) { return it * FW_KEYS; }, Kb, ts, Vb, ts, T, lds, L::KLD,
-                                           L::VLD, tid, body);
+  RegStage<HD, FW_THREADS> rs;
+  auto store = [&](int buf) {
+    bf16* sK = lds + buf * L::STAGE;
+    bf16* sV = sK + FW_KEYS * L::KLD;
+#pragma unroll
+    for (int i = 0; i < RegStage<HD, FW_THREADS>::CPT; ++i) {
+      const int c = tid + FW_THREADS * i, rr = c / (HD / 8), col = (c % (HD / 8)) * 8;
+      *(u32x4*)(sK + rr * L::KLD + col) = rs.x[i];
+      *(u32x4*)(sV + rr * L::VLD + col) = rs.y[i];
+    }
+  };
+  rs.load(rK, ts, rV, ts, 0, tid);
+  store(0);
+  __syncthreads();
+  for (int it = 0; it < nkt; ++it) {
+    if (it + 1 < nkt) rs.load(rK, ts, rV, ts, (it + 1) * FW_KEYS, tid);
+    const int kb = it * FW_KEYS;
+    const bf16* sK = lds + (it & 1) * L::STAGE;
+    if (kb <= q0 + 31 && q0 < T) {  // wave-uniform: else the whole tile lies past this wave's queries
+      if (kb + FW_KEYS - 1 > q0) tile(sK, sK + FW_KEYS * L::KLD, kb, std::true_type{});
+      else tile(sK, sK + FW_KEYS * L::KLD, kb, std::false_type{});
+    }
+    if (it + 1 < nkt) store((it + 1) & 1);
+    __syncthreads();
+  }
   l += __shfl_xor(l, 32, 64);
   if (q < T) {
     const float inv = 1.f / l;
@@ -815,21 +860,22 @@ __device__ __forceinline__ bf16x8 sw_tr(const bf16* t, int k0, int c0, int lane)
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-// Two [64][64] bf16 tiles (rows t0.., two operands) + optionally two fp32 row vectors [64] (lse, delta),
-// register-staged: load() issues the global loads, store() writes the swizzled images.
+// Two [64][64] bf16 tiles (rows t0.., two operands, buffer-resource loads) + optionally two fp32 row vectors
+// [64] (lse, delta) for the swizzled images; ONE register set (T14: tile t+1 loaded before tile t's
+// compute, written to the other LDS buffer after it), one barrier per tile.
 template <int NTH, bool VEC>
 struct SwStage {
   static constexpr int CPT = 64 * 8 / NTH;
   u32x4 x[CPT], y[CPT];
   f32x4 v;
-  __device__ __forceinline__ void load(const bf16* __restrict__ bx, long sx, const bf16* __restrict__ by, long sy,
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rx, long sx, __amdgpu_buffer_rsrc_t ry, long sy,
                                        const float* __restrict__ va, const float* __restrict__ vb, int t0, int T,
                                        int tid) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + NTH * i, r = c >> 3, ch = c & 7, t = t0 + r;
-      x[i] = t < T ? *(const u32x4*)(bx + (long)t * sx + ch * 8) : u32x4{0, 0, 0, 0};
-      y[i] = t < T ? *(const u32x4*)(by + (long)t * sy + ch * 8) : u32x4{0, 0, 0, 0};
+      const int c = tid + NTH * i, r = c >> 3, ch = c & 7;
+      x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((long)(t0 + r) * sx + 8 * ch) * 2), 0, 0));
+      y[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, (int)(((long)(t0 + r) * sy + 8 * ch) * 2), 0, 0));
     }
     if (VEC && tid < 32) {
       const float* src = tid < 16 ? va : vb;
@@ -850,29 +896,23 @@ struct SwStage {
 };
 constexpr int SW_STAGE = 2 * 64 * 64 + 2 * 64 * 2;  // bf16 elements per stage (2 images + 2 fp32 vectors)
 
-// body(sX, sY, sVec, it) over tiles t0_of(it), two LDS + two register stages, one barrier per tile
+// body(sX, sY, sVec, it) over tiles t0_of(it)
 template <int NTH, bool VEC, typename T0, typename Body>
-__device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, const bf16* bx, long sx, const bf16* by, long sy,
-                                                   const float* va, const float* vb, int T, bf16* lds, int tid,
-                                                   Body body) {
+__device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, __amdgpu_buffer_rsrc_t rx, long sx,
+                                                   __amdgpu_buffer_rsrc_t ry, long sy, const float* va,
+                                                   const float* vb, int T, bf16* lds, int tid, Body body) {
   if (n <= 0) return;
-  bf16* X[2] = {lds, lds + SW_STAGE};
-  SwStage<NTH, VEC> p0, p1;
-  auto Y = [&](int k) { return X[k] + 64 * 64; };
-  auto Vv = [&](int k) { return (float*)(X[k] + 2 * 64 * 64); };
-  p0.load(bx, sx, by, sy, va, vb, t0_of(0), T, tid);
-  if (n > 1) p1.load(bx, sx, by, sy, va, vb, t0_of(1), T, tid);
-  p0.store(X[0], Y(0), Vv(0), tid);
+  SwStage<NTH, VEC> st;
+  auto X = [&](int k) { return lds + k * SW_STAGE; };
+  auto Y = [&](int k) { return lds + k * SW_STAGE + 64 * 64; };
+  auto Vv = [&](int k) { return (float*)(lds + k * SW_STAGE + 2 * 64 * 64); };
+  st.load(rx, sx, ry, sy, va, vb, t0_of(0), T, tid);
+  st.store(X(0), Y(0), Vv(0), tid);
   __syncthreads();
-  for (int it = 0; it < n; it += 2) {
-    if (it + 2 < n) p0.load(bx, sx, by, sy, va, vb, t0_of(it + 2), T, tid);
-    body(X[0], Y(0), Vv(0), it);
-    if (it + 1 < n) p1.store(X[1], Y(1), Vv(1), tid);
-    __syncthreads();
-    if (it + 1 >= n) break;
-    if (it + 3 < n) p1.load(bx, sx, by, sy, va, vb, t0_of(it + 3), T, tid);
-    body(X[1], Y(1), Vv(1), it + 1);
-    if (it + 2 < n) p0.store(X[0], Y(0), Vv(0), tid);
+  for (int it = 0; it < n; ++it) {
+    if (it + 1 < n) st.load(rx, sx, ry, sy, va, vb, t0_of(it + 1), T, tid);
+    body(X(it & 1), Y(it & 1), Vv(it & 1), it);
+    if (it + 1 < n) st.store(X((it + 1) & 1), Y((it + 1) & 1), Vv((it + 1) & 1), tid);
     __syncthreads();
   }
 }
@@ -882,7 +922,7 @@ __device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, const bf16* 
 // dO stationary in registers), dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K transposed
 // fragments, dS^T straight from the accumulators).
 template <int HD>
-__global__ void __launch_bounds__(FW_THREADS) attn_bwd_dq32_kernel(
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
     float scale) {
@@ -918,39 +958,44 @@ __global__ void __launch_bounds__(FW_THREADS) attn_bwd_dq32_kernel(
   f32x16 acc[HB];
 #pragma unroll
   for (int i = 0; i < HB; ++i) acc[i] = f32x16{};
+  // one 32-key block; MASK only on the diagonal blocks (a separate instantiation, so the full blocks
+  // carry no per-element compares).  Keys >= T only meet queries >= T (key <= q), whose rows are never
+  // written, and load as zeros (buffer range): the causal mask suffices.
+  auto kblock = [&](const bf16* sK, const bf16* sV, int k2, int ks, auto MASK) {
+    f32x16 st = f32x16{}, dp = f32x16{};
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      st = mfma32(sw_row(sK, 32 * k2 + r, 2 * c + hh), qf[c], st);
+      dp = mfma32(sw_row(sV, 32 * k2 + r, 2 * c + hh), df[c], dp);
+    }
+    const int lim = q - (ks + 4 * hh);  // register i holds key ks + 4h + (i & 3) + 8 (i >> 2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float pv = fast_exp2(fmaf(st[i], cs, -lq));
+      if constexpr (decltype(MASK)::value) pv = ((i & 3) + 8 * (i >> 2) <= lim) ? pv : 0.f;
+      st[i] = pv * (dp[i] - dlt);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 dsb = pack8(st, s2);
+#pragma unroll
+      for (int i = 0; i < HB; ++i) acc[i] = mfma32(sw_tr(sK, 32 * k2 + 16 * s2, 32 * i, lane), dsb, acc[i]);
+    }
+  };
   auto body = [&](const bf16* sK, const bf16* sV, const float*, int it) {
     const int kb = it * 64;
     if (kb > q0 + 31 || q0 >= T) return;
-    const bool diag = kb + 63 > q0;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      if (kb + 32 * k2 > q0 + 31) break;  // wave-uniform: the second 32 keys lie past every query
-      f32x16 st = f32x16{}, dp = f32x16{};
-#pragma unroll
-      for (int c = 0; c < HC; ++c) {
-        st = mfma32(sw_row(sK, 32 * k2 + r, 2 * c + hh), qf[c], st);
-        dp = mfma32(sw_row(sV, 32 * k2 + r, 2 * c + hh), df[c], dp);
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pv = fast_exp2(fmaf(st[i], cs, -lq));
-        if (diag) {
-          const int key = kb + 32 * k2 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          pv = (key <= q && key < T && q < T) ? pv : 0.f;
-        }
-        st[i] = pv * (dp[i] - dlt);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 dsb = pack8(st, s2);
-#pragma unroll
-        for (int i = 0; i < HB; ++i) acc[i] = mfma32(sw_tr(sK, 32 * k2 + 16 * s2, 32 * i, lane), dsb, acc[i]);
-      }
+      const int ks = kb + 32 * k2;
+      if (ks > q0 + 31) break;  // wave-uniform: these 32 keys lie past every query
+      if (ks + 31 > q0) kblock(sK, sV, k2, ks, std::true_type{});
+      else kblock(sK, sV, k2, ks, std::false_type{});
     }
   };
   const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + 63) / 64;
-  sw_pipelined_tiles<FW_THREADS, false>(nkt, [](int it) { return it * 64; }, Kb, ts, Vb, ts, nullptr, nullptr, T, lds,
-                                        tid, body);
+  sw_pipelined_tiles<FW_THREADS, false>(nkt, [](int it) { return it * 64; }, rows_rsrc(Kb, ts, T, HD), ts,
+                                        rows_rsrc(Vb, ts, T, HD), ts, nullptr, nullptr, T, lds, tid, body);
   if (q < T) {
     bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
 #pragma unroll
@@ -967,8 +1012,14 @@ __global__ void __launch_bounds__(FW_THREADS) attn_bwd_dq32_kernel(
 // S = Q K^T and dP = dO V^T (Q / dO row fragments, K / V stationary), P and dS = P (dP - delta) with the
 // key on the lane, dV^T += dO^T P and dK^T += Q^T dS (Q / dO transposed fragments of the same images,
 // P / dS straight from the accumulators).  The heaviest key block (0: every query) goes first.
+#ifndef DTC_DKDV_SPLIT_MASK
+#define DTC_DKDV_SPLIT_MASK 0
+#endif
+#ifndef DTC_DKDV_OCC
+#define DTC_DKDV_OCC 2
+#endif
 template <int HD>
-__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dkdv32_kernel(
+__global__ void __launch_bounds__(FW_THREADS, DTC_DKDV_OCC) attn_bwd_dkdv32_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   static_assert(HD == 64, "swizzled 64-wide images");
@@ -999,53 +1050,59 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dkdv32_kernel(
 #pragma unroll
   for (int i = 0; i < HB; ++i) dk[i] = dv[i] = f32x16{};
   const int qt0 = kblk * FW_QROWS / 64;  // first 64-query tile (queries >= the block's keys)
+  // one 32-query block; MASK (causal, key <= query) only where the block straddles the wave's keys.
+  // Queries >= T need no mask: their Q / dO rows load as zeros (buffer range) and lse / delta as 0, so
+  // they add nothing to dK / dV; keys >= T are never written.
+  auto qblock = [&](const bf16* sQ, const bf16* sD, const float* sv, int k2, int qs, auto MASK) {
+    f32x16 sc = f32x16{}, dp = f32x16{};
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      sc = mfma32(sw_row(sQ, 32 * k2 + r, 2 * c + hh), kf[c], sc);
+      dp = mfma32(sw_row(sD, 32 * k2 + r, 2 * c + hh), vf[c], dp);
+    }
+    const int lim = key - (qs + 4 * hh);  // register 4 g4 + e holds query qs + 4h + 8 g4 + e
+    f32x16 ds;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int qr = 32 * k2 + 8 * g4 + 4 * hh;  // tile rows of registers 4 g4 .. 4 g4 + 3
+      const f32x4 l4 = *(const f32x4*)(sv + qr), d4 = *(const f32x4*)(sv + 64 + qr);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g4 + e;
+        float pv = fast_exp2(fmaf(sc[i], cs, -l4[e] * LOG2E));
+        if constexpr (decltype(MASK)::value) pv = (8 * g4 + e >= lim) ? pv : 0.f;
+        sc[i] = pv;
+        ds[i] = pv * (dp[i] - d4[e]);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb = pack8(sc, s2), dsb = pack8(ds, s2);
+#pragma unroll
+      for (int i = 0; i < HB; ++i) {
+        dv[i] = mfma32(sw_tr(sD, 32 * k2 + 16 * s2, 32 * i, lane), pb, dv[i]);
+        dk[i] = mfma32(sw_tr(sQ, 32 * k2 + 16 * s2, 32 * i, lane), dsb, dk[i]);
+      }
+    }
+  };
   auto body = [&](const bf16* sQ, const bf16* sD, const float* sv, int it) {
     const int qb = (qt0 + it) * 64;
     if (qb + 63 < k0w || k0w >= T) return;  // wave-uniform: every query of the tile before the keys
-    const float* sl = sv;
-    const float* sd = sv + 64;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
       const int qs = qb + 32 * k2;
       if (qs + 31 < k0w || qs >= T) continue;  // wave-uniform
-      const bool diag = qs < k0w + 31 || qs + 32 > T;
-      f32x16 sc = f32x16{}, dp = f32x16{};
-#pragma unroll
-      for (int c = 0; c < HC; ++c) {
-        sc = mfma32(sw_row(sQ, 32 * k2 + r, 2 * c + hh), kf[c], sc);
-        dp = mfma32(sw_row(sD, 32 * k2 + r, 2 * c + hh), vf[c], dp);
-      }
-      f32x16 ds;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int qr = 32 * k2 + 8 * g4 + 4 * hh;  // tile rows of registers 4 g4 .. 4 g4 + 3
-        const f32x4 l4 = *(const f32x4*)(sl + qr), d4 = *(const f32x4*)(sd + qr);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g4 + e;
-          float pv = fast_exp2(fmaf(sc[i], cs, -l4[e] * LOG2E));
-          if (diag) {
-            const int qq = qb + qr + e;
-            pv = (key <= qq && qq < T && key < T) ? pv : 0.f;
-          }
-          sc[i] = pv;
-          ds[i] = pv * (dp[i] - d4[e]);
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pb = pack8(sc, s2), dsb = pack8(ds, s2);
-#pragma unroll
-        for (int i = 0; i < HB; ++i) {
-          dv[i] = mfma32(sw_tr(sD, 32 * k2 + 16 * s2, 32 * i, lane), pb, dv[i]);
-          dk[i] = mfma32(sw_tr(sQ, 32 * k2 + 16 * s2, 32 * i, lane), dsb, dk[i]);
-        }
-      }
+#if DTC_DKDV_SPLIT_MASK
+      if (qs < k0w + 31) qblock(sQ, sD, sv, k2, qs, std::true_type{});
+      else qblock(sQ, sD, sv, k2, qs, std::false_type{});
+#else  // one instantiation: two exceed 256 VGPRs at 2 waves / SIMD (spills); lim < 0 masks nothing
+      qblock(sQ, sD, sv, k2, qs, std::true_type{});
+#endif
     }
   };
   const int nqt = (T - qt0 * 64 + 63) / 64;
-  sw_pipelined_tiles<FW_THREADS, true>(nqt, [qt0](int it) { return (qt0 + it) * 64; }, Qb, ts, dOb, dts, lseb, delb, T,
-                                       lds, tid, body);
+  sw_pipelined_tiles<FW_THREADS, true>(nqt, [qt0](int it) { return (qt0 + it) * 64; }, rows_rsrc(Qb, ts, T, HD), ts,
+                                       rows_rsrc(dOb, dts, T, HD), dts, lseb, delb, T, lds, tid, body);
   if (key < T) {
     bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
     bf16* pv = dqkv + ((long)b * T + key) * ts + (2 * H + h) * HD;
