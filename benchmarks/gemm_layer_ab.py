@@ -1,0 +1,119 @@
+"""In-process A/B of the layer-GEMM plans at a model's training shapes (every NT-layout GEMM the step
+runs: the forwards and the dgrads on transposed weights), interleaved rounds, with hipBLASLt
+(torch.matmul on the same bf16 operands) as a yardstick and a numerics check of every variant
+against an fp32 torch reference.
+
+    python benchmarks/gemm_layer_ab.py [--model gpt2-small] [--rounds 5] [--reps 30]
+
+Variants (dtc_gemm_set_4w): ``off`` (gemm4w off: the other kernels' plans), ``default`` (the shipped
+plan, DTC_GEMM4W as set at load) and ``4w`` (gemm4w_kernel on every covered problem).
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_training_compare_jax_amd.ops import _native as NV  # noqa: E402
+from distributed_training_compare_jax_amd.ops import gemm as G  # noqa: E402
+
+
+def graph_time(fn, reps):
+    """GPU time per call: `reps` calls captured in one hipGraph, replayed (host launch cost excluded)."""
+    fn()
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        gr.capture_begin()
+        for _ in range(reps):
+            fn()
+        gr.capture_end()
+    torch.cuda.current_stream().wait_stream(st)
+    gr.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    gr.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    from distributed_training_compare_jax_amd.config.schema import model_config_from_preset
+
+    mc = model_config_from_preset(a.model)
+    M, D, F = 8 * mc.max_seq_len, mc.d_model, mc.d_ff
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    r = lambda *s, sc=0.5: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)  # noqa: E731
+    L = NV.lib()
+    cases = []
+
+    def add(name, flops, fn, ref, blas):
+        if not a.only or any(o in name for o in a.only.split(",")):
+            cases.append((name, flops, fn, ref, blas))
+
+    for (n, k, tag) in [(3 * D, D, "qkv"), (D, D, "out"), (F, D, "fc1"), (D, F, "fc2")]:
+        x, w, b = r(M, k), r(n, k, sc=0.05), torch.randn(n, device=dev, generator=g) * 0.1
+        fl = 2.0 * M * n * k
+        if tag in ("out", "fc2"):
+            res = torch.randn(M, n, device=dev, generator=g)
+            add(f"fwd {tag} [{M}x{n}x{k}] resid", fl, lambda x=x, w=w, b=b, res=res: G.linear_resid(x, w, b, res),
+                lambda x=x, w=w, b=b, res=res: x.float() @ w.float().t() + b + res, lambda x=x, w=w: x @ w.t())
+        elif tag == "fc1":
+            add(f"fwd {tag} [{M}x{n}x{k}] gelu", fl, lambda x=x, w=w, b=b: G.linear_gelu(x, w, b)[1],
+                lambda x=x, w=w, b=b: G.gelu_tanh(x.float() @ w.float().t() + b), lambda x=x, w=w: x @ w.t())
+        else:
+            add(f"fwd {tag} [{M}x{n}x{k}]", fl, lambda x=x, w=w, b=b: G.linear(x, w, b),
+                lambda x=x, w=w, b=b: x.float() @ w.float().t() + b, lambda x=x, w=w: x @ w.t())
+        dy, wt = r(M, n), w.t().contiguous()
+        if tag == "fc2":
+            u = r(M, k)
+            add(f"ntdgrad {tag} [{M}x{k}x{n}] dgelu", fl, lambda dy=dy, wt=wt, u=u: G.matmul_nt_dgelu(dy, wt, u),
+                lambda dy=dy, w=w, u=u: (dy.float() @ w.float()) * u.float(), lambda dy=dy, w=w: dy @ w)
+        elif tag == "out":
+            add(f"ntdgrad {tag} [{M}x{k}x{n}] bf16", fl, lambda dy=dy, wt=wt: G.linear(dy, wt),
+                lambda dy=dy, w=w: dy.float() @ w.float(), lambda dy=dy, w=w: dy @ w)
+        else:
+            add(f"ntdgrad {tag} [{M}x{k}x{n}] f32", fl, lambda dy=dy, wt=wt: G.linear(dy, wt, out_dtype=torch.float32),
+                lambda dy=dy, w=w: dy.float() @ w.float(), lambda dy=dy, w=w: dy @ w)
+
+    old = L.dtc_gemm_set_4w(0)
+    variants = {"off": 0, "default": old, "4w": 2}
+    for name, _, fn, ref, _ in cases:
+        want = ref().float()
+        for vn, v in variants.items():
+            L.dtc_gemm_set_4w(v)
+            got = fn().float()
+            err = ((got - want).norm() / want.norm()).item()
+            print(f"check {name:36s} {vn:8s} rel err {err:.2e}", flush=True)
+            assert err < 1e-2, (name, vn, err)
+    res = {(c[0], v): [] for c in cases for v in list(variants) + ["hipBLASLt"]}
+    for _ in range(a.rounds):
+        for name, _, fn, _, blas in cases:
+            for vn, v in variants.items():
+                L.dtc_gemm_set_4w(v)
+                res[(name, vn)].append(graph_time(fn, a.reps))
+            res[(name, "hipBLASLt")].append(graph_time(blas, a.reps))
+    L.dtc_gemm_set_4w(old)
+    for name, fl, *_ in cases:
+        row = []
+        for vn in list(variants) + ["hipBLASLt"]:
+            v = sorted(res[(name, vn)])
+            med = v[len(v) // 2]
+            row.append(f"{vn} {med:7.1f} us ({fl / med / 1e6:6.0f} TF/s)")
+        print(f"{name:36s} " + "  ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

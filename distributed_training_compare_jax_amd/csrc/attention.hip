@@ -1012,14 +1012,8 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
 // S = Q K^T and dP = dO V^T (Q / dO row fragments, K / V stationary), P and dS = P (dP - delta) with the
 // key on the lane, dV^T += dO^T P and dK^T += Q^T dS (Q / dO transposed fragments of the same images,
 // P / dS straight from the accumulators).  The heaviest key block (0: every query) goes first.
-#ifndef DTC_DKDV_SPLIT_MASK
-#define DTC_DKDV_SPLIT_MASK 0
-#endif
-#ifndef DTC_DKDV_OCC
-#define DTC_DKDV_OCC 2
-#endif
 template <int HD>
-__global__ void __launch_bounds__(FW_THREADS, DTC_DKDV_OCC) attn_bwd_dkdv32_kernel(
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dkdv32_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   static_assert(HD == 64, "swizzled 64-wide images");
@@ -1092,12 +1086,10 @@ __global__ void __launch_bounds__(FW_THREADS, DTC_DKDV_OCC) attn_bwd_dkdv32_kern
     for (int k2 = 0; k2 < 2; ++k2) {
       const int qs = qb + 32 * k2;
       if (qs + 31 < k0w || qs >= T) continue;  // wave-uniform
-#if DTC_DKDV_SPLIT_MASK
-      if (qs < k0w + 31) qblock(sQ, sD, sv, k2, qs, std::true_type{});
-      else qblock(sQ, sD, sv, k2, qs, std::false_type{});
-#else  // one instantiation: two exceed 256 VGPRs at 2 waves / SIMD (spills); lim < 0 masks nothing
+      // one (masked) instantiation: a second, unmasked one pushes the kernel past 256 VGPRs at 2 waves /
+      // SIMD (59 spilled; measured 101 vs 85 us at 1 wave / SIMD, profiles/r4_attn32_ab.log).  Off the
+      // diagonal lim <= 0, so the compare keeps every element.
       qblock(sQ, sD, sv, k2, qs, std::true_type{});
-#endif
     }
   };
   const int nqt = (T - qt0 * 64 + 63) / 64;
