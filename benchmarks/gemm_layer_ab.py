@@ -5,8 +5,10 @@ against an fp32 torch reference.
 
     python benchmarks/gemm_layer_ab.py [--model gpt2-small] [--rounds 5] [--reps 30]
 
-Variants (dtc_gemm_set_4w): ``off`` (gemm4w off: the other kernels' plans), ``default`` (the shipped
-plan, DTC_GEMM4W as set at load) and ``4w`` (gemm4w_kernel on every covered problem).
+Variants (dtc_gemm_set_4w): ``default`` (the shipped plan, DTC_GEMM4W as set at load), ``4w``
+(gemm4w_kernel on every covered problem) and ``4p`` (gemm4p_kernel, one pipelined block per CU).
+``--cold``: every call follows a 512 MB buffer write, so its operands come from HBM as in the step (the
+warm numbers ranked gemm4w ahead; the step disagreed, profiles/r4_ab_step_knobs.log).
 """
 import argparse
 import os
@@ -19,8 +21,12 @@ from distributed_training_compare_jax_amd.ops import _native as NV  # noqa: E402
 from distributed_training_compare_jax_amd.ops import gemm as G  # noqa: E402
 
 
-def graph_time(fn, reps):
-    """GPU time per call: `reps` calls captured in one hipGraph, replayed (host launch cost excluded)."""
+def graph_time(fn, reps, pre=None):
+    """GPU time per call: `reps` calls captured in one hipGraph, replayed (host launch cost excluded).
+    ``pre``: a cache-flushing op captured before every call; its own time (measured alone) is subtracted."""
+    if pre is not None:
+        both = graph_time(lambda: (pre(), fn()), reps)
+        return both - graph_time(pre, reps)
     fn()
     torch.cuda.synchronize()
     gr = torch.cuda.CUDAGraph()
@@ -48,6 +54,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default="")
+    ap.add_argument("--cold", action="store_true",
+                    help="write a 512 MB buffer before every call (operands come from HBM, as in the step)")
     a = ap.parse_args()
     from distributed_training_compare_jax_amd.config.schema import model_config_from_preset
 
@@ -58,6 +66,10 @@ def main():
     r = lambda *s, sc=0.5: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)  # noqa: E731
     L = NV.lib()
     cases = []
+    pre = None
+    if a.cold:
+        flush = torch.empty(128 << 20, dtype=torch.float32, device=dev)
+        pre = lambda: flush.fill_(1.0)  # noqa: E731
 
     def add(name, flops, fn, ref, blas):
         if not a.only or any(o in name for o in a.only.split(",")):
@@ -89,7 +101,7 @@ def main():
                 lambda dy=dy, w=w: dy.float() @ w.float(), lambda dy=dy, w=w: dy @ w)
 
     old = L.dtc_gemm_set_4w(0)
-    variants = {"off": 0, "default": old, "4w": 2}
+    variants = {"default": old, "4w": 2, "4p": 4}
     for name, _, fn, ref, _ in cases:
         want = ref().float()
         for vn, v in variants.items():
@@ -103,8 +115,8 @@ def main():
         for name, _, fn, _, blas in cases:
             for vn, v in variants.items():
                 L.dtc_gemm_set_4w(v)
-                res[(name, vn)].append(graph_time(fn, a.reps))
-            res[(name, "hipBLASLt")].append(graph_time(blas, a.reps))
+                res[(name, vn)].append(graph_time(fn, a.reps, pre))
+            res[(name, "hipBLASLt")].append(graph_time(blas, a.reps, pre))
     L.dtc_gemm_set_4w(old)
     for name, fl, *_ in cases:
         row = []

@@ -1,5 +1,6 @@
-"""Layer-GEMM kernel with 4 waves and two blocks per CU (csrc/gemm.hip gemm4w_kernel: 128 x 192 tiles,
-64 x 96 per wave, two-stage LDS-DMA pipeline).  Every epilogue the NT-layout layer GEMMs use (bf16 +
+"""Layer-GEMM kernels with 4 waves, 128 x 192 tiles, 64 x 96 per wave (csrc/gemm.hip gemm4w_kernel: two
+blocks per CU, two-stage LDS-DMA pipeline; gemm4p_kernel: one block per CU, four stages, double-buffered
+fragments).  Both are opt-in (DTC_GEMM4W).  Every epilogue the NT-layout layer GEMMs use (bf16 +
 bias, fp32 residual, GELU pair, dGELU, fp32 / bf16 dgrad) at the GPT-2 small shapes and at small shapes
 with several K-steps and tiles, against the fp32 PyTorch reference of the same op and against the
 kernels the same call takes with the path switched off."""
@@ -26,11 +27,12 @@ def _close(a, b, rtol, name):
     assert err <= rtol * ref, f"{name}: max abs err {err:.3e} vs ref max {ref:.3e}"
 
 
-@pytest.fixture
-def w4(cuda):
-    """gemm4w forced on every covered shape (the default plan leaves the dGELU / K=768 residual ones)"""
+@pytest.fixture(params=[2, 4], ids=["gemm4w", "gemm4p"])
+def w4(cuda, request):
+    """gemm4w (two blocks per CU) or gemm4p (one pipelined block per CU) forced on every covered shape"""
     L = N.lib()
-    old = L.dtc_gemm_set_4w(2)
+    old = L.dtc_gemm_set_4w(request.param)
+    L.mode4 = request.param
     yield L
     L.dtc_gemm_set_4w(old)
 
@@ -64,7 +66,7 @@ def test_4w_epilogues(w4, M, Nn, K):
     w4.dtc_gemm_set_4w(0)
     yr0 = G.linear_resid(x, w, b, res)
     yf0 = G.linear(x, w, out_dtype=torch.float32)
-    w4.dtc_gemm_set_4w(2)
+    w4.dtc_gemm_set_4w(w4.mode4)
     _close(yr, yr0, 1e-4, "resid_vs_off")
     _close(yf, yf0, 1e-4, "f32_vs_off")
     # deterministic: the same launch twice is bitwise identical
