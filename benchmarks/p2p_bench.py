@@ -1,5 +1,6 @@
 """Latency of the xGMI P2P all-reduce kernels (parallel/p2p.py) per call, one-shot vs two-shot, at the
-TP message sizes, with W ranks.  On a multi-GPU node this is the real xGMI number; on the 1-GPU dev box
+TP message sizes, with W ranks: fp32 one-shot / two-shot, and the bf16 payload (tp_comm_dtype: bf16)
+staged by a copy kernel vs written in place by its producer (``x=None``: one launch fewer).  On a multi-GPU node this is the real xGMI number; on the 1-GPU dev box
 the W processes share one device (IPC within a device), so it measures the kernel path itself —
 launches, device barriers, the copy/reduce passes at HBM speed — not link bandwidth.
 
@@ -32,7 +33,14 @@ def _worker(reps, out_dir):
     for nbytes in SIZES:
         n = nbytes // 4
         t = torch.full((n,), float(d.rank + 1), device=d.device)
-        for mode, name in ((2, "one-shot"), (1, "two-shot")):
+        xb = torch.full((n,), float(d.rank + 1), dtype=torch.bfloat16, device=d.device)
+        ob = torch.empty(n, device=d.device)
+        variants = [(2, "one-shot", lambda m: ar.all_reduce_(t, mode=m)), (1, "two-shot", lambda m: ar.all_reduce_(t, mode=m)),
+                    # tp_comm_dtype: bf16 (the same element count, half the bytes): copied into the buffer
+                    # by the stage kernel, or already written there by its producer GEMM (staged)
+                    (0, "bf16 copy", lambda m: ar.all_reduce_bf16(xb, ob, mode=m)),
+                    (0, "bf16 staged", lambda m: ar.all_reduce_bf16(None, ob, mode=m))]
+        for mode, name, call in variants:
             if mode == 2 and nbytes > (8 << 20):
                 continue
             # captured: reps calls in one hipGraph (how the step runs them), timed by events
@@ -42,7 +50,8 @@ def _worker(reps, out_dir):
             with torch.cuda.stream(s):
                 g.capture_begin(capture_error_mode="thread_local")
                 for _ in range(reps):
-                    ar.all_reduce_(t, mode=mode)
+                    call(mode)
+                ar.end_step()
                 g.capture_end()
             torch.cuda.current_stream().wait_stream(s)
             times = []

@@ -318,6 +318,9 @@ int dtc_p2p_allreduce(const float* x, float* out, long n, void* const* bases, in
 
 // out (fp32) = resid + bias + sum over ranks of x (bf16, n % 8 == 0, n * 2 <= half_bytes); resid / bias
 // optional (null), bias indexed by column (ncols % 8 == 0).  mode as dtc_p2p_allreduce; x may not alias out.
+// x == nullptr: the partial is already in this rank's buffer half of the call (the row-parallel GEMM wrote
+// it there, parallel/p2p.py staged_out): no stage launch -- barrier + one-shot (2 launches) or barrier +
+// reduce-scatter + barrier + all-gather (4).
 int dtc_p2p_allreduce_bf16(const bf16* x, float* out, long n, void* const* bases, int rank, int world, long half_bytes,
                            uint32_t* epoch, int* err, int mode, const float* resid, const float* bias, int ncols,
                            hipStream_t st) {
@@ -327,9 +330,11 @@ int dtc_p2p_allreduce_bf16(const bf16* x, float* out, long n, void* const* bases
   const long n8 = n / 8;
   const int blocks = (int)std::min(1024L, std::max(1L, (n8 + 255) / 256));
   const bool one = mode == 2 || (mode == 0 && oneshot_auto(n * 2, world));
-  hipLaunchKernelGGL(p2p_stage_bf16_kernel, dim3(blocks), dim3(256), 0, st, (const bf16x8*)x, t, rank, n8, half_bytes,
-                     epoch);
-  DTC_CHECK_LAUNCH();
+  if (x) {
+    hipLaunchKernelGGL(p2p_stage_bf16_kernel, dim3(blocks), dim3(256), 0, st, (const bf16x8*)x, t, rank, n8,
+                       half_bytes, epoch);
+    DTC_CHECK_LAUNCH();
+  }
   if (one) {
     hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 2);
     DTC_CHECK_LAUNCH();
@@ -348,6 +353,18 @@ int dtc_p2p_allreduce_bf16(const bf16* x, float* out, long n, void* const* bases
   DTC_CHECK_LAUNCH();
   hipLaunchKernelGGL(p2p_all_gather_bf16_kernel, dim3(blocks), dim3(256), 0, st, t, world, n8, half_bytes, out, resid,
                      bias, ncols, epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// A call with no payload (one barrier round, epoch + 2): keeps the number of calls per step even, so the
+// buffer half of every call site -- which the host hands to a producer GEMM (staged_out) -- is the same
+// on every replay of a captured step.
+int dtc_p2p_barrier_round(void* const* bases, int rank, int world, uint32_t* epoch, int* err, hipStream_t st) {
+  if (world < 1 || world > P2P_MAX) return 4001;
+  PeerTable t;
+  for (int p = 0; p < P2P_MAX; ++p) t.base[p] = (unsigned char*)(p < world ? bases[p] : nullptr);
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 2);
   DTC_CHECK_LAUNCH();
   return 0;
 }

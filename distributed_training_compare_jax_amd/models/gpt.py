@@ -70,6 +70,15 @@ if _CE_CHUNK < 0 or _CE_CHUNK % 256:
     raise ValueError(f"DTC_CE_CHUNK={_CE_CHUNK}: must be 0 (off) or a positive multiple of 256 vocab columns")
 
 
+
+class _Staged:
+    """A TP input-gradient partial a dgrad GEMM wrote into the P2P buffer (``TPComm.partial_out``)."""
+
+    __slots__ = ("rows", "cols", "device")
+
+    def __init__(self, rows: int, cols: int, device):
+        self.rows, self.cols, self.device = rows, cols, device
+
 class NoComm:
     """TP communicator stub for tp_size == 1."""
 
@@ -293,7 +302,7 @@ class GPTStage:
             x2, (y2, mu2, rs2) = LF.linear_resid_ln(o, f.w(p + "out.w"), f.p(p + "out.b"), x, f.p(p + "ln2.g"),
                                                     f.p(p + "ln2.b"), self.eps, self.ln_sync, self._ln_site(l, 0, False))
         elif self.tp_bf16:
-            x2 = tp.reduce_to(G.linear(o, f.w(p + "out.w"), None, out_dtype=torch.bfloat16), resid=x, bias=f.p(p + "out.b"))
+            x2 = self._row_parallel(o, p + "out.w", resid=x, bias=f.p(p + "out.b"))
             y2, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
         else:
             x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
@@ -307,8 +316,7 @@ class GPTStage:
                                               f.p(nxt + ".b"), self.eps, self.ln_sync, self._ln_site(l, 1, False))
             ctx[("ln1", l + 1) if nxt != "lnf" else "lnf_pre"] = pre_next
         elif self.tp_bf16:
-            x3 = tp.reduce_to(G.linear(gact, f.w(p + "fc2.w"), None, out_dtype=torch.bfloat16), resid=x2,
-                              bias=f.p(p + "fc2.b"))
+            x3 = self._row_parallel(gact, p + "fc2.w", resid=x2, bias=f.p(p + "fc2.b"))
         else:
             x3 = G.linear_resid(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b") if lead else None, x2 if lead else None)
             tp.all_reduce_(x3)
@@ -416,9 +424,22 @@ class GPTStage:
             dx_hook(out[0])
         return out
 
+    def _row_parallel(self, a, wname: str, resid, bias):
+        """fp32 ``resid + bias + Σ_tp a·Wᵀ`` with a bf16 partial (``tp_bf16``): the GEMM writes the partial
+        straight into this rank's P2P buffer half (no stage copy) when the P2P path takes it."""
+        w = self.flat.w(wname)
+        dst = self.tp.partial_out(a.shape[0], w.shape[0], bias)
+        if dst is not None:
+            G.linear_into(a, w, dst)
+            return self.tp.reduce_staged(a.shape[0], w.shape[0], resid=resid, bias=bias, device=a.device)
+        return self.tp.reduce_to(G.linear(a, w, None, out_dtype=torch.bfloat16), resid=resid, bias=bias)
+
     def _tp_reduce(self, d):
         """All-reduce an input-gradient partial over the TP group (in place for fp32 payloads; with
-        ``tp_bf16`` ``d`` is the bf16 partial and a new fp32 sum comes back)."""
+        ``tp_bf16`` ``d`` is the bf16 partial -- or a ``_Staged`` marker when the dgrad wrote it into the
+        P2P buffer -- and a new fp32 sum comes back)."""
+        if isinstance(d, _Staged):
+            return self.tp.reduce_staged(d.rows, d.cols, device=d.device)
         if self.tp.size == 1:
             return d
         if d.dtype == torch.bfloat16 and self.tp_bf16:
@@ -433,8 +454,17 @@ class GPTStage:
         wt = f.wt(dense + ".w")
         if self._defer_wg:
             if self.tp_bf16 and self.tp.size > 1:  # bf16 partial for the bf16-payload all-reduce
-                dx = (G.linear(dy, wt, out_dtype=torch.bfloat16) if wt is not None
-                      else G.matmul_nn(dy, f.w(dense + ".w"), out_dtype=torch.bfloat16))
+                rows, cols = dy.shape[0], (wt.shape[0] if wt is not None else f.w(dense + ".w").shape[1])
+                dst = self.tp.partial_out(rows, cols)
+                if dst is not None:  # straight into this rank's P2P buffer half (no stage copy)
+                    if wt is not None:
+                        G.linear_into(dy, wt, dst)
+                    else:
+                        G.matmul_nn_into(dy, f.w(dense + ".w"), dst)
+                    dx = _Staged(rows, cols, dy.device)
+                else:
+                    dx = (G.linear(dy, wt, out_dtype=torch.bfloat16) if wt is not None
+                          else G.matmul_nn(dy, f.w(dense + ".w"), out_dtype=torch.bfloat16))
             else:
                 dx = G.linear_resid(dy, wt, None, None) if wt is not None else G.matmul_nn(dy, f.w(dense + ".w"))
             self._wg(dy, x, dense, bias=True)

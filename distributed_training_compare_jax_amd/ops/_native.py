@@ -138,6 +138,7 @@ def _declare(lib):
         "dtc_p2p_free": ([vp], i),
         "dtc_p2p_allreduce": ([vp, vp, l, vp, i, i, l, vp, vp, i, vp], i),
         "dtc_p2p_allreduce_bf16": ([vp, vp, l, vp, i, i, l, vp, vp, i, vp, vp, i, vp], i),
+        "dtc_p2p_barrier_round": ([vp, i, i, vp, vp, vp], i),
         "dtc_embed_sort_bits": ([i], i),
         "dtc_embed_sort": ([vp, i, i, vp, vp], i),
         "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),

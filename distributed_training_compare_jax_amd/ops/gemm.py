@@ -150,6 +150,38 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return y
 
 
+class RawOut:
+    """A GEMM output that is not a torch tensor: a raw device pointer to a row-major [M, N] buffer
+    (ldc = N) -- the own half of the P2P all-reduce buffer a row-parallel GEMM writes its partial
+    into (parallel/p2p.py ``staged_out``), so no copy kernel stages it."""
+
+    __slots__ = ("ptr", "dtype", "device")
+
+    def __init__(self, ptr: int, dtype: torch.dtype, device):
+        self.ptr, self.dtype, self.device = int(ptr), dtype, torch.device(device)
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+
+def linear_into(x: torch.Tensor, w: torch.Tensor, out: RawOut):
+    """``out = x·Wᵀ`` (no bias) into a raw buffer (bf16 or fp32 per ``out.dtype``)."""
+    M, K = x.shape
+    Nn = w.shape[0]
+    assert w.shape[1] == K and x.is_cuda
+    _check2d(x, "x"); _check2d(w, "w")
+    _gemm_native(0, M, Nn, K, x, x.stride(0), w, w.stride(0), out, Nn)
+
+
+def matmul_nn_into(dy: torch.Tensor, w: torch.Tensor, out: RawOut):
+    """``out = dY·W`` (W [N, K] row-major, the NN dgrad) into a raw buffer."""
+    M, Nn = dy.shape
+    K = w.shape[1]
+    assert w.shape[0] == Nn and dy.is_cuda
+    _check2d(dy, "dy"); _check2d(w, "w")
+    _gemm_native(1, M, K, Nn, dy, dy.stride(0), w, w.stride(0), out, K)
+
+
 def linear_resid(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
                  resid: Optional[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fp32 ``out = resid + x·Wᵀ + bias`` (resid/bias optional; ``out`` may alias ``resid``)."""

@@ -101,6 +101,9 @@ class P2PAllReduce:
         self._bases = (ctypes.c_void_p * 8)(*(bases + [None] * (8 - world)))
         self._bases_ptr = ctypes.addressof(self._bases)
         self.epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # calls issued so far (host mirror of epoch / 2): the buffer half of the next call is calls & 1
+        self.calls = 0
+        self._flag_bytes = int(L.dtc_p2p_flag_bytes())
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         # all ranks' flag areas are zero before anyone's first barrier can run
         torch.cuda.synchronize(self.device)
@@ -117,20 +120,45 @@ class P2PAllReduce:
         N.check(N.lib().dtc_p2p_allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._bases_ptr, self.rank, self.world,
                                           self.half, self.epoch.data_ptr(), self.err.data_ptr(), int(mode),
                                           N.stream_ptr(t.device)), "dtc_p2p_allreduce")
+        self.calls += 1
         return t
+
+    def staged_out(self, numel: int, dtype=torch.bfloat16):
+        """Where the producer of the NEXT call's bf16 payload should write it (this rank's buffer half
+        of that call, a :class:`ops.gemm.RawOut`), or None if it does not fit.  The next call must then
+        be :meth:`all_reduce_bf16` with ``x=None``.  The half is ``calls & 1``; :meth:`end_step` keeps
+        the calls per step even so the half of each call site is the same on every graph replay."""
+        from ..ops.gemm import RawOut
+
+        if dtype != torch.bfloat16 or numel % 8 or numel * 2 > self.half:
+            return None
+        return RawOut(self._own + self._flag_bytes + (self.calls & 1) * self.half, dtype, self.device)
+
+    def end_step(self):
+        """Pad the step's calls to an even count with a payload-free barrier round (epoch + 2)."""
+        if self.calls & 1:
+            N.check(N.lib().dtc_p2p_barrier_round(self._bases_ptr, self.rank, self.world, self.epoch.data_ptr(),
+                                                  self.err.data_ptr(), N.stream_ptr(self.device)),
+                    "dtc_p2p_barrier_round")
+            self.calls += 1
 
     def supports_bf16(self, x: torch.Tensor) -> bool:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
                 and x.numel() * 2 <= self.half)
 
-    def all_reduce_bf16(self, x: torch.Tensor, out: torch.Tensor, resid=None, bias=None, mode: int = 0) -> torch.Tensor:
+    def all_reduce_bf16(self, x, out: torch.Tensor, resid=None, bias=None, mode: int = 0) -> torch.Tensor:
         """out (fp32) = resid + bias + Σ_ranks x, x bf16 (the payload), fp32 sums in rank order; ``bias``
-        indexed by the last dimension of ``out``.  Same barrier / buffer-half protocol as all_reduce_."""
+        indexed by the last dimension of ``out``.  Same barrier / buffer-half protocol as all_reduce_.
+        ``x=None``: the payload (``out.numel()`` values) was written by its producer straight into
+        :meth:`staged_out`, so no stage copy runs."""
         ncols = out.shape[-1] if bias is not None else 0
-        N.check(N.lib().dtc_p2p_allreduce_bf16(x.data_ptr(), out.data_ptr(), x.numel(), self._bases_ptr, self.rank,
+        n = out.numel() if x is None else x.numel()
+        assert x is not None or n * 2 <= self.half
+        N.check(N.lib().dtc_p2p_allreduce_bf16(N.ptr(x), out.data_ptr(), n, self._bases_ptr, self.rank,
                                                self.world, self.half, self.epoch.data_ptr(), self.err.data_ptr(),
-                                               int(mode), N.ptr(resid), N.ptr(bias), ncols, N.stream_ptr(x.device)),
+                                               int(mode), N.ptr(resid), N.ptr(bias), ncols, N.stream_ptr(out.device)),
                 "dtc_p2p_allreduce_bf16")
+        self.calls += 1
         return out
 
     def check(self):

@@ -67,6 +67,19 @@ class TPComm:
             out.add_(bias)
         return out
 
+    def partial_out(self, rows: int, cols: int, bias=None):
+        """Where a row-parallel GEMM should write its bf16 partial [rows, cols] so the P2P all-reduce
+        needs no stage copy (the own half of the P2P buffer, an ``ops.gemm.RawOut``), or None (no P2P,
+        size, or a bias the kernels cannot index).  Follow it by :meth:`reduce_staged`."""
+        if self.size == 1 or self.p2p is None or (bias is not None and cols % 8):
+            return None
+        return self.p2p.staged_out(rows * cols)
+
+    def reduce_staged(self, rows: int, cols: int, resid=None, bias=None, device=None) -> torch.Tensor:
+        """fp32 ``resid + bias + Σ_ranks partial`` for the partial a GEMM wrote into :meth:`partial_out`."""
+        out = torch.empty(rows, cols, dtype=torch.float32, device=device or self.p2p.device)
+        return self.p2p.all_reduce_bf16(None, out, resid, bias)
+
     def all_gather_stack(self, t: torch.Tensor) -> torch.Tensor:
         """[...] → [size, ...] (shard-major).  With the P2P path: every rank writes its slot of a
         zeroed [size, ...] buffer and the buffer is summed (x + 0 = x exactly, so it IS the gather),

@@ -490,7 +490,10 @@ class Engine:
         return self.loss
 
     def _step_fn(self):
-        return self._step_fn_pp() if self.mesh.pp > 1 else self._step_fn_dp_tp()
+        out = self._step_fn_pp() if self.mesh.pp > 1 else self._step_fn_dp_tp()
+        if self.p2p is not None:
+            self.p2p.end_step()  # even P2P calls per step: every call site keeps its buffer half on replay
+        return out
 
     # ------------------------------------------------------------------ public
     def run_step(self) -> torch.Tensor:

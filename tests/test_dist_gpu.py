@@ -173,6 +173,7 @@ def _p2p_worker(out_dir):
         t = x[d.rank].to(d.device).clone()
         ar.all_reduce_(t)
         res[f"eager{k}"] = t.cpu()
+    ar.end_step()  # 3 calls: padded to an even count (as every engine step ends)
     # captured in a hipGraph and replayed: the device epoch counter keeps ranks in step
     t = torch.zeros(4096 * 2, device=d.device)
     s = torch.cuda.Stream()
@@ -181,6 +182,7 @@ def _p2p_worker(out_dir):
     with torch.cuda.stream(s):
         gr.capture_begin(capture_error_mode="thread_local")
         ar.all_reduce_(t)
+        ar.end_step()
         gr.capture_end()
     torch.cuda.current_stream().wait_stream(s)
     outs = []
@@ -198,6 +200,40 @@ def _p2p_worker(out_dir):
         out = torch.empty(3 * 256, 64, device=d.device)
         ar.all_reduce_bf16(xb[d.rank].to(d.device).contiguous(), out, rs.to(d.device), bs.to(d.device), mode=mode)
         res[f"bf16_{mode}"] = out.cpu()
+    # staged payload (tp_comm_dtype: bf16 in the model): a GEMM writes the partial straight into this
+    # rank's buffer half of the next call (identity weight here: the partial is x), then the payload-free
+    # all-reduce; eager once, then captured with end_step's padding and replayed with new inputs
+    from distributed_training_compare_jax_amd.ops.gemm import linear_into
+
+    eye = torch.eye(64, dtype=torch.bfloat16, device=d.device)
+    xin = torch.empty(3 * 256, 64, dtype=torch.bfloat16, device=d.device)
+    rsd, bsd = rs.to(d.device), bs.to(d.device)
+    out = torch.empty(3 * 256, 64, device=d.device)
+
+    def staged():
+        linear_into(xin, eye, ar.staged_out(xin.numel()))
+        ar.all_reduce_bf16(None, out, rsd, bsd)
+
+    xin.copy_(xb[d.rank])
+    staged()
+    ar.end_step()
+    res["staged_eager"] = out.cpu()
+    gr2 = torch.cuda.CUDAGraph()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gr2.capture_begin(capture_error_mode="thread_local")
+        staged()
+        ar.end_step()
+        gr2.capture_end()
+    torch.cuda.current_stream().wait_stream(s)
+    outs = []
+    for it in range(3):
+        xin.copy_(xb[d.rank] * float(it + 1))
+        dist.barrier()
+        gr2.replay()
+        torch.cuda.synchronize()
+        outs.append(out.cpu().clone())
+    res["staged_graph"] = outs
     ar.check()
     torch.save(res, os.path.join(out_dir, f"p2p{d.rank}.pt"))
     ar.close()
@@ -206,7 +242,8 @@ def _p2p_worker(out_dir):
 
 def test_p2p_allreduce_two_ranks_one_gpu():
     """IPC-mapped two-shot all-reduce, 2 processes on one GPU: exact sum, identical on both ranks,
-    eager and replayed from a captured hipGraph."""
+    eager and replayed from a captured hipGraph; bf16 payloads (staged copy and written in place by a
+    GEMM, with end_step's even-call padding across replays)."""
     world = 2
     with tempfile.TemporaryDirectory() as td:
         spawn(_p2p_worker, world, args=(td,))
@@ -229,3 +266,9 @@ def test_p2p_allreduce_two_ranks_one_gpu():
             tol = 2e-2 if mode == 1 else 1e-5
             assert torch.allclose(r[i][f"bf16_{mode}"], exp, atol=tol, rtol=tol), (mode, i)
         assert torch.equal(r[0][f"bf16_{mode}"], r[1][f"bf16_{mode}"])
+    # staged (one-shot at W = 2): exact fp32 sums of the bf16 partials, eager and every graph replay
+    for i in range(world):
+        assert torch.allclose(r[i]["staged_eager"], exp, atol=1e-5, rtol=1e-5), i
+        for it in range(3):
+            e_it = rs + bs + (xb.float() * float(it + 1)).to(torch.bfloat16).float().sum(0)
+            assert torch.allclose(r[i]["staged_graph"][it], e_it, atol=1e-4, rtol=1e-5), (i, it)
