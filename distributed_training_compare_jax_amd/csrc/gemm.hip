@@ -159,6 +159,7 @@ struct Epi {
   float* label_out;
   float* colsum;
   int cs_accum;  // colsum IS the bias gradient: colsum[m] = beta*colsum[m] + sum (split == 1 only)
+  float* sq;     // gemm8p_tile, fp32 store: this tile's sum of squares of the stored values (one float)
   LnEpi ln;
 };
 
@@ -172,7 +173,7 @@ struct Epi {
 #endif
 
 template <int EPI, bool OUTF32>
-__device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4 v) {
+__device__ __forceinline__ float epilogue_store(const Epi& e, int m, int n, f32x4 v) {  // returns sum o^2 of fp32 stores
   DTC_ASSERT(m >= 0 && m < e.M && n >= 0 && n < e.N);
   const bool full = (n + 4 <= e.N);
   float b[4] = {0.f, 0.f, 0.f, 0.f};
@@ -199,8 +200,14 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
   }
   if (OUTF32) {
     float* c = (float*)e.C + (long)m * e.ldc + n;
-    if (full) DTC_OUT_STORE((f32x4*)c, (f32x4{o[0], o[1], o[2], o[3]}));
-    else for (int r = 0; r < 4; ++r) if (n + r < e.N) c[r] = o[r];
+    if (full) {
+      DTC_OUT_STORE((f32x4*)c, (f32x4{o[0], o[1], o[2], o[3]}));
+      return o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3];
+    }
+    float ss = 0.f;
+    for (int r = 0; r < 4; ++r)
+      if (n + r < e.N) { c[r] = o[r]; ss += o[r] * o[r]; }
+    return ss;
   } else {
     bf16* c = (bf16*)e.C + (long)m * e.ldc + n;
     bf16x4 gb;
@@ -222,6 +229,7 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int m, int n, f32x4
       else for (int r = 0; r < 4; ++r) if (n + r < e.N) g[r] = gb[r];
     }
   }
+  return 0.f;
 }
 
 
@@ -1381,14 +1389,27 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
       for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
+  float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       int m = m0 + wr * 128 + j * 16 + (lane & 15);
       int n = n0 + wc * WN + i * 16 + g4;
-      if (m < M && n < N) epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
+      if (m < M && n < N) ss += epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
     }
+  if (OUTF32 && e.sq) {  // grad-norm partial of the tile (fixed order: lanes, then waves 0..7)
+    ss = warp_sum(ss);
+    float* red = (float*)smem;  // free: every wave is past the main loop's last barrier
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT2 / 64; ++w) t += red[w];
+      *e.sq = t;
+    }
+  }
 }
 
 template <bool AK, bool BKM, int EPI, bool OUTF32, int CB = 4>
@@ -1424,6 +1445,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
   Epi e{};
   e.M = w.M; e.N = w.N; e.C = w.C; e.ldc = w.N; e.alpha = 1.f; e.beta = b.beta;
   e.colsum = w.cs; e.cs_accum = 1;
+  e.sq = b.sq ? b.sq + lid : nullptr;
   gemm8p_tile<false, false, EPI_STORE, true, 4>(w.A, w.M, w.B, w.N, w.M, w.N, b.K, tm_idx, tn_idx, 0, 1, b.K,
                                                  nullptr, e);
 }

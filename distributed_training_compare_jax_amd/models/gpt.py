@@ -188,6 +188,12 @@ class GPTStage:
         # launch of whole 256^2 tiles (ops/gemm.py wgrad_group) -- single-stream backward only
         self.wg_group = -1  # -1 = off
         self.wg_queue = []
+        # grad-norm partials from the grouped launch (engine: dp == 1 and one launch per step): the first
+        # flush records its problems (wg_seen), the engine then hands back the partial slots (wg_sq)
+        self.wg_record = False
+        self.wg_seen = None
+        self.wg_sq: Optional[torch.Tensor] = None
+        self._wg_keys = None
         # LayerNorm fused into the layer GEMMs (ops/ln_fused.py), set up by enable_ln_fusion
         self.ln_sync: Optional[LF.LnSync] = None
         self._fuse_fwd = self._fuse_bwd = False
@@ -216,7 +222,21 @@ class GPTStage:
         """Launch every queued weight gradient (one grouped launch), then the reducer's batched launch."""
         if self.wg_queue:
             q, self.wg_queue = self.wg_queue, []
-            G.wgrad_group(q, beta, red=self.red)
+            if self.wg_record and self.wg_seen is None:
+                self.wg_seen = [(dw, dy.shape[1], x.shape[1]) for dy, x, dw, _ in q]
+            sq = None
+            if self.wg_sq is not None:
+                keys = sorted(dw.data_ptr() for _, _, dw, _ in q)
+                if keys != self._wg_keys:
+                    raise RuntimeError("grouped weight gradients: the problems differ from the ones whose grad-norm "
+                                       "partials were registered (one grouped launch per step expected)")
+                sq = self.wg_sq
+            G.wgrad_group(q, beta, red=self.red, sq=sq)
+
+    def use_wgrad_sumsq(self, sq: torch.Tensor):
+        """From now on the grouped launch writes its tiles' Σ dW² into ``sq`` (FusedAdamW.set_fused_sumsq)."""
+        self.wg_sq = sq
+        self._wg_keys = sorted(dw.data_ptr() for dw, _, _ in self.wg_seen)
 
     def enable_ln_fusion(self, tokens: int, step: torch.Tensor, fwd: bool, bwd: bool) -> bool:
         """Fuse the LayerNorms into the GEMMs that produce their input (forward) and their output

@@ -88,7 +88,8 @@ WG_MAX = 64  # csrc/common.h WG_MAX
 
 
 class WgBatch(ctypes.Structure):
-    _fields_ = [("n", c_int), ("K", c_int), ("beta", c_float), ("ntiles", c_int), ("e", WgEntry * WG_MAX)]
+    _fields_ = [("n", c_int), ("K", c_int), ("beta", c_float), ("ntiles", c_int), ("sq", c_vp),
+                ("e", WgEntry * WG_MAX)]
 
 
 EPI_STORE = 0       # C = alpha*acc (+bias) (+beta*C if fp32)

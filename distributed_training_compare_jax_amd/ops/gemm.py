@@ -320,14 +320,23 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
 _WG_CHECKED = [False]
 
 
-def wgrad_group(items, beta: float = 0.0, red=None):
+def wgrad_tiles(m: int, n: int) -> int:
+    """256² tiles of one grouped weight-gradient problem dW[m, n] (its grad-norm partial slots)."""
+    return ((m + 255) // 256) * ((n + 255) // 256)
+
+
+def wgrad_group(items, beta: float = 0.0, red=None, sq: Optional[torch.Tensor] = None):
     """Weight gradients of several Dense layers that share the token dimension, in ONE launch:
     for every ``(dy, x, dw, db)``: dW = β·dW + dYᵀ·X and (``db`` not None) db = β·db + Σ_rows dY.
 
     GPU bf16: ``gemm8p_group_kernel`` (csrc/gemm.hip) runs whole 256² tiles of every problem — no
     split-K slabs and no reduction pass, the bias gradients summed by the tiles' MFMAs.  Problems it
     cannot take (fp32 operands, a width not a multiple of 8, tokens not a multiple of 64) go through
-    :func:`wgrad` one by one (``red``: its batched reducer), as do CPU tensors."""
+    :func:`wgrad` one by one (``red``: its batched reducer), as do CPU tensors.
+
+    ``sq`` (fp32, >= Σ :func:`wgrad_tiles` slots): every tile also writes the sum of squares of its final
+    dW values there (the global grad norm's partials, so the norm pass skips these grads); then every
+    item must take the grouped kernel."""
     if not items:
         return
     dy0 = items[0][0]
@@ -342,6 +351,9 @@ def wgrad_group(items, beta: float = 0.0, red=None):
                 and tuple(dw.shape) == (dy.shape[1], x.shape[1]) and dw.data_ptr() % 16 == 0
                 and (db is None or (db.is_contiguous() and db.dtype == torch.float32)))
         (fast if good else slow).append(it)
+    if sq is not None and slow:
+        raise ValueError("wgrad_group(sq=...): every problem must take the grouped kernel "
+                         f"({len(slow)} of {len(items)} cannot)")
     for dy, x, dw, db in slow:
         wgrad(dy, x, dw, beta, red=red, db=db)
     if not fast:
@@ -352,12 +364,18 @@ def wgrad_group(items, beta: float = 0.0, red=None):
         _WG_CHECKED[0] = True
     # largest problems first: their tiles start in the first rounds, the small ones fill the tail
     fast.sort(key=lambda it: -(it[0].shape[1] * it[1].shape[1]))
+    if sq is not None:
+        assert sq.dtype == torch.float32 and sq.is_contiguous() and sq.is_cuda
+        assert sq.numel() >= sum(wgrad_tiles(it[0].shape[1], it[1].shape[1]) for it in fast), "sq too small"
+    off = 0
     for i0 in range(0, len(fast), N.WG_MAX):
         chunk = fast[i0:i0 + N.WG_MAX]
         b = N.WgBatch()
         b.n, b.K, b.beta, b.ntiles = len(chunk), K, float(beta), 0
+        b.sq = None if sq is None else sq.data_ptr() + 4 * off
         for j, (dy, x, dw, db) in enumerate(chunk):
             b.e[j] = N.WgEntry(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N.ptr(db), dy.shape[1], x.shape[1], 0, 0)
+            off += wgrad_tiles(dy.shape[1], x.shape[1])
         N.check(L.dtc_wgrad_group(ctypes.byref(b), N.stream_ptr(dy0.device)), "dtc_wgrad_group")
 
 

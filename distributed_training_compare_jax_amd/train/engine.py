@@ -156,6 +156,10 @@ class Engine:
                 bk = self.buckets
                 cuts = [bk.head_end_offset()] + [bk.layer_end_offset(l) for l in reversed(self.layout.layers)]
                 self.opt.set_chunks(sorted(set(c for c in cuts if 0 < c < self.flat.numel)) + [self.flat.numel])
+                # the grouped weight-gradient launch also emits its tiles' Σ dW² (the final grads at
+                # dp == 1), so the norm pass skips ~3/4 of the grads (DTC_FUSED_NORM=0: off)
+                self.stage.wg_record = (on_gpu and self.stage.wg_group == 0 and self.act_dtype == torch.bfloat16
+                                        and os.environ.get("DTC_FUSED_NORM", "1") == "1")
             elif self.embed_gather:
                 self.opt.set_chunks([self.buckets.reduce_end, self.flat.numel])
 
@@ -517,6 +521,14 @@ class Engine:
         if check and p.sigs is not None:
             p.verify("first step")
         self.steps_done += 1
+        st = self.stage
+        if st.wg_record and st.wg_sq is None and st.wg_seen is not None:  # after the first (eager) step
+            ranges, tiles = [], 0
+            base = self.flat.grads.data_ptr()
+            for dw, m, n in st.wg_seen:
+                ranges.append(((dw.data_ptr() - base) // 4, dw.numel()))
+                tiles += G.wgrad_tiles(m, n)
+            st.use_wgrad_sumsq(self.opt.set_fused_sumsq(ranges, tiles))
         return self.loss
 
     def loss_value(self) -> float:

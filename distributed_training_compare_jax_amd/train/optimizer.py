@@ -39,6 +39,26 @@ def merge_segments(segs, total: int):
     return out
 
 
+def _subtract_ranges(segs, ranges):
+    """``segs`` [(offset, n, weight)] minus the flat ranges [(offset, n)] (sorted, disjoint)."""
+    out = []
+    for (o, n, w) in segs:
+        cur = o
+        end = o + n
+        for (ro, rn) in ranges:
+            re_ = ro + rn
+            if re_ <= cur or ro >= end:
+                continue
+            if ro > cur:
+                out.append((cur, ro - cur, w))
+            cur = max(cur, re_)
+            if cur >= end:
+                break
+        if cur < end:
+            out.append((cur, end - cur, w))
+    return out
+
+
 class FusedAdamW:
     def __init__(self, flat: FlatParams, cfg: OptimConfig, program, tp_size: int = 1, tp_group=None,
                  pp_group=None, pp_global_clip: bool = False):
@@ -57,6 +77,9 @@ class FusedAdamW:
         self._done = []
         self.reducer = None  # GradReducer of the model stage (single-stream GPU backward)
         self.tp_comm = None  # parallel.tp.TPComm: the TP norm partial through its P2P path when it has one
+        self._fused = ([], 0)  # flat ranges whose Σg² arrives precomputed (set_fused_sumsq), slot count
+        self._cuts = None
+        self.fused_part = None
 
     # -- incremental global norm ------------------------------------------------------
     def set_chunks(self, cuts, elems_per_block: int = 16384):
@@ -66,17 +89,23 @@ class FusedAdamW:
         fixed-order finish remain between backward and the AdamW pass."""
         f = self.flat
         assert cuts and cuts[-1] == f.numel and all(c % 4 == 0 for c in cuts)
+        self._cuts = list(cuts)
+        fused, nfused = self._fused
         specs, lo = [], 0
         for hi in cuts:
             segs = [(max(o, lo), min(o + n, hi) - max(o, lo), wt) for (o, n, wt) in self._merged
                     if o < hi and o + n > lo]
+            segs = _subtract_ranges(segs, fused)
             # partial slots per segment (a batched-reducer task each; one block per ~16K elements so
             # no block of the batched launch streams more than 64 KB), >= 8 per chunk in total
             nbs = [max(1, (n + elems_per_block - 1) // elems_per_block) for (_, n, _) in segs]
-            nbs[-1] += max(0, 8 - sum(nbs))
+            if nbs:
+                nbs[-1] += max(0, 8 - sum(nbs))
             specs.append((segs, lo, hi, nbs))
             lo = hi
-        self.part = torch.zeros(sum(sum(s[3]) for s in specs), dtype=torch.float32, device=f.device)
+        nchunk = sum(sum(s[3]) for s in specs)
+        self.part = torch.zeros(nchunk + nfused, dtype=torch.float32, device=f.device)
+        self.fused_part = self.part[nchunk:] if nfused else None
         self.chunks, off = [], 0
         for segs, lo, hi, nbs in specs:
             nb = sum(nbs)
@@ -85,9 +114,25 @@ class FusedAdamW:
             for (o, n, w), k in zip(segs, nbs):
                 tasks.append((o, n, w, part[o2:o2 + k]))
                 o2 += k
-            self.chunks.append((O.make_segments(segs, f.device), lo, hi, part, tasks))
+            self.chunks.append((O.make_segments(segs, f.device) if segs else None, lo, hi, part, tasks))
             off += nb
         self._done = [False] * len(self.chunks)
+
+    def set_fused_sumsq(self, ranges, nslots: int) -> torch.Tensor:
+        """The Σg² of the flat ranges ``[(offset, n), ...]`` arrives as ``nslots`` per-tile partials written
+        by the grouped weight-gradient epilogue (``ops.gemm.wgrad_group(sq=...)``): the norm chunks skip
+        those ranges and the finish sums the partials after theirs (one fixed order).  Returns the partial
+        buffer (a view of the norm's partial array) for the writer.  Call after :meth:`set_chunks`, only
+        for grads that are final where they are written (dp == 1) and whose norm weight is 1."""
+        assert self._cuts is not None, "set_fused_sumsq needs the incremental-norm chunks"
+        ranges = sorted((int(o), int(n)) for o, n in ranges)
+        for o, n in ranges:
+            for (so, sn, wt) in self._merged:
+                if so < o + n and so + sn > o and wt != 1.0:
+                    raise ValueError(f"fused Σg² range at {o} overlaps a weight-{wt} segment")
+        self._fused = (ranges, int(nslots))
+        self.set_chunks(self._cuts)
+        return self.fused_part
 
     def chunk_ready(self, i: int, runner=None):
         """Σg² partials of chunk i (its grads must be final).  ``runner``: a ``GradReducer``
@@ -95,6 +140,9 @@ class FusedAdamW:
         if self._done[i]:
             return
         segs, _, _, part, tasks = self.chunks[i]
+        if segs is None:  # every grad of the chunk is covered by the fused partials
+            self._done[i] = True
+            return
         g = self.flat.grads
         if isinstance(runner, GradReducer):
             for o, n, w, pt in tasks:

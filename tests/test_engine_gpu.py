@@ -167,6 +167,32 @@ def test_deferred_optimizer_matches_immediate(cuda, monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_fused_grad_norm_matches(cuda, monkeypatch):
+    """The grouped weight-gradient launch's per-tile Σ dW² (switched on after the first, eager step)
+    replaces ~3/4 of the norm pass: the clipped updates and the grad norm match the unfused run to fp32
+    summation order, step by step (graph-replayed steps included)."""
+    runs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DTC_FUSED_NORM", fused)
+        eng, mc = _engine(cuda, use_graph=True, preset="ref", vocab=50258, batch=8)
+        it = get_batch_iterator(8, mc.max_seq_len + 1)
+        out = []
+        for _ in range(5):
+            eng.set_batch(next(it))
+            eng.run_step()
+            out.append((eng.loss_value(), eng.opt.grad_norm()))
+        assert (eng.stage.wg_sq is not None) == (fused == "1")
+        if fused == "1":  # the engine's norm of the last step = the norm of the grads it left behind
+            g = eng.flat.grads.double().norm().item()
+            assert out[-1][1] == pytest.approx(g, rel=1e-5)
+        runs[fused] = (out, eng.flat.params.clone())
+        del eng
+    for (l1, n1), (l0, n0) in zip(runs["1"][0], runs["0"][0]):
+        assert l1 == pytest.approx(l0, rel=1e-5) and n1 == pytest.approx(n0, rel=1e-5)
+    d = (runs["1"][1] - runs["0"][1]).abs().max().item()
+    assert d < 1e-5, d
+
+
 def test_fp32_mode_matches_oracle(cuda):
     """dtype: fp32 on the GPU (the reference's precision): every GEMM, the attention and the CE on our
     exact-fp32 MFMA kernels (csrc/gemm_f32.hip, csrc/attention_f32.hip) + the HIP LayerNorm / embedding /
