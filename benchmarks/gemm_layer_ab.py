@@ -5,10 +5,11 @@ against an fp32 torch reference.
 
     python benchmarks/gemm_layer_ab.py [--model gpt2-small] [--rounds 5] [--reps 30]
 
-Variants (dtc_gemm_set_4w): ``default`` (the shipped plan, DTC_GEMM4W as set at load), ``4w``
-(gemm4w_kernel on every covered problem) and ``4p`` (gemm4p_kernel, one pipelined block per CU).
-``--cold``: every call follows a 512 MB buffer write, so its operands come from HBM as in the step (the
-warm numbers ranked gemm4w ahead; the step disagreed, profiles/r4_ab_step_knobs.log).
+``--cold``: every call follows a 512 MB buffer write, so its operands come from HBM as in the step.  The
+warm (default) mode misranked a candidate kernel in round 4 (gemm4w: ahead warm, profiles/r4_gemm4w_ab.log;
+behind cold and in the step, profiles/r4_gemm_cold_ab.log / r4_ab_step_knobs.log): rank candidates cold.
+To A/B a kernel variant, build it into another library (scripts/build_variant.py) and run this script
+under DTC_KERNEL_LIB for each.
 """
 import argparse
 import os
@@ -17,7 +18,6 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from distributed_training_compare_jax_amd.ops import _native as NV  # noqa: E402
 from distributed_training_compare_jax_amd.ops import gemm as G  # noqa: E402
 
 
@@ -64,7 +64,6 @@ def main():
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
     r = lambda *s, sc=0.5: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)  # noqa: E731
-    L = NV.lib()
     cases = []
     pre = None
     if a.cold:
@@ -100,12 +99,10 @@ def main():
             add(f"ntdgrad {tag} [{M}x{k}x{n}] f32", fl, lambda dy=dy, wt=wt: G.linear(dy, wt, out_dtype=torch.float32),
                 lambda dy=dy, w=w: dy.float() @ w.float(), lambda dy=dy, w=w: dy @ w)
 
-    old = L.dtc_gemm_set_4w(0)
-    variants = {"default": old, "4w": 2, "4p": 4}
+    variants = {"ours": None}
     for name, _, fn, ref, _ in cases:
         want = ref().float()
         for vn, v in variants.items():
-            L.dtc_gemm_set_4w(v)
             got = fn().float()
             err = ((got - want).norm() / want.norm()).item()
             print(f"check {name:36s} {vn:8s} rel err {err:.2e}", flush=True)
@@ -114,10 +111,8 @@ def main():
     for _ in range(a.rounds):
         for name, _, fn, _, blas in cases:
             for vn, v in variants.items():
-                L.dtc_gemm_set_4w(v)
                 res[(name, vn)].append(graph_time(fn, a.reps, pre))
             res[(name, "hipBLASLt")].append(graph_time(blas, a.reps, pre))
-    L.dtc_gemm_set_4w(old)
     for name, fl, *_ in cases:
         row = []
         for vn in list(variants) + ["hipBLASLt"]:

@@ -1451,201 +1451,6 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
 }
 
 // ============================================================================================
-// gemm4w: the layer GEMMs of a block at M = tokens in the NT layout (both operands K-major: the
-// forwards, and the dgrads on the transposed weights).  Tile 128 x 64*CB, 4 waves (2 x 2, 64 x 32*CB
-// per wave, 16x16x32 MFMAs), BK = 64, two LDS stages of p8 chunk images ((2 + CB) x 8 KB each) filled
-// by LDS-DMA, TWO blocks per CU.  Why: these GEMMs have short K (768-3072) and N = 768-3072, so 256^2
-// tiles leave CUs idle (96 tiles at N = 768) and one block per CU exposes every tile's prologue (an HBM
-// burst) and epilogue.  At CB = 3 the tile counts are 256 / 768 / 1024 for N = 768 / 2304 / 3072 (whole
-// rounds of 256 CUs) and each CU's second block runs its MFMAs under the other one's prologue and
-// epilogue.  64 x 96 per wave reads 10 KB of fragments per 24 MFMAs (gemm8n's 64 x 48: 7 KB per 12).
-// Pipeline per K-step t: wait for this thread's DMAs of stage t (vmcnt 0: issued one K-step earlier),
-// barrier (every thread's stage t landed, every wave done reading stage t-1), issue stage t+1 into the
-// buffer stage t-1 used, MFMAs on stage t, drain the LDS reads (lgkmcnt 0) so the next barrier also
-// retires them.  Requires M % 128 == 0, N % (64 CB) == 0, K % 64 == 0 (host-checked).
-template <int CB, int EPI, bool OUTF32>
-__global__ void __launch_bounds__(256, 2)
-gemm4w_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
-              int tiles_m, int tiles_n, int gm, Epi e) {
-  constexpr int TM = 4, TN = 2 * CB;        // 16x16 fragments per wave: 64 (m) x 32*CB (n)
-  constexpr int STG = (2 + CB) * P8_CHUNK;  // elements per stage: A chunks 0-1, B chunks 0..CB-1
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STG];  // the only LDS object
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int ntiles = tiles_m * tiles_n;
-  const int lid = xcd_remap(blockIdx.x, ntiles);
-  const int grp = lid / (gm * tiles_n), in_g = lid % (gm * tiles_n);
-  const int gm_eff = min(gm, tiles_m - grp * gm);
-  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
-  const int m0 = tm_idx * 128, n0 = tn_idx * (64 * CB);
-  DTC_ASSERT(m0 + 128 <= M && n0 + 64 * CB <= N && K % 64 == 0 && K >= 64);
-  const int nk = K / 64;
-  // DMA: a wave instruction moves 8 image rows x 128 B; this lane's row r8 (+32 h, +64 q) and its
-  // 16-B k-piece, swizzled on the source so the image holds piece c of row r at c ^ ((r >> 1) & 7)
-  const int r8 = wave * 8 + (lane >> 3);
-  const int cpos = ((lane & 7) ^ ((r8 >> 1) & 7)) * 8;
-  const bf16* pa = A + (long)(m0 + r8) * lda + cpos;
-  const bf16* pb = B + (long)(n0 + r8) * ldb + cpos;
-  auto stage = [&](int s, int k0) {
-    bf16* img = smem + s * STG;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        __builtin_amdgcn_global_load_lds((glb_vptr)(pa + (long)(64 * q + 32 * h) * lda + k0),
-                                         (lds_vptr)(img + q * P8_CHUNK + (wave + 4 * h) * 512), 16, 0, 0);
-#pragma unroll
-    for (int q = 0; q < CB; ++q)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        __builtin_amdgcn_global_load_lds((glb_vptr)(pb + (long)(64 * q + 32 * h) * ldb + k0),
-                                         (lds_vptr)(img + (2 + q) * P8_CHUNK + (wave + 4 * h) * 512), 16, 0, 0);
-  };
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  stage(0, 0);
-  for (int t = 0; t < nk; ++t) {
-    P8_VMCNT(0);
-    __builtin_amdgcn_s_barrier();
-    if (t + 1 < nk) stage((t + 1) & 1, (t + 1) * 64);
-    const bf16* sA = smem + (t & 1) * STG;
-    const bf16* sB = sA + 2 * P8_CHUNK;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 fa[TM], fb[TN];
-#pragma unroll
-      for (int j = 0; j < TM; ++j) fa[j] = big_frag<true>(sA, 4 * wr + j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TN; ++i) fb[i] = big_frag<true>(sB, TN * wc + i, kk, lane);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-  const int g4 = 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j)
-      epilogue_store<EPI, OUTF32>(e, m0 + 64 * wr + 16 * j + (lane & 15), n0 + 32 * CB * wc + 16 * i + g4, acc[i][j]);
-}
-
-// gemm4p: the same tile, waves and images as gemm4w, software-pipelined for ONE block (one wave per
-// SIMD) per CU and a deeper DMA ring (experiment, DTC_GEMM4W=4).
-//  * 4 LDS stages (160 KB): stage t+3 is issued right after the barrier of K-step t (into the buffer of
-//    stage t-1), so a stage has two K-steps to land; the wait before that barrier is counted (vmcnt 10 =
-//    one stage of this thread's DMAs left in flight).
-//  * fragments in two register sets: the second half (k 32-63) of stage t is read while the MFMAs of the
-//    first half run, and the first half of stage t+1 while the second half's run (LDS returns in order:
-//    the compiler's counted lgkmcnt waits for each set only).
-//  * built as it is, hipcc puts the accumulators in AGPRs and copies all 96 of them every K-step; with
-//    -mllvm -amdgpu-mfma-vgpr-form (scripts/build_variant.py) the loop is clean.
-template <int CB, int EPI, bool OUTF32>
-__global__ void __launch_bounds__(256, 2)
-gemm4p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
-              int tiles_m, int tiles_n, int gm, Epi e) {
-  constexpr int TM = 4, TN = 2 * CB, NS = 4;
-  constexpr int STG = (2 + CB) * P8_CHUNK;
-  static_assert(NS * STG * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STG];  // the only LDS object
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int ntiles = tiles_m * tiles_n;
-  const int lid = xcd_remap(blockIdx.x, ntiles);
-  const int grp = lid / (gm * tiles_n), in_g = lid % (gm * tiles_n);
-  const int gm_eff = min(gm, tiles_m - grp * gm);
-  const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
-  const int m0 = tm_idx * 128, n0 = tn_idx * (64 * CB);
-  DTC_ASSERT(m0 + 128 <= M && n0 + 64 * CB <= N && K % 64 == 0 && K >= 64);
-  const int nk = K / 64;
-  const int r8 = wave * 8 + (lane >> 3);
-  const int cpos = ((lane & 7) ^ ((r8 >> 1) & 7)) * 8;
-  const bf16* pa = A + (long)(m0 + r8) * lda + cpos;
-  const bf16* pb = B + (long)(n0 + r8) * ldb + cpos;
-  auto stage = [&](int t) {  // 2 (2 + CB) = 10 DMA instructions per thread
-    bf16* img = smem + (t % NS) * STG;
-    const int k0 = t * 64;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        __builtin_amdgcn_global_load_lds((glb_vptr)(pa + (long)(64 * q + 32 * h) * lda + k0),
-                                         (lds_vptr)(img + q * P8_CHUNK + (wave + 4 * h) * 512), 16, 0, 0);
-#pragma unroll
-    for (int q = 0; q < CB; ++q)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        __builtin_amdgcn_global_load_lds((glb_vptr)(pb + (long)(64 * q + 32 * h) * ldb + k0),
-                                         (lds_vptr)(img + (2 + q) * P8_CHUNK + (wave + 4 * h) * 512), 16, 0, 0);
-  };
-  auto rd = [&](int t, int kk, bf16x8 (&fa)[TM], bf16x8 (&fb)[TN]) {
-    const bf16* sA = smem + (t % NS) * STG;
-    const bf16* sB = sA + 2 * P8_CHUNK;
-#pragma unroll
-    for (int j = 0; j < TM; ++j) fa[j] = big_frag<true>(sA, 4 * wr + j, kk, lane);
-#pragma unroll
-    for (int i = 0; i < TN; ++i) fb[i] = big_frag<true>(sB, TN * wc + i, kk, lane);
-  };
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mm = [&](const bf16x8 (&fa)[TM], const bf16x8 (&fb)[TN]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  stage(0);
-  if (nk > 1) stage(1);
-  if (nk > 2) stage(2);
-  if (nk > 2) vmcnt_c<20>(); else if (nk > 1) vmcnt_c<10>(); else P8_VMCNT(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-  rd(0, 0, fa0, fb0);
-  for (int t = 0; t + 1 < nk; ++t) {  // the last K-step is peeled: no branch around the accumulators
-    rd(t, 1, fa1, fb1);
-    mm(fa0, fb0);
-    if (t + 2 < nk) vmcnt_c<10>(); else P8_VMCNT(0);  // stage t+1 landed (stage t+2 may stay in flight)
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 3 < nk) stage(t + 3);  // into the buffer of stage t-1: every wave finished reading it
-    rd(t + 1, 0, fa0, fb0);
-    mm(fa1, fb1);
-  }
-  rd(nk - 1, 1, fa1, fb1);
-  mm(fa0, fb0);
-  mm(fa1, fb1);
-  const int g4 = 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j)
-      epilogue_store<EPI, OUTF32>(e, m0 + 64 * wr + 16 * j + (lane & 15), n0 + 32 * CB * wc + 16 * i + g4, acc[i][j]);
-}
-
-// ============================================================================================
 // 128 x (64*CB) tile, 8 waves (2 along M x 4 along N, 64 x 16*CB per wave), NS-stage LDS-DMA ring,
 // phase-interleaved like gemm8p_kernel -- for the layer GEMMs.  Their shapes quantise badly on
 // 128^2 / 256^2 tiles (GPT-2 small: M = 8192 tokens, N = 768 / 2304 / 3072 = 4 / 12 / 16 x 192;
@@ -2829,54 +2634,6 @@ int launch_n8_any(const GemmArgs& a, int cb, hipStream_t st) {
   return -1;
 }
 
-// ---- gemm4w plans (layer GEMMs in the NT layout, 128 x 192 tiles, two blocks per CU) ------------------
-// Isolated (L2-warm, back-to-back graph replays; profiles/r4_gemm4w_ab.log) gemm4w beat the shipped
-// plans on the bf16 / fp32 stores and the GELU forward (qkv fwd 45.1 -> 42.1 us, fc1 fwd 71.0 -> 69.7,
-// NT dgrads -0.2..-1.4 us) and tied hipBLASLt on the plain NT dgrads, but in the step every gemm4w
-// launch ran ~25 % slower than in isolation (qkv fwd 53, fc1 fwd 92, fc2 fwd 68 us; rocprofv3,
-// profiles/r4_gemm4w_instep.md) and the whole step lost 0.63 ms (12.07 vs 11.44 ms, 3 interleaved
-// rounds, profiles/r4_ab_step_knobs.log): its two-stage ring cannot hide the cold (HBM) operand
-// fetches the step sees.  So it is off by default.
-// DTC_GEMM4W: 0 = off (default), 1 = that plan, 2 = every covered problem, 4 = every covered problem on the
-// one-block-per-CU pipelined variant gemm4p_kernel (tests / A/B).
-// Covered: layout 0, M % 128, N % 192, K % 64, alpha 1, beta 0.
-static int g_4w = [] { const char* v = getenv("DTC_GEMM4W"); return v ? atoi(v) : 0; }();
-
-template <int EPI, bool OUTF32>
-int launch_4w(const GemmArgs& a, hipStream_t st) {
-  constexpr int CB = 3;
-  Epi e{};
-  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
-  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
-  const int tiles_m = a.M / 128, tiles_n = a.N / (64 * CB), ntiles = tiles_m * tiles_n;
-  // an XCD's share of the tiles is one group: gm M-tiles x every N-tile (A panels and B shared in its L2)
-  const int gm = std::max(1, std::min({tiles_m, 8, ntiles / 8 / tiles_n}));
-  if (g_4w == 4)
-    hipLaunchKernelGGL((gemm4p_kernel<CB, EPI, OUTF32>), dim3(ntiles), dim3(256), 0, st, (const bf16*)a.A, a.lda,
-                       (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, e);
-  else
-    hipLaunchKernelGGL((gemm4w_kernel<CB, EPI, OUTF32>), dim3(ntiles), dim3(256), 0, st, (const bf16*)a.A, a.lda,
-                       (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, e);
-  DTC_CHECK_LAUNCH();
-  return 0;
-}
-
-// -1 = not taken (shape, layout, epilogue, plan or switched off)
-int launch_4w_any(const GemmArgs& a, hipStream_t st) {
-  if (!g_4w || a.layout != 0 || a.M % 128 || a.N % 192 || a.K % 64 || a.K > 4096 || a.colsum || a.alpha != 1.f ||
-      a.beta != 0.f)
-    return -1;  // (K > 4096: the lm_head dgrad through the vocabulary keeps its split-K 256^2 plan)
-  if (g_4w == 1 && (a.epi == EPI_DGELU || (a.epi == EPI_RESID && a.K < 1024))) return -1;
-  const bool f32 = a.c_f32 != 0;
-  switch (a.epi) {
-    case EPI_STORE: return f32 ? launch_4w<EPI_STORE, true>(a, st) : launch_4w<EPI_STORE, false>(a, st);
-    case EPI_RESID: return f32 ? launch_4w<EPI_RESID, true>(a, st) : -1;
-    case EPI_GELU: return f32 ? -1 : launch_4w<EPI_GELU, false>(a, st);
-    case EPI_DGELU: return f32 ? -1 : launch_4w<EPI_DGELU, false>(a, st);
-    default: return -1;
-  }
-}
-
 // Paired launch: a1 = dgrad (layout 1, whole-K tiles), a2 = weight gradient (layout 2, split-K slabs
 // left for the caller's batched reducer when split > 1).  Only register-staged, BK = 64 plans pair.
 template <class C1, class C2, int BM1, int BM2, bool BKM1 = false>
@@ -3156,13 +2913,6 @@ int dtc_gemm_set_n8(int mask) {
   return old;
 }
 
-// gemm4w plan (DTC_GEMM4W at load time: 0 off, 1 measured plan, 2 every covered problem); returns the previous value
-int dtc_gemm_set_4w(int on) {
-  const int old = g_4w;
-  g_4w = on;
-  return old;
-}
-
 int dtc_wg_entry_bytes() { return (int)sizeof(WgEntry); }
 int dtc_wg_max() { return WG_MAX; }
 
@@ -3191,7 +2941,6 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
-  if (const int r = launch_4w_any(*a, st); r >= 0) return r;
   if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f) {
     const int cb = n8_cb(a->layout, a->M, a->N, a->K, epi);
     if (cb) {

@@ -12,8 +12,11 @@ namespace {
 
 // RPW rows per wave, every row's loads issued before the first reduction (as the backward): with one
 // row per wave a wave had 3 x 16 B in flight per lane and the kernel ran at ~4 TB/s
+// resid (optional): the row is x + resid (the residual add of the producing layer, moved here from its
+// GEMM epilogue), written to x_out (may alias x) before it is normalised.
 template <int NV, int RPW>
-__global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const float* x, const float* __restrict__ resid, float* x_out,
+                                                     const float* __restrict__ g,
                                                      const float* __restrict__ b, void* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int M, int D, float eps, int out_f32) {
@@ -32,6 +35,14 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
     for (int i = 0; i < NV; ++i) {
       int c = lane + 64 * i;
       v[q][i] = c < D4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (resid) {
+      const f32x4* rr = (const f32x4*)(resid + (long)min(row, M - 1) * D);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        int c = lane + 64 * i;
+        if (c < D4) v[q][i] += rr[c];
+      }
     }
   }
 #pragma unroll
@@ -59,6 +70,13 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
     const float rstd = rsqrtf(warp_sum(qs) / D + eps);
     if (row >= M) continue;
     if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+    if (x_out) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        int c = lane + 64 * i;
+        if (c < D4) ((f32x4*)(x_out + (long)row * D))[c] = v[q][i];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       int c = lane + 64 * i;
@@ -328,21 +346,28 @@ __global__ void __launch_bounds__(256) reduce_tasks_kernel(RedBatch batch) {
 
 extern "C" {
 
-int dtc_layernorm_fwd(const float* x, const float* g, const float* b, void* y, float* mean, float* rstd, int M, int D,
-                      float eps, int out_f32, hipStream_t st) {
+int dtc_add_layernorm_fwd(const float* x, const float* resid, float* x_out, const float* g, const float* b, void* y,
+                          float* mean, float* rstd, int M, int D, float eps, int out_f32, hipStream_t st) {
   if (D % 4) return 2002;
   int nv = (D / 4 + 63) / 64;
   // DTC_LN_FWD_RPW: rows per wave (1 or 2)
   static const int rpw = [] { const char* v = getenv("DTC_LN_FWD_RPW"); return v ? atoi(v) : 1; }();
   if (rpw == 2) {
     dim3 grid((M + 7) / 8);
-    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 2>), grid, dim3(256), 0, st, x, g, b, y, mean, rstd, M, D, eps, out_f32));
+    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 2>), grid, dim3(256), 0, st, x, resid, x_out, g, b, y, mean,
+                                         rstd, M, D, eps, out_f32));
   } else {
     dim3 grid((M + 3) / 4);
-    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 1>), grid, dim3(256), 0, st, x, g, b, y, mean, rstd, M, D, eps, out_f32));
+    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 1>), grid, dim3(256), 0, st, x, resid, x_out, g, b, y, mean,
+                                         rstd, M, D, eps, out_f32));
   }
   DTC_CHECK_LAUNCH();
   return 0;
+}
+
+int dtc_layernorm_fwd(const float* x, const float* g, const float* b, void* y, float* mean, float* rstd, int M, int D,
+                      float eps, int out_f32, hipStream_t st) {
+  return dtc_add_layernorm_fwd(x, nullptr, nullptr, g, b, y, mean, rstd, M, D, eps, out_f32, st);
 }
 
 long dtc_layernorm_bwd_workspace_bytes(int M, int D) {

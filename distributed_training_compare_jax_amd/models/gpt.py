@@ -64,6 +64,9 @@ def _ce_fused(tokens: int, d: int) -> bool:
 # columns vs 824 MB) held from the forward to the backward -- for memory-bound configurations
 # (SURVEY K10 "never materialize full logits"); it costs one extra lm_head GEMM (the recompute).
 _CE_CHUNK = int(_os.environ.get("DTC_CE_CHUNK", "0"))
+# residual adds of out_proj / fc2 done by the LayerNorm pass that follows (tp == 1): the GEMM epilogue
+# stores a·Wᵀ + b without reading the fp32 residual (DTC_ADD_LN=0: the fused residual epilogue)
+_ADD_LN = _os.environ.get("DTC_ADD_LN", "1") == "1"
 if _CE_CHUNK < 0 or _CE_CHUNK % 256:
     # chunk offsets feed 16-byte vector loads of w[c0:], wt[:, c0:] and gw[c0:]: a ragged offset would
     # surface as an opaque native error deep in the backward
@@ -324,6 +327,12 @@ class GPTStage:
         elif self.tp_bf16:
             x2 = self._row_parallel(o, p + "out.w", resid=x, bias=f.p(p + "out.b"))
             y2, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
+        elif tp.size == 1 and _ADD_LN:
+            # residual add in the LayerNorm pass (the GEMM stores o·Wᵀ + b; its epilogue skips the fp32
+            # residual read) -- same fp32 arithmetic, (acc + b) + x
+            x2, (y2, mu2, rs2) = LN.add_layernorm_fwd(G.linear(o, f.w(p + "out.w"), f.p(p + "out.b"),
+                                                               out_dtype=torch.float32), x,
+                                                      f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
         else:
             x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
             tp.all_reduce_(x2)
@@ -334,6 +343,11 @@ class GPTStage:
         if self._fuse_fwd and nxt is not None:
             x3, pre_next = LF.linear_resid_ln(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b"), x2, f.p(nxt + ".g"),
                                               f.p(nxt + ".b"), self.eps, self.ln_sync, self._ln_site(l, 1, False))
+            ctx[("ln1", l + 1) if nxt != "lnf" else "lnf_pre"] = pre_next
+        elif tp.size == 1 and _ADD_LN and nxt is not None and not self.tp_bf16:
+            x3, pre_next = LN.add_layernorm_fwd(G.linear(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b"),
+                                                         out_dtype=torch.float32), x2,
+                                                f.p(nxt + ".g"), f.p(nxt + ".b"), self.eps, self.act_dtype)
             ctx[("ln1", l + 1) if nxt != "lnf" else "lnf_pre"] = pre_next
         elif self.tp_bf16:
             x3 = self._row_parallel(gact, p + "fc2.w", resid=x2, bias=f.p(p + "fc2.b"))

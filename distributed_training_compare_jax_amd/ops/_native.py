@@ -107,12 +107,12 @@ def _declare(lib):
         "dtc_gemm_workspace_bytes": ([i, i, i, i], l),
         "dtc_lmhead_nparts": ([i, i, i], i),
         "dtc_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
+        "dtc_add_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
         "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, i, vp], i),
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, i, vp], i),
         "dtc_gemm_wgrad_split": ([i, i, i, i], i),
         "dtc_gemm_set_n8": ([i], i),
-        "dtc_gemm_set_4w": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
         "dtc_wgrad_group": ([ctypes.POINTER(WgBatch), vp], i),
         "dtc_wg_entry_bytes": ([], i),

@@ -38,6 +38,28 @@ def layernorm_fwd(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
     return y, mean, rstd
 
 
+def add_layernorm_fwd(d: torch.Tensor, resid: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
+                      out_dtype: Optional[torch.dtype] = None):
+    """``x = d + resid`` (fp32, written over ``d``) and ``(LN(x), mean, rstd)``: the residual add of the
+    layer that produced ``d`` (its GEMM stores ``a·Wᵀ + bias``), done in the LayerNorm pass that reads
+    the row anyway instead of in the GEMM epilogue.  Same arithmetic as the fused epilogue
+    (``(acc + bias) + resid``).  Returns ``(x, (y, mean, rstd))``."""
+    M, D = d.shape
+    out_dtype = out_dtype or d.dtype
+    if not d.is_cuda:
+        d.add_(resid)
+        return d, layernorm_fwd(d, g, b, eps, out_dtype)
+    assert d.dtype == torch.float32 and d.is_contiguous() and resid.dtype == torch.float32 and resid.is_contiguous()
+    y = torch.empty(M, D, dtype=out_dtype, device=d.device)
+    mean = torch.empty(M, dtype=torch.float32, device=d.device)
+    rstd = torch.empty_like(mean)
+    N.check(N.lib().dtc_add_layernorm_fwd(d.data_ptr(), resid.data_ptr(), d.data_ptr(), g.data_ptr(), b.data_ptr(),
+                                          y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), M, D, eps,
+                                          1 if out_dtype == torch.float32 else 0, N.stream_ptr(d.device)),
+            "dtc_add_layernorm_fwd")
+    return d, (y, mean, rstd)
+
+
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, g: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
                   dres: Optional[torch.Tensor], dg: torch.Tensor, db: torch.Tensor, beta: float = 0.0,
                   out: Optional[torch.Tensor] = None, out_c: Optional[torch.Tensor] = None,

@@ -24,6 +24,7 @@ from ..config.schema import ModelConfig, OptimConfig, TrainConfig
 from ..models.gpt import GPTStage, StageLayout
 from ..models.params import stage_param_specs
 from ..ops import embedding as E
+from ..ops import gemm as G
 from ..ops import optim as O
 from ..parallel.buffers import FlatParams
 from ..parallel.dist import DistInfo

@@ -30,10 +30,8 @@ def _close(a, b, rtol, name):
 def n8(cuda):
     L = N.lib()
     old = L.dtc_gemm_set_n8(7)  # every whole-round shape (the default takes one-round shapes)
-    old4 = L.dtc_gemm_set_4w(0)  # gemm4w (tests/test_gemm4w_gpu.py) would take the GPT-2 small shapes first
     yield L
     L.dtc_gemm_set_n8(old)
-    L.dtc_gemm_set_4w(old4)
 
 
 # (M, N, K): GPT-2 small qkv / out_proj / fc1 / fc2 (8192 tokens), ragged M (8100 -> 64 M-tiles),

@@ -150,6 +150,22 @@ def test_layernorm(cuda, D):
     _close(db.cpu(), dbc, 1e-4, "ln_db")
 
 
+@pytest.mark.parametrize("D", [512, 768, 1024])
+def test_add_layernorm(cuda, D):
+    """Residual add in the LayerNorm pass (models/gpt.py DTC_ADD_LN): x = d + resid written over d
+    (bitwise the fp32 sum), LN(x) as the plain LayerNorm of that sum."""
+    M = 1000
+    d = _r(M, D, dtype=torch.float32, seed=17)
+    r = _r(M, D, dtype=torch.float32, seed=18) * 3 + 1
+    g, b = _r(D, dtype=torch.float32, seed=19), _r(D, dtype=torch.float32, seed=20)
+    want = d + r
+    d2 = d.clone()
+    x, (y, mu, rs) = LN.add_layernorm_fwd(d2, r, g, b, 1e-6, torch.bfloat16)
+    assert x.data_ptr() == d2.data_ptr() and torch.equal(x, want)
+    y0, mu0, rs0 = LN.layernorm_fwd(want, g, b, 1e-6, torch.bfloat16)
+    assert torch.equal(y, y0) and torch.equal(mu, mu0) and torch.equal(rs, rs0)
+
+
 def test_embedding_dropout_bits(cuda):
     B, T, D, V = 4, 64, 128, 1000
     ids = torch.randint(0, V, (B, T), dtype=torch.int32)
