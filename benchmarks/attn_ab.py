@@ -60,6 +60,7 @@ def main():
         variants = {"fwd (32 q/wave, 32x32x16)": lambda: A.attn_fwd(qkv, H),
                     "fwd (16 q/wave chunk)": lambda: A.attn_fwd(qkv, H, flags=4),
                     "bwd (32 rows/wave)": lambda: A.attn_bwd(qkv, o, lse, do, H),
+                    "bwd merged (delta + 1 launch)": lambda: A.attn_bwd(qkv, o, lse, do, H, flags=8),
                     "bwd (16-row chunk)": lambda: A.attn_bwd(qkv, o, lse, do, H, flags=4)}
     res = {k: [] for k in variants}
     for _ in range(a.rounds):

@@ -77,10 +77,9 @@ def main():
     for (n, k, tag) in [(3 * D, D, "qkv"), (D, D, "out"), (F, D, "fc1"), (D, F, "fc2")]:
         x, w, b = r(M, k), r(n, k, sc=0.05), torch.randn(n, device=dev, generator=g) * 0.1
         fl = 2.0 * M * n * k
-        if tag in ("out", "fc2"):
-            res = torch.randn(M, n, device=dev, generator=g)
-            add(f"fwd {tag} [{M}x{n}x{k}] resid", fl, lambda x=x, w=w, b=b, res=res: G.linear_resid(x, w, b, res),
-                lambda x=x, w=w, b=b, res=res: x.float() @ w.float().t() + b + res, lambda x=x, w=w: x @ w.t())
+        if tag in ("out", "fc2"):  # as the step runs them (DTC_ADD_LN): fp32 a·Wᵀ + b, residual added by the LN
+            add(f"fwd {tag} [{M}x{n}x{k}] f32+b", fl, lambda x=x, w=w, b=b: G.linear(x, w, b, out_dtype=torch.float32),
+                lambda x=x, w=w, b=b: x.float() @ w.float().t() + b, lambda x=x, w=w: x @ w.t())
         elif tag == "fc1":
             add(f"fwd {tag} [{M}x{n}x{k}] gelu", fl, lambda x=x, w=w, b=b: G.linear_gelu(x, w, b)[1],
                 lambda x=x, w=w, b=b: G.gelu_tanh(x.float() @ w.float().t() + b), lambda x=x, w=w: x @ w.t())

@@ -923,19 +923,20 @@ __device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, __amdgpu_buf
 // = 32 queries on the lane.  Per 32-key block: S^T = K Q^T and dP^T = V dO^T (K / V row fragments, Q /
 // dO stationary in registers), dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K transposed
 // fragments, dS^T straight from the accumulators).
-template <int HD>
-__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
-    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
-    float scale) {
+// DELTA_IN (the merged launch): delta comes precomputed (attn_delta_kernel) instead of from O here.
+template <int HD, bool DELTA_IN>
+__device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ o,
+                                          const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                          float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
+                                          float scale) {
   static_assert(HD == 64, "swizzled 64-wide images");
   constexpr int HC = HD / 16, HB = HD / 32;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nqb = (T + FW_QROWS - 1) / FW_QROWS, nbh = B * H;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);
-  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  const int qblk = nqb - 1 - (int)(bid / nbh);
+  const int bh = bid % nbh, b = bh / H, h = bh % H;
   DTC_ASSERT(qblk >= 0 && b < B && h < H);
   const long ts = 3L * H * HD, dts = (long)H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
@@ -949,12 +950,19 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
   for (int c = 0; c < HC; ++c) {
     qf[c] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + 16 * c + 8 * hh) : bf16x8{};
     df[c] = q < T ? *(const bf16x8*)(dOb + (long)q * dts + 16 * c + 8 * hh) : bf16x8{};
-    const bf16x8 of = q < T ? *(const bf16x8*)(o + ((long)b * T + q) * dts + h * HD + 16 * c + 8 * hh) : bf16x8{};
+    if constexpr (!DELTA_IN) {
+      const bf16x8 of = q < T ? *(const bf16x8*)(o + ((long)b * T + q) * dts + h * HD + 16 * c + 8 * hh) : bf16x8{};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dpart += (float)of[e] * (float)df[c][e];
+      for (int e = 0; e < 8; ++e) dpart += (float)of[e] * (float)df[c][e];
+    }
   }
-  const float dlt = dpart + __shfl_xor(dpart, 32, 64);
-  if (hh == 0 && q < T) delta[((long)b * H + h) * T + q] = dlt;
+  float dlt;
+  if constexpr (DELTA_IN) {
+    dlt = q < T ? delta[((long)b * H + h) * T + q] : 0.f;
+  } else {
+    dlt = dpart + __shfl_xor(dpart, 32, 64);
+    if (hh == 0 && q < T) delta[((long)b * H + h) * T + q] = dlt;
+  }
   const float lq = q < T ? lse[((long)b * H + h) * T + q] * LOG2E : 0.f;
   const float cs = scale * LOG2E;
   f32x16 acc[HB];
@@ -1010,22 +1018,30 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
   }
 }
 
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
+    float scale) {
+  dq32_body<HD, false>((int)blockIdx.x, qkv, o, dout, lse, delta, dqkv, B, T, H, scale);
+}
+
 // dK, dV: block = 4 waves = 128 keys of one (b, h); wave = 32 keys on the lane.  Per 32-query block:
 // S = Q K^T and dP = dO V^T (Q / dO row fragments, K / V stationary), P and dS = P (dP - delta) with the
 // key on the lane, dV^T += dO^T P and dK^T += Q^T dS (Q / dO transposed fragments of the same images,
 // P / dS straight from the accumulators).  The heaviest key block (0: every query) goes first.
 template <int HD>
-__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dkdv32_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+__device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                            const float* __restrict__ lse, const float* __restrict__ delta,
+                                            bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
   static_assert(HD == 64, "swizzled 64-wide images");
   constexpr int HC = HD / 16, HB = HD / 32;
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nbh = B * H;
-  const int kblk = (int)(blockIdx.x / nbh);
-  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  const int kblk = (int)(bid / nbh);
+  const int bh = bid % nbh, b = bh / H, h = bh % H;
   DTC_ASSERT(kblk * FW_QROWS < T && b < B && h < H);
   const long ts = 3L * H * HD, dts = (long)H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
@@ -1111,6 +1127,25 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dkdv32_kernel(
                                      f2bf(dv[i][4 * g4 + 3])};
       }
   }
+}
+
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dkdv32_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
+  dkdv32_body<HD>((int)blockIdx.x, qkv, dout, lse, delta, dqkv, B, T, H, scale);
+}
+
+// dK/dV and dQ blocks in ONE launch (delta precomputed by attn_delta_kernel): the dK/dV blocks first,
+// then the dQ blocks, each heaviest first, so the second kernel's blocks fill the first one's tail
+// instead of each launch ending in its own partial round (DTC_ATTN_BWD_MERGED).
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_merged32_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale, int nk) {
+  const int bid = (int)blockIdx.x;
+  if (bid < nk) dkdv32_body<HD>(bid, qkv, dout, lse, delta, dqkv, B, T, H, scale);
+  else dq32_body<HD, true>(bid - nk, qkv, nullptr, dout, lse, delta, dqkv, B, T, H, scale);
 }
 
 // Chunked backward for T > RES_MAXT / head_dim 64 (the tiled kernels above with 16 waves = 256
@@ -1891,10 +1926,20 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
       allow_lds(attn_bwd_dq32_kernel<64>, lb);
       allow_lds(attn_bwd_dkdv32_kernel<64>, lb);
       const dim3 g32(B * H * ((T + FW_QROWS - 1) / FW_QROWS));
-      hipLaunchKernelGGL(attn_bwd_dq32_kernel<64>, g32, dim3(FW_THREADS), lb, st, qkv, o, dout, lse, ws, dqkv, B, T, H,
-                         scale);
-      hipLaunchKernelGGL(attn_bwd_dkdv32_kernel<64>, g32, dim3(FW_THREADS), lb, st, qkv, dout, lse, ws, dqkv, B, T, H,
-                         scale);
+      // DTC_ATTN_BWD_MERGED (flags bit 3 forces it): delta pass + one launch of dK/dV and dQ blocks
+      static const int bwd_merged = [] { const char* v = getenv("DTC_ATTN_BWD_MERGED"); return v ? atoi(v) : 0; }();
+      if (bwd_merged || (flags & 8)) {
+        allow_lds(attn_bwd_merged32_kernel<64>, lb);
+        const long n = (long)B * T * H;
+        hipLaunchKernelGGL(attn_delta_kernel<64>, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, ws, B, T, H);
+        hipLaunchKernelGGL(attn_bwd_merged32_kernel<64>, dim3(2 * g32.x), dim3(FW_THREADS), lb, st, qkv, dout, lse, ws,
+                           dqkv, B, T, H, scale, (int)g32.x);
+      } else {
+        hipLaunchKernelGGL(attn_bwd_dq32_kernel<64>, g32, dim3(FW_THREADS), lb, st, qkv, o, dout, lse, ws, dqkv, B, T,
+                           H, scale);
+        hipLaunchKernelGGL(attn_bwd_dkdv32_kernel<64>, g32, dim3(FW_THREADS), lb, st, qkv, dout, lse, ws, dqkv, B, T,
+                           H, scale);
+      }
     } else if (HD == 64) {
       allow_lds(attn_bwd_dkdv_chunk_kernel<64>, ch_lds_bwd<64>());
       allow_lds(attn_bwd_dq_chunk_kernel<64>, ch_lds_bwd<64>());

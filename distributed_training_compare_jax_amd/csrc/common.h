@@ -62,7 +62,7 @@ struct WgBatch {
   int K;
   float beta;
   int ntiles;
-  float* sq;  // optional [ntiles]: per-tile sum of squares of the final dW values (the grad-norm partials)
+  float* sq;  // optional [ntiles][8]: per-tile, per-wave sums of squares of the final dW (grad-norm partials)
   WgEntry e[WG_MAX];
 };
 

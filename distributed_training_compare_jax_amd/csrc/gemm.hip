@@ -159,7 +159,7 @@ struct Epi {
   float* label_out;
   float* colsum;
   int cs_accum;  // colsum IS the bias gradient: colsum[m] = beta*colsum[m] + sum (split == 1 only)
-  float* sq;     // gemm8p_tile, fp32 store: this tile's sum of squares of the stored values (one float)
+  float* sq;     // gemm8p_tile, fp32 store: per-wave sums of squares of the stored values (8 slots)
   LnEpi ln;
 };
 
@@ -1398,17 +1398,9 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
       int n = n0 + wc * WN + i * 16 + g4;
       if (m < M && n < N) ss += epilogue_store<EPI, OUTF32>(e, m, n, acc[i][j]);
     }
-  if (OUTF32 && e.sq) {  // grad-norm partial of the tile (fixed order: lanes, then waves 0..7)
-    ss = warp_sum(ss);
-    float* red = (float*)smem;  // free: every wave is past the main loop's last barrier
-    if (lane == 0) red[wave] = ss;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NT2 / 64; ++w) t += red[w];
-      *e.sq = t;
-    }
+  if (OUTF32 && e.sq) {  // grad-norm partial of this wave's part of the tile: one slot per wave, no barrier
+    ss = warp_sum(ss);     // (a block-wide sum needed a __syncthreads that waited for every store: +70 us)
+    if (lane == 0) e.sq[wave] = ss;
   }
 }
 
@@ -1445,7 +1437,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
   Epi e{};
   e.M = w.M; e.N = w.N; e.C = w.C; e.ldc = w.N; e.alpha = 1.f; e.beta = b.beta;
   e.colsum = w.cs; e.cs_accum = 1;
-  e.sq = b.sq ? b.sq + lid : nullptr;
+  e.sq = b.sq ? b.sq + (long)lid * (NT2 / 64) : nullptr;  // NT2 / 64 wave slots per tile
   gemm8p_tile<false, false, EPI_STORE, true, 4>(w.A, w.M, w.B, w.N, w.M, w.N, b.K, tm_idx, tn_idx, 0, 1, b.K,
                                                  nullptr, e);
 }

@@ -320,8 +320,11 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, beta: float = 0.0
 _WG_CHECKED = [False]
 
 
+WG_SQ_SLOTS = 8  # grad-norm partial slots per 256² tile (one per wave of gemm8p_group_kernel)
+
+
 def wgrad_tiles(m: int, n: int) -> int:
-    """256² tiles of one grouped weight-gradient problem dW[m, n] (its grad-norm partial slots)."""
+    """256² tiles of one grouped weight-gradient problem dW[m, n] (WG_SQ_SLOTS grad-norm slots each)."""
     return ((m + 255) // 256) * ((n + 255) // 256)
 
 
@@ -334,8 +337,8 @@ def wgrad_group(items, beta: float = 0.0, red=None, sq: Optional[torch.Tensor] =
     cannot take (fp32 operands, a width not a multiple of 8, tokens not a multiple of 64) go through
     :func:`wgrad` one by one (``red``: its batched reducer), as do CPU tensors.
 
-    ``sq`` (fp32, >= Σ :func:`wgrad_tiles` slots): every tile also writes the sum of squares of its final
-    dW values there (the global grad norm's partials, so the norm pass skips these grads); then every
+    ``sq`` (fp32, >= WG_SQ_SLOTS · Σ :func:`wgrad_tiles` slots): every tile's waves also write the sums of
+    squares of their final dW values there (the global grad norm's partials, so the norm pass skips these grads); then every
     item must take the grouped kernel."""
     if not items:
         return
@@ -366,13 +369,13 @@ def wgrad_group(items, beta: float = 0.0, red=None, sq: Optional[torch.Tensor] =
     fast.sort(key=lambda it: -(it[0].shape[1] * it[1].shape[1]))
     if sq is not None:
         assert sq.dtype == torch.float32 and sq.is_contiguous() and sq.is_cuda
-        assert sq.numel() >= sum(wgrad_tiles(it[0].shape[1], it[1].shape[1]) for it in fast), "sq too small"
+        assert sq.numel() >= WG_SQ_SLOTS * sum(wgrad_tiles(it[0].shape[1], it[1].shape[1]) for it in fast), "sq"
     off = 0
     for i0 in range(0, len(fast), N.WG_MAX):
         chunk = fast[i0:i0 + N.WG_MAX]
         b = N.WgBatch()
         b.n, b.K, b.beta, b.ntiles = len(chunk), K, float(beta), 0
-        b.sq = None if sq is None else sq.data_ptr() + 4 * off
+        b.sq = None if sq is None else sq.data_ptr() + 4 * WG_SQ_SLOTS * off
         for j, (dy, x, dw, db) in enumerate(chunk):
             b.e[j] = N.WgEntry(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N.ptr(db), dy.shape[1], x.shape[1], 0, 0)
             off += wgrad_tiles(dy.shape[1], x.shape[1])

@@ -529,7 +529,7 @@ class Engine:
             for dw, m, n in st.wg_seen:
                 ranges.append(((dw.data_ptr() - base) // 4, dw.numel()))
                 tiles += G.wgrad_tiles(m, n)
-            st.use_wgrad_sumsq(self.opt.set_fused_sumsq(ranges, tiles))
+            st.use_wgrad_sumsq(self.opt.set_fused_sumsq(ranges, tiles * G.WG_SQ_SLOTS))
         return self.loss
 
     def loss_value(self) -> float:

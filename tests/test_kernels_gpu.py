@@ -264,12 +264,16 @@ def test_attention_fwd32_vs_chunk_and_reference(cuda, B, T, H, spike):
     do = _r(B, T, H * hd, seed=41)
     d = A.attn_bwd(qkv, o, lse, do, H)
     d4 = A.attn_bwd(qkv, o, lse, do, H, flags=4)
+    d8 = A.attn_bwd(qkv, o, lse, do, H, flags=8)  # merged: delta pass + dK/dV and dQ blocks in one launch
     dref = A.attn_bwd(qkv.cpu().float(), o.cpu().float(), lse.cpu(), do.cpu().float(), H)
     d3, r3, o3 = d.cpu().float().view(B, T, 3, -1), dref.view(B, T, 3, -1), d4.cpu().float().view(B, T, 3, -1)
+    m3 = d8.cpu().float().view(B, T, 3, -1)
     for i, n in enumerate("qkv"):
         _close(d3[:, :, i], r3[:, :, i], 3e-2, f"attn32_d{n}")
         _close(d3[:, :, i], o3[:, :, i], 3e-2, f"attn32_vs_chunk_d{n}")
+        _close(m3[:, :, i], r3[:, :, i], 3e-2, f"attn32_merged_d{n}")
     assert torch.equal(d, A.attn_bwd(qkv, o, lse, do, H))  # deterministic
+    assert torch.equal(d8, A.attn_bwd(qkv, o, lse, do, H, flags=8))
 
 
 @pytest.mark.parametrize("B,T,H", [(2, 512, 4), (1, 200, 3), (2, 64, 2)])
