@@ -104,23 +104,26 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
                                                      const float* __restrict__ g, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ dres,
                                                      float* __restrict__ dx, bf16* __restrict__ dx_c,
-                                                     float* __restrict__ part, int nslab, int M, int D) {
+                                                     float* __restrict__ part, int nslab, int M, int D, int iters) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int D4 = D / 4;
   f32x4 ag[NV], ab[NV], ao[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) { ag[i] = f32x4{0.f, 0.f, 0.f, 0.f}; ab[i] = ag[i]; ao[i] = ag[i]; }
-  const int r0 = blockIdx.x * LN_BWD_ROWS + wave * LN_RPW;
-  DTC_ASSERT(D % 4 == 0 && D / 4 <= NV * 64 && (long)blockIdx.x * LN_BWD_ROWS < M + LN_BWD_ROWS);
-  f32x4 xh[LN_RPW][NV], d[LN_RPW][NV], rv[LN_RPW][NV], gv[NV];
-  float s1[LN_RPW] = {}, s2[LN_RPW] = {}, rsv[LN_RPW] = {};
-  // every global load of the block (x, dy, the residual gradient, gamma) is issued before the first
-  // use: the residual-gradient read used to sit after the row reductions, fully exposed
+  DTC_ASSERT(D % 4 == 0 && D / 4 <= NV * 64 && (long)blockIdx.x * LN_BWD_ROWS * iters < M + LN_BWD_ROWS * iters);
+  f32x4 gv[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     gv[i] = c < D4 ? ((const f32x4*)g)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  // iters row groups per block (one partial row per block: fewer partials for the column reduction)
+  for (int it = 0; it < iters; ++it) {
+  const int r0 = (blockIdx.x * iters + it) * LN_BWD_ROWS + wave * LN_RPW;
+  f32x4 xh[LN_RPW][NV], d[LN_RPW][NV], rv[LN_RPW][NV];
+  float s1[LN_RPW] = {}, s2[LN_RPW] = {}, rsv[LN_RPW] = {};
+  // every global load of the row group (x, dy, the residual gradient) is issued before the first
+  // use: the residual-gradient read used to sit after the row reductions, fully exposed
 #pragma unroll
   for (int q = 0; q < LN_RPW; ++q) {
     const int row = r0 + q;
@@ -174,6 +177,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
       }
     }
   }
+  }  // row groups
   // block reduce of the column partials over the 4 waves (fixed order); part[block][nslab][D]
   __shared__ __attribute__((aligned(16))) float red[4][3][NV * 256];
 #pragma unroll
@@ -370,8 +374,15 @@ int dtc_layernorm_fwd(const float* x, const float* g, const float* b, void* y, f
   return dtc_add_layernorm_fwd(x, nullptr, nullptr, g, b, y, mean, rstd, M, D, eps, out_f32, st);
 }
 
+// DTC_LN_BWD_ITER: row groups of LN_BWD_ROWS per block (1: one group, 1024 blocks at 8192 rows)
+static int ln_bwd_iters() {
+  static const int v = [] { const char* e = getenv("DTC_LN_BWD_ITER"); return e ? std::max(1, atoi(e)) : 1; }();
+  return v;
+}
+
 long dtc_layernorm_bwd_workspace_bytes(int M, int D) {
-  long blocks = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  const int rows = LN_BWD_ROWS * ln_bwd_iters();
+  long blocks = (M + rows - 1) / rows;
   return blocks * 3 * D * 4;
 }
 
@@ -379,12 +390,13 @@ int dtc_layernorm_bwd(const void* dy, int dy_f32, const float* x, const float* g
                       const float* dres, float* dx, bf16* dx_c, float* dg, float* db, float* dbias, int M, int D,
                       int accumulate, float* ws, long ws_bytes, int defer, hipStream_t st) {
   if (D % 4 || D > 1024) return 2002;  // dgamma/dbeta block reduce holds D <= 1024 in LDS
-  int blocks = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  const int iters = ln_bwd_iters();
+  int blocks = (M + LN_BWD_ROWS * iters - 1) / (LN_BWD_ROWS * iters);
   if (ws_bytes < dtc_layernorm_bwd_workspace_bytes(M, D)) return 2003;
   int nv = (D / 4 + 63) / 64;
   const int nslab = dbias ? 3 : 2;
   DTC_NV_SWITCH(nv, hipLaunchKernelGGL(ln_bwd_kernel<NVC>, dim3(blocks), dim3(256), 0, st, dy, dy_f32, x, g, mean, rstd,
-                                       dres, dx, dx_c, ws, nslab, M, D));
+                                       dres, dx, dx_c, ws, nslab, M, D, iters));
   DTC_CHECK_LAUNCH();
   if (defer) return 0;  // partials stay in ws: [blocks][nslab][D] (a RED_TALL task per slab)
   hipLaunchKernelGGL(slab_reduce, dim3((nslab * D + SR_COLS - 1) / SR_COLS), dim3(256), 0, st, ws, blocks, nslab * D, dg, db, dbias,
