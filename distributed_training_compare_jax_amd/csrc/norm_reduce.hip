@@ -374,9 +374,11 @@ int dtc_layernorm_fwd(const float* x, const float* g, const float* b, void* y, f
   return dtc_add_layernorm_fwd(x, nullptr, nullptr, g, b, y, mean, rstd, M, D, eps, out_f32, st);
 }
 
-// DTC_LN_BWD_ITER: row groups of LN_BWD_ROWS per block (1: one group, 1024 blocks at 8192 rows)
+// DTC_LN_BWD_ITER: row groups of LN_BWD_ROWS per block.  2 (512 blocks at 8192 rows): half the partial
+// rows for the batched column reduction -- GPT-2 small step 11.22-11.24 vs 11.31-11.34 ms with 1,
+// 11.25-11.29 with 4 (profiles/r4_ab_ln_bwd_iter.log)
 static int ln_bwd_iters() {
-  static const int v = [] { const char* e = getenv("DTC_LN_BWD_ITER"); return e ? std::max(1, atoi(e)) : 1; }();
+  static const int v = [] { const char* e = getenv("DTC_LN_BWD_ITER"); return e ? std::max(1, atoi(e)) : 2; }();
   return v;
 }
 
