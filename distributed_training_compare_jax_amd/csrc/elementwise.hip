@@ -272,17 +272,22 @@ __global__ void ce_bwd_kernel(bf16* __restrict__ logits, long ld, const float* _
 }
 
 // Same, plus per-column partial sums of dlogits (the lm_head bias gradient) over chunks of
-// CE_ROWS rows: colpart[chunk][V] (fp32, pre-rounding).  Grid (ceil(V/8/256), ceil(M/CE_ROWS)):
-// a thread walks CE_ROWS rows of one 8-column group, so the 412 MB dlogits pass also yields
+// ce_rows() rows: colpart[chunk][V] (fp32, pre-rounding).  Grid (ceil(V/8/256), ceil(M/rows)):
+// a thread walks `rows` rows of one 8-column group, so the 412 MB dlogits pass also yields
 // db without a second read of it.
-constexpr int CE_ROWS = 64;
+// DTC_CE_ROWS (default 64): rows per block of the CE backward = rows per column-partial slab
+static int ce_rows() {
+  static const int v = [] { const char* e = getenv("DTC_CE_ROWS"); return e ? std::max(8, atoi(e)) : 64; }();
+  return v;
+}
 __global__ void __launch_bounds__(256) ce_bwd_colsum_kernel(bf16* __restrict__ logits, long ld,
                                                            const float* __restrict__ lse,
                                                            const int* __restrict__ labels, int M, int V, int vstart,
-                                                           int n_valid, float scale, float* __restrict__ colpart) {
+                                                           int n_valid, float scale, float* __restrict__ colpart,
+                                                           int rows) {
   const int n = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (n >= V) return;
-  const int m0 = blockIdx.y * CE_ROWS, m1 = min(M, m0 + CE_ROWS);
+  const int m0 = blockIdx.y * rows, m1 = min(M, m0 + rows);
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   DTC_ASSERT(m0 < M && n + 8 <= V);
 #pragma unroll 4
@@ -309,10 +314,10 @@ __global__ void __launch_bounds__(256) ce_bwd_colsum_f32_kernel(float* __restric
                                                                const float* __restrict__ lse,
                                                                const int* __restrict__ labels, int M, int V,
                                                                int vstart, int n_valid, float scale,
-                                                               float* __restrict__ colpart) {
+                                                               float* __restrict__ colpart, int rows) {
   const int n = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (n >= V) return;
-  const int m0 = blockIdx.y * CE_ROWS, m1 = min(M, m0 + CE_ROWS);
+  const int m0 = blockIdx.y * rows, m1 = min(M, m0 + rows);
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
   for (int m = m0; m < m1; ++m) {
@@ -591,16 +596,16 @@ int dtc_ce_combine(const float* part, int M, int P, long srow, long spart, const
   return 0;
 }
 
-int dtc_ce_colsum_rows() { return CE_ROWS; }
+int dtc_ce_colsum_rows() { return ce_rows(); }
 
-// colpart (optional): [ceil(M/CE_ROWS)][V] fp32 column partial sums of dlogits
+// colpart (optional): [ceil(M/ce_rows())][V] fp32 column partial sums of dlogits
 int dtc_ce_bwd(bf16* logits, long ld, const float* lse, const int* labels, int M, int V, int vstart, int n_valid,
                float scale, float* colpart, hipStream_t st) {
   if (V % 8 || ld % 8) return 3003;
   if (colpart) {
-    dim3 grid((V / 8 + 255) / 256, (M + CE_ROWS - 1) / CE_ROWS);
+    dim3 grid((V / 8 + 255) / 256, (M + ce_rows() - 1) / ce_rows());
     hipLaunchKernelGGL(ce_bwd_colsum_kernel, grid, dim3(256), 0, st, logits, ld, lse, labels, M, V, vstart, n_valid,
-                       scale, colpart);
+                       scale, colpart, ce_rows());
     DTC_CHECK_LAUNCH();
     return 0;
   }
@@ -611,13 +616,13 @@ int dtc_ce_bwd(bf16* logits, long ld, const float* lse, const int* labels, int M
   return 0;
 }
 
-// fp32 logits: colpart (optional) [ceil(M/CE_ROWS)][V]
+// fp32 logits: colpart (optional) [ceil(M/ce_rows())][V]
 int dtc_ce_bwd_f32(float* logits, long ld, const float* lse, const int* labels, int M, int V, int vstart, int n_valid,
                    float scale, float* colpart, hipStream_t st) {
   if (V % 8 || ld % 4) return 3003;
-  dim3 grid((V / 8 + 255) / 256, (M + CE_ROWS - 1) / CE_ROWS);
+  dim3 grid((V / 8 + 255) / 256, (M + ce_rows() - 1) / ce_rows());
   hipLaunchKernelGGL(ce_bwd_colsum_f32_kernel, grid, dim3(256), 0, st, logits, ld, lse, labels, M, V, vstart, n_valid,
-                     scale, colpart);
+                     scale, colpart, ce_rows());
   DTC_CHECK_LAUNCH();
   return 0;
 }
