@@ -275,9 +275,11 @@ __global__ void ce_bwd_kernel(bf16* __restrict__ logits, long ld, const float* _
 // ce_rows() rows: colpart[chunk][V] (fp32, pre-rounding).  Grid (ceil(V/8/256), ceil(M/rows)):
 // a thread walks `rows` rows of one 8-column group, so the 412 MB dlogits pass also yields
 // db without a second read of it.
-// DTC_CE_ROWS (default 64): rows per block of the CE backward = rows per column-partial slab
+// DTC_CE_ROWS (default 128): rows per block of the CE backward = rows per column-partial slab; 128 halves
+// the slabs the batched reduction reads (GPT-2 small 11.18-11.22 vs 11.22-11.25 ms with 64,
+// profiles/r4_ab_ce_rows.log)
 static int ce_rows() {
-  static const int v = [] { const char* e = getenv("DTC_CE_ROWS"); return e ? std::max(8, atoi(e)) : 64; }();
+  static const int v = [] { const char* e = getenv("DTC_CE_ROWS"); return e ? std::max(8, atoi(e)) : 128; }();
   return v;
 }
 __global__ void __launch_bounds__(256) ce_bwd_colsum_kernel(bf16* __restrict__ logits, long ld,
