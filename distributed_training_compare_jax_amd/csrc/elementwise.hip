@@ -178,6 +178,7 @@ __global__ void wpe_bwd_kernel(const float* __restrict__ dh, float* __restrict__
   if (i >= (long)T * D4) return;
   int t = (int)(i / D4);
   int d = (int)(i % D4) * 4;
+  DTC_ASSERT(D % 4 == 0 && t < T && d + 4 <= D && B >= 1);
   const uint32_t thr = drop_threshold(p), stp = (uint32_t)step[0];
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -199,6 +200,7 @@ __global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__
                                                        float* __restrict__ lse_out, float* __restrict__ rowstat) {
   const int r = threadIdx.x % CC_ROWS, pl = threadIdx.x / CC_ROWS;
   const int row = blockIdx.x * CC_ROWS + r;
+  DTC_ASSERT(P >= 1 && pl < CC_LANES && (long)blockIdx.x * CC_ROWS < M);
   __shared__ float red[CC_LANES][CC_ROWS];
   __shared__ float rmax[CC_ROWS];
   float mx = -INFINITY;
@@ -352,6 +354,7 @@ __global__ void __launch_bounds__(256) sumsq_stage1(const float* __restrict__ x,
   for (int s = 0; s < S; ++s) {
     const long off = (long)seg[3 * s], len = (long)seg[3 * s + 1];
     const float w = (float)seg[3 * s + 2];
+    DTC_ASSERT(off >= 0 && len >= 0 && off % 4 == 0);
     float a = 0.f;
     const long len4 = len >> 2;  // ranges are 64-element aligned: 16-byte loads, 4 in flight
     const f32x4* x4 = (const f32x4*)(x + off);
@@ -418,6 +421,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     for (int c = 0; c < CH; ++c) {
       const long j = i + (long)c * blockDim.x * 4;
       if (CH > 1 && j >= n) break;
+      DTC_ASSERT(j + 4 <= n && n_mirror <= n);  // n % 4 == 0 (host-checked)
       pp[c] = __builtin_nontemporal_load((f32x4*)(p + j));
       gg[c] = __builtin_nontemporal_load((const f32x4*)(g + j));
       mm[c] = __builtin_nontemporal_load((f32x4*)(m + j));

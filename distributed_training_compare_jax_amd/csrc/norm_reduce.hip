@@ -206,6 +206,7 @@ __global__ void __launch_bounds__(256) slab_reduce(const float* __restrict__ par
                                                    float* __restrict__ o1, float* __restrict__ o2, int seg, float beta) {
   const int tx = threadIdx.x % SR_COLS, ty = threadIdx.x / SR_COLS;
   const int c = blockIdx.x * SR_COLS + tx;
+  DTC_ASSERT(P >= 1 && ty < SR_GROUPS && (long)blockIdx.x * SR_COLS < C);
   float s = 0.f;
   if (c < C) {
 #pragma unroll 4
@@ -233,6 +234,7 @@ __global__ void __launch_bounds__(256) colsum_stage1(const void* __restrict__ dy
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int n = (blockIdx.x * 64 + tx) * 4;
   const int r0 = blockIdx.y * CS_ROWS + ty * (CS_ROWS / 4);
+  DTC_ASSERT((long)blockIdx.y * CS_ROWS < M && ld >= N && ld % 4 == 0);
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (n < N) {
     if (n + 4 <= N) {

@@ -66,6 +66,7 @@ __global__ void p2p_barrier_kernel(PeerTable t, int rank, int world, uint32_t* _
 __global__ void p2p_stage_kernel(const f32x4* __restrict__ x, PeerTable t, int rank, long n4, long half_bytes,
                                  const uint32_t* __restrict__ epoch) {
   const int h = (epoch[0] >> 1) & 1;
+  DTC_ASSERT(16 * n4 <= half_bytes && rank >= 0);
   f32x4* dst = (f32x4*)(t.base[rank] + FLAG_BYTES + h * half_bytes);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) dst[i] = x[i];
 }
@@ -104,6 +105,7 @@ __global__ void p2p_oneshot_kernel(PeerTable t, int world, long n4, long half_by
                                    const uint32_t* __restrict__ epoch) {
   const int h = ((epoch[0] - 2) >> 1) & 1;
   const long off = FLAG_BYTES + h * half_bytes;
+  DTC_ASSERT(16 * n4 <= half_bytes && world >= 1);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     f32x4 s = ((const f32x4*)(t.base[0] + off))[i];
     for (int p = 1; p < world; ++p) s += ((const f32x4*)(t.base[p] + off))[i];
@@ -120,6 +122,7 @@ __global__ void p2p_oneshot_kernel(PeerTable t, int world, long n4, long half_by
 __global__ void p2p_stage_bf16_kernel(const bf16x8* __restrict__ x, PeerTable t, int rank, long n8, long half_bytes,
                                       const uint32_t* __restrict__ epoch) {
   const int h = (epoch[0] >> 1) & 1;
+  DTC_ASSERT(16 * n8 <= half_bytes && rank >= 0);
   bf16x8* dst = (bf16x8*)(t.base[rank] + FLAG_BYTES + h * half_bytes);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) dst[i] = x[i];
 }
@@ -151,6 +154,7 @@ __global__ void p2p_oneshot_bf16_kernel(PeerTable t, int world, long n8, long ha
                                         const uint32_t* __restrict__ epoch) {
   const int h = ((epoch[0] - 2) >> 1) & 1;
   const long off = FLAG_BYTES + h * half_bytes;
+  DTC_ASSERT(16 * n8 <= half_bytes && world >= 1 && ncols % 8 == 0);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < world; ++p) add8(a, ((const bf16x8*)(t.base[p] + off))[i]);
@@ -164,6 +168,7 @@ __global__ void p2p_reduce_scatter_bf16_kernel(PeerTable t, int rank, int world,
   const long chunk = (n8 + world - 1) / world;
   const long lo = rank * chunk, hi = min(n8, lo + chunk);
   const long off = FLAG_BYTES + h * half_bytes;
+  DTC_ASSERT(16 * n8 <= half_bytes && rank < world);
   for (long i = lo + (long)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (long)gridDim.x * blockDim.x) {
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < world; ++p) add8(a, ((const bf16x8*)(t.base[p] + off))[i]);
@@ -180,6 +185,7 @@ __global__ void p2p_all_gather_bf16_kernel(PeerTable t, int world, long n8, long
   const int h = ((epoch[0] - 2) >> 1) & 1;
   const long chunk = (n8 + world - 1) / world;
   const long off = FLAG_BYTES + h * half_bytes;
+  DTC_ASSERT(16 * n8 <= half_bytes && world >= 1 && ncols % 8 == 0);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     add8(a, ((const bf16x8*)(t.base[(int)(i / chunk)] + off))[i]);
@@ -273,6 +279,9 @@ int dtc_device_pci_bus_id(int dev, char* buf, int len) { return (int)hipDeviceGe
 int dtc_device_count(int* n) { return (int)hipGetDeviceCount(n); }
 int dtc_can_access_peer(int dev, int peer, int* ok) { return (int)hipDeviceCanAccessPeer(ok, dev, peer); }
 int dtc_p2p_free(void* ptr) { return (int)hipFree(ptr); }
+// Node count of a captured (not yet instantiated) hipGraph: parallel/program.py drops segments that
+// captured nothing (e.g. between a collective and its wait) instead of replaying empty graphs.
+int dtc_graph_num_nodes(void* graph, size_t* n) { return (int)hipGraphGetNodes((hipGraph_t)graph, nullptr, n); }
 
 // out = sum over ranks of x (fp32, n % 4 == 0, n*4 <= half_bytes).  x and out may alias.
 // mode: 0 auto, 1 two-shot, 2 one-shot.  Per link, one-shot moves n bytes (each rank reads every peer

@@ -135,6 +135,7 @@ def _declare(lib):
         "dtc_p2p_close": ([vp], i),
         "dtc_device_pci_bus_id": ([i, ctypes.c_char_p, i], i),
         "dtc_device_count": ([ctypes.POINTER(c_int)], i),
+        "dtc_graph_num_nodes": ([c_vp, ctypes.POINTER(ctypes.c_size_t)], i),
         "dtc_can_access_peer": ([i, i, ctypes.POINTER(c_int)], i),
         "dtc_p2p_free": ([vp], i),
         "dtc_p2p_allreduce": ([vp, vp, l, vp, i, i, l, vp, vp, i, vp], i),

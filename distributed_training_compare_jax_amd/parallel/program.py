@@ -28,7 +28,9 @@ produced in one segment and consumed in a later one stay valid.
 
 from __future__ import annotations
 
+import ctypes
 import time
+import warnings
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -99,6 +101,14 @@ def check_collective_sequences(per_rank: List[List[Tuple]]) -> Optional[str]:
     return None
 
 
+def _graph_nodes(g) -> int:
+    from ..ops import _native as N
+
+    n = ctypes.c_size_t(0)
+    N.check(N.lib().dtc_graph_num_nodes(ctypes.c_void_p(g.raw_cuda_graph()), ctypes.byref(n)), "hipGraphGetNodes")
+    return int(n.value)
+
+
 class StepProgram:
     def __init__(self, device: torch.device, use_graph: bool):
         self.device = torch.device(device)
@@ -108,6 +118,7 @@ class StepProgram:
         self.recorded = False
         self._graph = None
         self._pool = None
+        self._empty: List[Any] = []  # captured-empty segments (see _cut)
         self._handles: Dict[str, Any] = {}
         self._stream = torch.cuda.Stream(self.device) if self.use_graph else None
         # called before every cut/collective: forked streams (e.g. the backward side stream)
@@ -232,13 +243,22 @@ class StepProgram:
     def _begin(self):
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        g = torch.cuda.CUDAGraph()
+        # keep_graph: the captured graph is inspected (node count) before it is instantiated
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
         self._graph = g
 
     def _cut(self):
         g, self._graph = self._graph, None
-        g.capture_end()
+        with warnings.catch_warnings():
+            warnings.filterwarnings("ignore", message=".*Graph is empty")
+            g.capture_end()
+        if _graph_nodes(g) == 0:  # nothing captured since the last cut (e.g. a collective, then its wait)
+            # not replayed, but kept alive: releasing a graph drops its reference on the shared memory
+            # pool, which the allocator asserts on at the next capture into that pool
+            self._empty.append(g)
+            return
+        g.instantiate()
         self.items.append(("graph", g, None))
 
     def record(self, step_fn: Callable[[], Any]) -> Any:
