@@ -14,8 +14,9 @@ namespace {
 // row per wave a wave had 3 x 16 B in flight per lane and the kernel ran at ~4 TB/s
 // resid (optional): the row is x + resid (the residual add of the producing layer, moved here from its
 // GEMM epilogue), written to x_out (may alias x) before it is normalised.
-template <int NV, int RPW>
-__global__ void __launch_bounds__(256) ln_fwd_kernel(const float* x, const float* __restrict__ resid, float* x_out,
+// XB: x is bf16 (a bf16 GEMM output; the sum x + resid is fp32 in x_out, which must not alias x)
+template <int NV, int RPW, bool XB = false>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const void* x, const float* __restrict__ resid, float* x_out,
                                                      const float* __restrict__ g,
                                                      const float* __restrict__ b, void* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -30,11 +31,25 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* x, const float
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int row = row0 + q;
-    const f32x4* xr = (const f32x4*)(x + (long)min(row, M - 1) * D);
+    if constexpr (XB) {
+      const bf16x4* xr = (const bf16x4*)((const bf16*)x + (long)min(row, M - 1) * D);
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      int c = lane + 64 * i;
-      v[q][i] = c < D4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NV; ++i) {
+        int c = lane + 64 * i;
+        if (c < D4) {
+          const bf16x4 t = xr[c];
+          v[q][i] = f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+        } else {
+          v[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    } else {
+      const f32x4* xr = (const f32x4*)((const float*)x + (long)min(row, M - 1) * D);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        int c = lane + 64 * i;
+        v[q][i] = c < D4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     if (resid) {
       const f32x4* rr = (const f32x4*)(resid + (long)min(row, M - 1) * D);
@@ -367,6 +382,19 @@ int dtc_add_layernorm_fwd(const float* x, const float* resid, float* x_out, cons
     DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 1>), grid, dim3(256), 0, st, x, resid, x_out, g, b, y, mean,
                                          rstd, M, D, eps, out_f32));
   }
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// x_out = (fp32) d + resid with d bf16 (a bf16 out_proj / fc2 output, DTC_FWD_BF16), then LayerNorm(x_out)
+int dtc_add_layernorm_fwd_bf16(const bf16* d, const float* resid, float* x_out, const float* g, const float* b,
+                               void* y, float* mean, float* rstd, int M, int D, float eps, int out_f32, hipStream_t st) {
+  if (D % 4) return 2002;
+  DTC_HOST_CHECK(d && resid && x_out && (const void*)d != (const void*)x_out);
+  int nv = (D / 4 + 63) / 64;
+  dim3 grid((M + 3) / 4);
+  DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 1, true>), grid, dim3(256), 0, st, d, resid, x_out, g, b, y,
+                                       mean, rstd, M, D, eps, out_f32));
   DTC_CHECK_LAUNCH();
   return 0;
 }

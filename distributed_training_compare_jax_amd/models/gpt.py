@@ -67,6 +67,13 @@ _CE_CHUNK = int(_os.environ.get("DTC_CE_CHUNK", "0"))
 # residual adds of out_proj / fc2 done by the LayerNorm pass that follows (tp == 1): the GEMM epilogue
 # stores a·Wᵀ + b without reading the fp32 residual (DTC_ADD_LN=0: the fused residual epilogue)
 _ADD_LN = _os.environ.get("DTC_ADD_LN", "1") == "1"
+# qkv / fc1 input-gradient GEMMs (the LayerNorm backward's dy, tp == 1, bf16 compute) store bf16 instead
+# of fp32: half the bytes of the dgrad's store and of the LayerNorm backward's dy read (autocast-style
+# bf16 GEMM outputs; dx itself stays fp32, dx = dres + LN'(dy))
+_DGRAD_BF16 = _os.environ.get("DTC_DGRAD_BF16", "0") == "1"
+# out_proj / fc2 forwards (tp == 1, DTC_ADD_LN, bf16 compute) store a·Wᵀ + b as bf16, the LayerNorm pass
+# adds it to the fp32 residual (autocast-style bf16 GEMM outputs; the residual stream stays fp32)
+_FWD_BF16 = _os.environ.get("DTC_FWD_BF16", "0") == "1"
 if _CE_CHUNK < 0 or _CE_CHUNK % 256:
     # chunk offsets feed 16-byte vector loads of w[c0:], wt[:, c0:] and gw[c0:]: a ragged offset would
     # surface as an opaque native error deep in the backward
@@ -308,6 +315,11 @@ class GPTStage:
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
 
+    @property
+    def _branch_dtype(self) -> torch.dtype:
+        """dtype of the out_proj / fc2 outputs the LayerNorm pass adds to the residual (DTC_FWD_BF16)."""
+        return torch.bfloat16 if _FWD_BF16 and self.act_dtype == torch.bfloat16 else torch.float32
+
     def block_forward(self, l: int, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
         self._await_params(l)
         f, p = self.flat, f"h.{l}."
@@ -331,7 +343,7 @@ class GPTStage:
             # residual add in the LayerNorm pass (the GEMM stores o·Wᵀ + b; its epilogue skips the fp32
             # residual read) -- same fp32 arithmetic, (acc + b) + x
             x2, (y2, mu2, rs2) = LN.add_layernorm_fwd(G.linear(o, f.w(p + "out.w"), f.p(p + "out.b"),
-                                                               out_dtype=torch.float32), x,
+                                                               out_dtype=self._branch_dtype), x,
                                                       f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
         else:
             x2 = G.linear_resid(o, f.w(p + "out.w"), f.p(p + "out.b") if lead else None, x if lead else None)
@@ -346,7 +358,7 @@ class GPTStage:
             ctx[("ln1", l + 1) if nxt != "lnf" else "lnf_pre"] = pre_next
         elif tp.size == 1 and _ADD_LN and nxt is not None and not self.tp_bf16:
             x3, pre_next = LN.add_layernorm_fwd(G.linear(gact, f.w(p + "fc2.w"), f.p(p + "fc2.b"),
-                                                         out_dtype=torch.float32), x2,
+                                                         out_dtype=self._branch_dtype), x2,
                                                 f.p(nxt + ".g"), f.p(nxt + ".b"), self.eps, self.act_dtype)
             ctx[("ln1", l + 1) if nxt != "lnf" else "lnf_pre"] = pre_next
         elif self.tp_bf16:
@@ -499,6 +511,9 @@ class GPTStage:
                 else:
                     dx = (G.linear(dy, wt, out_dtype=torch.bfloat16) if wt is not None
                           else G.matmul_nn(dy, f.w(dense + ".w"), out_dtype=torch.bfloat16))
+            elif _DGRAD_BF16 and self.tp.size == 1 and dy.dtype == torch.bfloat16:
+                dx = (G.linear(dy, wt, out_dtype=torch.bfloat16) if wt is not None
+                      else G.matmul_nn(dy, f.w(dense + ".w"), out_dtype=torch.bfloat16))
             else:
                 dx = G.linear_resid(dy, wt, None, None) if wt is not None else G.matmul_nn(dy, f.w(dense + ".w"))
             self._wg(dy, x, dense, bias=True)

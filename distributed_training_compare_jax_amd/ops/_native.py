@@ -108,6 +108,7 @@ def _declare(lib):
         "dtc_lmhead_nparts": ([i, i, i], i),
         "dtc_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
         "dtc_add_layernorm_fwd": ([vp, vp, vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
+        "dtc_add_layernorm_fwd_bf16": ([vp, vp, vp, vp, vp, vp, vp, vp, i, i, f, i, vp], i),
         "dtc_layernorm_bwd": ([vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, i, i, vp, l, i, vp], i),
         "dtc_layernorm_bwd_workspace_bytes": ([i, i], l),
         "dtc_colsum": ([vp, i, i, i, l, vp, f, vp, l, i, vp], i),

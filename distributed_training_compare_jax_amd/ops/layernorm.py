@@ -43,9 +43,25 @@ def add_layernorm_fwd(d: torch.Tensor, resid: torch.Tensor, g: torch.Tensor, b: 
     """``x = d + resid`` (fp32, written over ``d``) and ``(LN(x), mean, rstd)``: the residual add of the
     layer that produced ``d`` (its GEMM stores ``a·Wᵀ + bias``), done in the LayerNorm pass that reads
     the row anyway instead of in the GEMM epilogue.  Same arithmetic as the fused epilogue
-    (``(acc + bias) + resid``).  Returns ``(x, (y, mean, rstd))``."""
+    (``(acc + bias) + resid``).  Returns ``(x, (y, mean, rstd))``.
+
+    ``d`` bf16 (a bf16 GEMM output, ``DTC_FWD_BF16``): ``x = float(d) + resid`` goes to a new fp32 tensor."""
     M, D = d.shape
-    out_dtype = out_dtype or d.dtype
+    out_dtype = out_dtype or resid.dtype
+    if d.dtype == torch.bfloat16:
+        if not d.is_cuda:
+            x = d.float() + resid
+            return x, layernorm_fwd(x, g, b, eps, out_dtype)
+        assert d.is_contiguous() and resid.dtype == torch.float32 and resid.is_contiguous()
+        x = torch.empty(M, D, dtype=torch.float32, device=d.device)
+        y = torch.empty(M, D, dtype=out_dtype, device=d.device)
+        mean = torch.empty(M, dtype=torch.float32, device=d.device)
+        rstd = torch.empty_like(mean)
+        N.check(N.lib().dtc_add_layernorm_fwd_bf16(d.data_ptr(), resid.data_ptr(), x.data_ptr(), g.data_ptr(),
+                                                   b.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), M, D,
+                                                   eps, 1 if out_dtype == torch.float32 else 0,
+                                                   N.stream_ptr(d.device)), "dtc_add_layernorm_fwd_bf16")
+        return x, (y, mean, rstd)
     if not d.is_cuda:
         d.add_(resid)
         return d, layernorm_fwd(d, g, b, eps, out_dtype)

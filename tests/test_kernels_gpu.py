@@ -164,6 +164,13 @@ def test_add_layernorm(cuda, D):
     assert x.data_ptr() == d2.data_ptr() and torch.equal(x, want)
     y0, mu0, rs0 = LN.layernorm_fwd(want, g, b, 1e-6, torch.bfloat16)
     assert torch.equal(y, y0) and torch.equal(mu, mu0) and torch.equal(rs, rs0)
+    # bf16 branch output (DTC_FWD_BF16): x = float(d) + resid into a new fp32 tensor
+    db = d.to(torch.bfloat16)
+    want = db.float() + r
+    x, (y, mu, rs) = LN.add_layernorm_fwd(db, r, g, b, 1e-6, torch.bfloat16)
+    assert x.dtype == torch.float32 and x.data_ptr() != db.data_ptr() and torch.equal(x, want)
+    y0, mu0, rs0 = LN.layernorm_fwd(want, g, b, 1e-6, torch.bfloat16)
+    assert torch.equal(y, y0) and torch.equal(mu, mu0) and torch.equal(rs, rs0)
 
 
 def test_embedding_dropout_bits(cuda):
