@@ -83,10 +83,20 @@ def main():
         elif tag == "fc1":
             add(f"fwd {tag} [{M}x{n}x{k}] gelu", fl, lambda x=x, w=w, b=b: G.linear_gelu(x, w, b)[1],
                 lambda x=x, w=w, b=b: G.gelu_tanh(x.float() @ w.float().t() + b), lambda x=x, w=w: x @ w.t())
+            # the same GEMM with one plain bf16 output (what the yardstick computes): the dual-output GELU
+            # epilogue's share of the gap
+            add(f"fwd {tag} [{M}x{n}x{k}] plain", fl, lambda x=x, w=w, b=b: G.linear(x, w, b),
+                lambda x=x, w=w, b=b: x.float() @ w.float().t() + b, lambda x=x, w=w: x @ w.t())
         else:
             add(f"fwd {tag} [{M}x{n}x{k}]", fl, lambda x=x, w=w, b=b: G.linear(x, w, b),
                 lambda x=x, w=w, b=b: x.float() @ w.float().t() + b, lambda x=x, w=w: x @ w.t())
         dy, wt = r(M, n), w.t().contiguous()
+        if tag in ("qkv", "fc1"):  # DTC_DGRAD_BF16: the input gradient stored bf16
+            add(f"ntdgrad {tag} [{M}x{k}x{n}] bf16", fl, lambda dy=dy, wt=wt: G.linear(dy, wt),
+                lambda dy=dy, w=w: dy.float() @ w.float(), lambda dy=dy, w=w: dy @ w)
+        if tag in ("out", "fc2"):  # DTC_FWD_BF16: the forward stored bf16 + bias
+            add(f"fwd {tag} [{M}x{n}x{k}] bf16+b", fl, lambda x=x, w=w, b=b: G.linear(x, w, b),
+                lambda x=x, w=w, b=b: x.float() @ w.float().t() + b, lambda x=x, w=w: x @ w.t())
         if tag == "fc2":
             u = r(M, k)
             add(f"ntdgrad {tag} [{M}x{k}x{n}] dgelu", fl, lambda dy=dy, wt=wt, u=u: G.matmul_nt_dgelu(dy, wt, u),
