@@ -94,14 +94,14 @@ __device__ __forceinline__ f32x4 dropped_row(const float* __restrict__ dh, long 
   return g;
 }
 
-// grid (pieces, ceil(D/256)), 64 threads x 4 channels
-__global__ void __launch_bounds__(64) embed_piece_sums(const uint32_t* __restrict__ keys, int n, int nb, int piece,
-                                                       const float* __restrict__ dh, float* __restrict__ P, int T,
-                                                       int D, float p, uint32_t seed, const int64_t* __restrict__ step,
-                                                       long row0) {
-  const int d = (blockIdx.y * 64 + threadIdx.x) * 4;
+// block (bx, by) of the (pieces, ceil(D/256)) grid, 64 threads x 4 channels
+__device__ __forceinline__ void embed_piece_sums(int bx, int by, const uint32_t* __restrict__ keys, int n, int nb,
+                                                 int piece, const float* __restrict__ dh, float* __restrict__ P, int T,
+                                                 int D, float p, uint32_t seed, const int64_t* __restrict__ step,
+                                                 long row0) {
+  const int d = (by * 64 + threadIdx.x) * 4;
   if (d >= D) return;
-  const int q_beg = blockIdx.x * piece, q_end = min(n, q_beg + piece);
+  const int q_beg = bx * piece, q_end = min(n, q_beg + piece);
   DTC_ASSERT(q_beg < n && nb >= 1 && nb < 32 && d + 4 <= D);
   const uint32_t tmask = (1u << nb) - 1;
   const uint32_t thr = drop_threshold(p), stp = (uint32_t)step[0];
@@ -171,10 +171,10 @@ __global__ void __launch_bounds__(64) embed_segment_sum(const uint32_t* __restri
   *(f32x4*)o = acc;
 }
 
-__global__ void wpe_bwd_kernel(const float* __restrict__ dh, float* __restrict__ dwpe, int B, int T, int D, float p,
-                               uint32_t seed, const int64_t* __restrict__ step, long row0, int accumulate) {
+__device__ __forceinline__ void wpe_bwd(long i, const float* __restrict__ dh, float* __restrict__ dwpe, int B, int T,
+                                        int D, float p, uint32_t seed, const int64_t* __restrict__ step, long row0,
+                                        int accumulate) {
   const int D4 = D / 4;
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)T * D4) return;
   int t = (int)(i / D4);
   int d = (int)(i % D4) * 4;
@@ -186,6 +186,33 @@ __global__ void wpe_bwd_kernel(const float* __restrict__ dh, float* __restrict__
   float* o = dwpe + (long)t * D + d;
   if (accumulate) acc += *(f32x4*)o;
   *(f32x4*)o = acc;
+}
+
+// The embedding backward's first launch: three independent jobs in one grid of 64-thread blocks, so the
+// latency-bound piece sums run alongside the bandwidth-bound table zeroing instead of after it:
+// [0, nzero) zero the dwte table (EB_ZCH float4 per block; beta = 0 only), then the piece-sum blocks
+// (pieces x dblk), then dwpe (one thread per (t, 4 channels)).  Was three launches, 53 us at GPT-2 small.
+constexpr int EB_ZCH = 64 * 32;
+__global__ void __launch_bounds__(64) embed_bwd_stage1(const uint32_t* __restrict__ keys, int n, int nb, int piece,
+                                                       int npieces, int dblk, const float* __restrict__ dh,
+                                                       float* __restrict__ P, float* __restrict__ dwte, long n4zero,
+                                                       int nzero, float* __restrict__ dwpe, int B, int T, int D,
+                                                       float p, uint32_t seed, const int64_t* __restrict__ step,
+                                                       long row0, int accumulate) {
+  int b = blockIdx.x;
+  if (b < nzero) {
+    f32x4* z = (f32x4*)dwte;
+    const long e0 = (long)b * EB_ZCH, e1 = min(n4zero, e0 + EB_ZCH);
+    for (long e = e0 + threadIdx.x; e < e1; e += 64) z[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  b -= nzero;
+  if (b < npieces * dblk) {
+    embed_piece_sums(b % npieces, b / npieces, keys, n, nb, piece, dh, P, T, D, p, seed, step, row0);
+    return;
+  }
+  b -= npieces * dblk;
+  wpe_bwd((long)b * 64 + threadIdx.x, dh, dwpe, B, T, D, p, seed, step, row0, accumulate);
 }
 
 // ---------------------------------------------------------------- cross-entropy
@@ -568,22 +595,20 @@ int dtc_embed_bwd(const uint32_t* keys, const float* dh, float* dwte, float* dwp
   const int n = B * T;
   if (n > SORT_MAX) return 3003;
   const int nb = dtc_embed_sort_bits(n);
-  if (!accumulate) {  // zero the table with a kernel node (not a memset node) before the row writes
-    long n4 = (long)V * D / 4;
-    hipLaunchKernelGGL(zero4_kernel, dim3(blocks_for(n4, 256)), dim3(256), 0, st, (f32x4*)dwte, n4);
-    DTC_CHECK_LAUNCH();
-  }
   // piece length trades the sequential in-piece sum against the per-id walk over pieces
   const int piece = n <= 4096 ? 16 : (n <= 16384 ? 32 : 64);
   const int dblk = (D / 4 + 63) / 64;
-  hipLaunchKernelGGL(embed_piece_sums, dim3((n + piece - 1) / piece, dblk), dim3(64), 0, st, keys, n, nb, piece, dh, P,
-                     T, D, p, (uint32_t)seed, step, row0);
+  const int npieces = (n + piece - 1) / piece;
+  // zero the table (beta = 0) with kernel blocks (not a memset node) in the same launch as the piece sums
+  const long n4 = accumulate ? 0 : (long)V * D / 4;
+  const long nzero = (n4 + EB_ZCH - 1) / EB_ZCH;
+  const long nwpe = ((long)T * (D / 4) + 63) / 64;
+  const long nblk = nzero + (long)npieces * dblk + nwpe;
+  if (nblk > 0x7fffffffL) return 3004;
+  hipLaunchKernelGGL(embed_bwd_stage1, dim3((unsigned)nblk), dim3(64), 0, st, keys, n, nb, piece, npieces, dblk, dh, P,
+                     dwte, n4, (int)nzero, dwpe, B, T, D, p, (uint32_t)seed, step, row0, accumulate);
   DTC_CHECK_LAUNCH();
   hipLaunchKernelGGL(embed_segment_sum, dim3(n, dblk), dim3(64), 0, st, keys, n, nb, piece, P, dwte, D, accumulate);
-  DTC_CHECK_LAUNCH();
-  long nt = (long)T * (D / 4);
-  hipLaunchKernelGGL(wpe_bwd_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, st, dh, dwpe, B, T, D, p,
-                     (uint32_t)seed, step, row0, accumulate);
   DTC_CHECK_LAUNCH();
   return 0;
 }
