@@ -18,6 +18,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_training_compare_jax_amd.ops import _native as N  # noqa: E402
 from distributed_training_compare_jax_amd.ops import gemm as G  # noqa: E402
 
 
@@ -54,6 +55,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default="")
+    ap.add_argument("--variants", default="", help="comma list of plan variants: n8, n8w3, n8w4")
     ap.add_argument("--cold", action="store_true",
                     help="write a 512 MB buffer before every call (operands come from HBM, as in the step)")
     a = ap.parse_args()
@@ -108,10 +110,21 @@ def main():
             add(f"ntdgrad {tag} [{M}x{k}x{n}] f32", fl, lambda dy=dy, wt=wt: G.linear(dy, wt, out_dtype=torch.float32),
                 lambda dy=dy, w=w: dy.float() @ w.float(), lambda dy=dy, w=w: dy @ w)
 
-    variants = {"ours": None}
+    # plan variants switched in-process: (gemm8n layout mask, gemm8n tile width) -- "n8" = the persistent
+    # 128 x 64CB kernel for multi-round problems too (DTC_GEMM8N bit 4), "n8w4" = with 128 x 256 tiles
+    L = N.lib()
+    variants = {"ours": (3, 0)}
+    for v in [x for x in a.variants.split(",") if x]:
+        variants[v] = {"n8": (7, 0), "n8w3": (7, 3), "n8w4": (7, 4)}[v]
+
+    def use(v):
+        L.dtc_gemm_set_n8(v[0])
+        L.dtc_gemm_set_n8_cb(v[1])
+
     for name, _, fn, ref, _ in cases:
         want = ref().float()
         for vn, v in variants.items():
+            use(v)
             got = fn().float()
             err = ((got - want).norm() / want.norm()).item()
             print(f"check {name:36s} {vn:8s} rel err {err:.2e}", flush=True)
@@ -120,7 +133,9 @@ def main():
     for _ in range(a.rounds):
         for name, _, fn, _, blas in cases:
             for vn, v in variants.items():
+                use(v)
                 res[(name, vn)].append(graph_time(fn, a.reps, pre))
+            use(variants["ours"])
             res[(name, "hipBLASLt")].append(graph_time(blas, a.reps, pre))
     for name, fl, *_ in cases:
         row = []

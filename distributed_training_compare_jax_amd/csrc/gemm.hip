@@ -2569,6 +2569,8 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
 // 256^2 kernels (fc1 forward 75.6 -> 85.6 us: each round pays its own prologue fill and epilogue at
 // one block per CU), and so does a vocab-sized K (the lm_head dgrad keeps its split-K 256^2 kernel).
 static int g_n8_mask = [] { const char* v = getenv("DTC_GEMM8N"); return v ? atoi(v) : 3; }();
+// DTC_N8_CB: only this tile width (3 = 128 x 192, 4 = 128 x 256) for gemm8n plans (0 = 3 then 4; A/B)
+static int g_n8_cb = [] { const char* v = getenv("DTC_N8_CB"); return v ? atoi(v) : 0; }();
 
 static int n8_cb(int layout, int M, int N, int K, int epi) {
   // K >= 1024: at K = 768 (out_proj forward, 12 K-steps) the one-block-per-CU epilogue (fp32 residual
@@ -2577,6 +2579,7 @@ static int n8_cb(int layout, int M, int N, int K, int epi) {
   if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU && epi != EPI_DGELU) return 0;
   const long tm = (M + 127) / 128;
   for (int cb : {3, 4}) {
+    if (g_n8_cb && cb != g_n8_cb) continue;
     const int bn = 64 * cb;
     if (N % bn) continue;
     const long t = tm * (N / bn);
@@ -2902,6 +2905,12 @@ int dtc_gemm_set_wgrad256(int on) {
 int dtc_gemm_set_n8(int mask) {
   const int old = g_n8_mask;
   g_n8_mask = mask;
+  return old;
+}
+
+int dtc_gemm_set_n8_cb(int cb) {
+  const int old = g_n8_cb;
+  g_n8_cb = cb;
   return old;
 }
 
