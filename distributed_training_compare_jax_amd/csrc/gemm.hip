@@ -2528,6 +2528,8 @@ static int cu_count() {
   return n;
 }
 
+static int g_big_cb3 = [] { const char* v = getenv("DTC_BIG_CB3"); return v ? atoi(v) : 0; }();
+
 template <bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   Epi e{};
@@ -2546,10 +2548,27 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, 32 / tiles_n));
   const int kps = big_kps(a.K, split);
   if (split > 1 && (a.ws_bytes < (long)split * a.M * a.N * 4 || a.N % 4)) return 1005;
-  hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
-                     (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split, kps,
-                     (float*)a.workspace, e);
-  DTC_CHECK_LAUNCH();
+  // DTC_BIG_CB3: split-K problems whose 256^2 grid leaves CUs idle (the GPT-2 small lm_head dgrad: 96 tiles
+  // x split 2 = 192 blocks) run 256 x 192 tiles when that grid is exactly one block per CU (128 x 2 = 256)
+  const int cb3 = g_big_cb3;
+  bool done = false;
+  if constexpr (EPI == EPI_STORE && OUTF32) {
+    const int tn3 = a.N / 192;
+    if (cb3 && split > 1 && a.N % 192 == 0 && ntiles * split < cu_count() && tiles_m * tn3 * split == cu_count()) {
+      const int gm3 = std::max(1, std::min(tiles_m, 32 / tn3));
+      hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32, 3>), dim3(tiles_m * tn3 * split), dim3(NT2), 0, st,
+                         (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tn3, gm3, split,
+                         kps, (float*)a.workspace, e);
+      DTC_CHECK_LAUNCH();
+      done = true;
+    }
+  }
+  if (!done) {
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles * split), dim3(NT2), 0, st,
+                       (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, split,
+                       kps, (float*)a.workspace, e);
+    DTC_CHECK_LAUNCH();
+  }
   if (split > 1 && !a.defer_reduce) {
     long MN = (long)a.M * a.N;
     int blocks = (int)((MN / 4 + 255) / 256);
@@ -2905,6 +2924,13 @@ int dtc_gemm_set_wgrad256(int on) {
 int dtc_gemm_set_n8(int mask) {
   const int old = g_n8_mask;
   g_n8_mask = mask;
+  return old;
+}
+
+// 256 x 192 split-K plan of launch_big (DTC_BIG_CB3 at load time); returns the previous value
+int dtc_gemm_set_big_cb3(int on) {
+  const int old = g_big_cb3;
+  g_big_cb3 = on;
   return old;
 }
 

@@ -125,3 +125,24 @@ def test_wgrad_split256(cuda, Nn, K, M):
         outs.append(dw)
     _close(outs[0], outs[1], 1e-4, "split256_vs_default")
 
+
+
+def test_lmhead_dgrad_cb3(cuda):
+    """The lm_head dgrad through the vocabulary (GPT-2 small: M 8192, N 768, K 50304, NT on W^T, split-K
+    fp32 slabs): the 256 x 192 plan (DTC_BIG_CB3, 128 tiles x split 2 = one block per CU) against fp32
+    torch and against the 256^2 plan (96 tiles x split 2)."""
+    L = N.lib()
+    M, Nn, K = 8192, 768, 50304
+    dy, wt = _r(M, K, scale=0.05, seed=21), _r(Nn, K, scale=0.05, seed=22)
+    ref = dy.float() @ wt.float().t()
+    outs = []
+    for on in (1, 0):
+        old = L.dtc_gemm_set_big_cb3(on)
+        try:
+            out = G.linear(dy, wt, out_dtype=torch.float32)
+            torch.cuda.synchronize()
+        finally:
+            L.dtc_gemm_set_big_cb3(old)
+        _close(out, ref, 2e-3, f"lm_head dgrad (cb3={on})")
+        outs.append(out)
+    _close(outs[0], outs[1], 1e-5, "cb3_vs_256")
