@@ -63,6 +63,12 @@ struct WgBatch {
   float beta;
   int ntiles;
   float* sq;  // optional [ntiles][8]: per-tile, per-wave sums of squares of the final dW (grad-norm partials)
+  // tail split (host-set by dtc_wgrad_group when tail_slab is given): the last tail_tiles logical tiles run
+  // as tail_split K-pieces into fp32 tile slabs [tail][split][256][256], finished by wg_tail_reduce
+  // in: tail_split 0 = off, 1 = auto (CUs / tail, 2..4), >= 2 = that many pieces; tail_cap = slab floats
+  int tail_tiles, tail_split;
+  float* tail_slab;
+  long tail_cap;
   WgEntry e[WG_MAX];
 };
 

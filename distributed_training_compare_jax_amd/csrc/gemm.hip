@@ -160,6 +160,7 @@ struct Epi {
   float* colsum;
   int cs_accum;  // colsum IS the bias gradient: colsum[m] = beta*colsum[m] + sum (split == 1 only)
   float* sq;     // gemm8p_tile, fp32 store: per-wave sums of squares of the stored values (8 slots)
+  int slab_tile; // gemm8p_tile split-K: slab = [split][BIG][64 CB] tile-local slabs instead of [split][M][N]
   LnEpi ln;
 };
 
@@ -1344,7 +1345,18 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
       }
     }
   }
-  if (split > 1) {  // fp32 slab z; splitk_reduce sums the slabs in a fixed order
+  if (split > 1) {  // fp32 slab z; splitk_reduce (or wg_tail_reduce) sums the slabs in a fixed order
+    if (e.slab_tile) {  // tile-local [split][BIG][64 CB] slab (grouped weight gradients' tail split)
+      float* sl = slab + (long)z * BIG * (64 * CB);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int r = wr * 128 + j * 16 + (lane & 15), c = wc * WN + i * 16 + g4;
+          if (m0 + r < M && n0 + c < N) *(f32x4*)(sl + (long)r * (64 * CB) + c) = acc[i][j];
+        }
+      return;
+    }
     float* sl = slab + (long)z * M * N;
 #pragma unroll
     for (int i = 0; i < TN; ++i)
@@ -1425,21 +1437,77 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
 // 13.2 ms step); twelve layers together are 1296 whole tiles, ~5 rounds of 256 CUs.
 // Block -> (problem, tile): XCD-remapped logical id, problems back to back, M-tiles fastest (the
 // blocks an XCD runs together share the X panel of one N-tile).
-__global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
-  const int lid = xcd_remap(blockIdx.x, b.ntiles);
+// Tail split (b.tail_tiles > 0): the grid's last blocks are K-pieces of the last tail_tiles logical tiles,
+// so the final, partly filled round of whole tiles (GPT-2 small: 1887 tiles = 7 rounds + 95) becomes
+// tail_split times as many blocks of 1/tail_split the length; wg_tail_reduce finishes those tiles.
+__device__ __forceinline__ const WgEntry& wg_entry(const WgBatch& b, int lid) {
   int i = 0;
   while (i + 1 < b.n && lid >= b.e[i + 1].tile0) ++i;
-  const WgEntry& w = b.e[i];
+  return b.e[i];
+}
+
+__global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
+  const int nmain = b.ntiles - b.tail_tiles;
+  int lid, z = 0;
+  if ((int)blockIdx.x < nmain) {
+    lid = xcd_remap(blockIdx.x, nmain);
+  } else {
+    const int u = blockIdx.x - nmain;
+    lid = nmain + u / b.tail_split;
+    z = u % b.tail_split;
+  }
+  DTC_ASSERT(lid < b.ntiles);
+  const WgEntry& w = wg_entry(b, lid);
   const int t = lid - w.tile0;
   const int tiles_m = (w.M + BIG - 1) / BIG;
   const int tm_idx = t % tiles_m, tn_idx = t / tiles_m;
   DTC_ASSERT(tn_idx * BIG < w.N);
   Epi e{};
   e.M = w.M; e.N = w.N; e.C = w.C; e.ldc = w.N; e.alpha = 1.f; e.beta = b.beta;
+  if (lid >= nmain) {  // K-piece z of a tail tile (no bias column sums there: host-checked)
+    DTC_ASSERT(w.cs == nullptr && b.tail_slab != nullptr);
+    e.slab_tile = 1;
+    const int kps = b.K / b.tail_split;
+    gemm8p_tile<false, false, EPI_STORE, true, 4>(w.A, w.M, w.B, w.N, w.M, w.N, b.K, tm_idx, tn_idx, z, b.tail_split,
+                                                   kps, b.tail_slab + (long)(lid - nmain) * b.tail_split * BIG * BIG, e);
+    return;
+  }
   e.colsum = w.cs; e.cs_accum = 1;
   e.sq = b.sq ? b.sq + (long)lid * (NT2 / 64) : nullptr;  // NT2 / 64 wave slots per tile
   gemm8p_tile<false, false, EPI_STORE, true, 4>(w.A, w.M, w.B, w.N, w.M, w.N, b.K, tm_idx, tn_idx, 0, 1, b.K,
                                                  nullptr, e);
+}
+
+// Finish the tail tiles: dW = beta*dW + sum_z slab[z] (z ascending), and their grad-norm partials (block
+// (tail tile, row group q) of 32 rows writes sq slot q of its tile, the slots the whole tile's waves
+// fill in the main kernel).  Grid (tail_tiles * 8), 256 threads: 32 rows x 64 float4 columns.
+__global__ void __launch_bounds__(256) wg_tail_reduce(WgBatch b) {
+  const int nmain = b.ntiles - b.tail_tiles;
+  const int tt = blockIdx.x / 8, q = blockIdx.x % 8;
+  const int lid = nmain + tt;
+  const WgEntry& w = wg_entry(b, lid);
+  const int t = lid - w.tile0;
+  const int tiles_m = (w.M + BIG - 1) / BIG;
+  const int m0 = (t % tiles_m) * BIG, n0 = (t / tiles_m) * BIG;
+  const float* slab = b.tail_slab + (long)tt * b.tail_split * BIG * BIG;
+  float ss = 0.f;
+  for (int k = threadIdx.x; k < 32 * 64; k += 256) {
+    const int r = q * 32 + k / 64, c = (k % 64) * 4;
+    const int m = m0 + r, n = n0 + c;
+    if (m >= w.M || n >= w.N) continue;
+    f32x4 v = *(const f32x4*)(slab + (long)r * BIG + c);
+    for (int z = 1; z < b.tail_split; ++z) v += *(const f32x4*)(slab + (long)z * BIG * BIG + (long)r * BIG + c);
+    f32x4* dst = (f32x4*)(w.C + (long)m * w.N + n);
+    if (b.beta != 0.f) v += b.beta * *dst;
+    *dst = v;
+    ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  if (!b.sq) return;
+  __shared__ float red[4];
+  ss = warp_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) b.sq[(long)lid * (NT2 / 64) + q] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ============================================================================================
@@ -2944,6 +3012,7 @@ int dtc_gemm_set_n8_cb(int cb) {
 
 int dtc_wg_entry_bytes() { return (int)sizeof(WgEntry); }
 int dtc_wg_max() { return WG_MAX; }
+int dtc_wg_batch_bytes() { return (int)sizeof(WgBatch); }
 
 // Grouped weight gradients (gemm8p_group_kernel).  Host-side checks: K a positive multiple of 64,
 // M and N multiples of 8 (MN-major operand extents), 16-B aligned operands.
@@ -2959,8 +3028,31 @@ int dtc_wgrad_group(const WgBatch* in, hipStream_t st) {
     t += ((w.M + BIG - 1) / BIG) * ((w.N + BIG - 1) / BIG);
   }
   b.ntiles = t;
-  hipLaunchKernelGGL(gemm8p_group_kernel, dim3(t), dim3(NT2), 0, st, b);
+  // tail split: the last (t mod CUs) tiles as K-pieces when every one of them belongs to a problem without
+  // bias column sums, K divides into 64-multiples, and the caller gave a slab big enough
+  int tail = 0, split = 0;
+  const int cus = cu_count();
+  if (in->tail_slab && in->tail_split > 0 && cus > 0 && t > cus) {
+    tail = t % cus;
+    split = in->tail_split > 1 ? in->tail_split : std::max(2, std::min(4, tail > 0 ? cus / tail : 0));
+    bool ok = tail > 0 && b.K % (64 * split) == 0 && (long)tail * split <= 2L * cus &&
+              (long)tail * split * BIG * BIG <= in->tail_cap;
+    for (int i = 0; ok && i < b.n; ++i) {
+      const WgEntry& w = b.e[i];
+      const int end = w.tile0 + ((w.M + BIG - 1) / BIG) * ((w.N + BIG - 1) / BIG);
+      if (end > t - tail && w.cs) ok = false;
+    }
+    if (!ok) tail = split = 0;
+  }
+  b.tail_tiles = tail;
+  b.tail_split = split > 1 ? split : 1;
+  if (!tail) b.tail_slab = nullptr;
+  hipLaunchKernelGGL(gemm8p_group_kernel, dim3(t - tail + tail * b.tail_split), dim3(NT2), 0, st, b);
   DTC_CHECK_LAUNCH();
+  if (tail) {
+    hipLaunchKernelGGL(wg_tail_reduce, dim3(tail * 8), dim3(256), 0, st, b);
+    DTC_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -89,6 +89,7 @@ WG_MAX = 64  # csrc/common.h WG_MAX
 
 class WgBatch(ctypes.Structure):
     _fields_ = [("n", c_int), ("K", c_int), ("beta", c_float), ("ntiles", c_int), ("sq", c_vp),
+                ("tail_tiles", c_int), ("tail_split", c_int), ("tail_slab", c_vp), ("tail_cap", c_long),
                 ("e", WgEntry * WG_MAX)]
 
 
@@ -120,6 +121,7 @@ def _declare(lib):
         "dtc_wgrad_group": ([ctypes.POINTER(WgBatch), vp], i),
         "dtc_wg_entry_bytes": ([], i),
         "dtc_wg_max": ([], i),
+        "dtc_wg_batch_bytes": ([], i),
         "dtc_gemm_pair": ([ctypes.POINTER(GemmArgs), ctypes.POINTER(GemmArgs), vp], i),
         "dtc_gemm_ln": ([ctypes.POINTER(LnArgs), vp], i),
         "dtc_gemm_ln_sync_words": ([i, i], l),

@@ -328,6 +328,19 @@ def wgrad_tiles(m: int, n: int) -> int:
     return ((m + 255) // 256) * ((n + 255) // 256)
 
 
+# DTC_WG_TAIL_SPLIT: the grouped launch's last, partly filled round of whole tiles runs as K-pieces of those
+# tiles (0 off, 1 auto = CUs // tail pieces, clamped to 2..4; >= 2 forced), finished by wg_tail_reduce
+_WG_TAIL = int(__import__("os").environ.get("DTC_WG_TAIL_SPLIT", "0"))
+_CUS = {}
+
+
+def _cu_count(device) -> int:
+    n = _CUS.get(device.index)
+    if n is None:
+        n = _CUS[device.index] = torch.cuda.get_device_properties(device).multi_processor_count
+    return n
+
+
 def wgrad_group(items, beta: float = 0.0, red=None, sq: Optional[torch.Tensor] = None):
     """Weight gradients of several Dense layers that share the token dimension, in ONE launch:
     for every ``(dy, x, dw, db)``: dW = β·dW + dYᵀ·X and (``db`` not None) db = β·db + Σ_rows dY.
@@ -364,9 +377,14 @@ def wgrad_group(items, beta: float = 0.0, red=None, sq: Optional[torch.Tensor] =
     L = N.lib()
     if not _WG_CHECKED[0]:
         assert L.dtc_wg_entry_bytes() == ctypes.sizeof(N.WgEntry) and L.dtc_wg_max() == N.WG_MAX
+        assert L.dtc_wg_batch_bytes() == ctypes.sizeof(N.WgBatch)
         _WG_CHECKED[0] = True
-    # largest problems first: their tiles start in the first rounds, the small ones fill the tail
-    fast.sort(key=lambda it: -(it[0].shape[1] * it[1].shape[1]))
+    # largest problems first: their tiles start in the first rounds, the small ones fill the tail.  With
+    # the tail split the bias-free problems (the lm_head's) go last: the split tail tiles carry no bias sums
+    if _WG_TAIL:
+        fast.sort(key=lambda it: (it[3] is None, -(it[0].shape[1] * it[1].shape[1])))
+    else:
+        fast.sort(key=lambda it: -(it[0].shape[1] * it[1].shape[1]))
     if sq is not None:
         assert sq.dtype == torch.float32 and sq.is_contiguous() and sq.is_cuda
         assert sq.numel() >= WG_SQ_SLOTS * sum(wgrad_tiles(it[0].shape[1], it[1].shape[1]) for it in fast), "sq"
@@ -376,6 +394,14 @@ def wgrad_group(items, beta: float = 0.0, red=None, sq: Optional[torch.Tensor] =
         b = N.WgBatch()
         b.n, b.K, b.beta, b.ntiles = len(chunk), K, float(beta), 0
         b.sq = None if sq is None else sq.data_ptr() + 4 * WG_SQ_SLOTS * off
+        if _WG_TAIL:  # fp32 tile slabs of the split tail (the kernel re-derives tail and split, checks the cap)
+            t = sum(wgrad_tiles(it[0].shape[1], it[1].shape[1]) for it in chunk)
+            cus = _cu_count(dy0.device)
+            tail = t % cus if t > cus else 0
+            split = _WG_TAIL if _WG_TAIL > 1 else max(2, min(4, cus // tail)) if tail else 0
+            nbytes = tail * split * 256 * 256 * 4
+            if nbytes:
+                b.tail_split, b.tail_slab, b.tail_cap = _WG_TAIL, _workspace(dy0.device, nbytes).data_ptr(), nbytes // 4
         for j, (dy, x, dw, db) in enumerate(chunk):
             b.e[j] = N.WgEntry(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N.ptr(db), dy.shape[1], x.shape[1], 0, 0)
             off += wgrad_tiles(dy.shape[1], x.shape[1])

@@ -64,3 +64,35 @@ def test_wgrad_group_lmhead_and_layers(cuda):
         _close(dw, dy.float().t() @ x.float(), 2e-3, f"problem {k}")
         if db is not None:
             _close(db, dy.float().sum(0), 2e-3, f"bias {k}")
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_wgrad_group_tail_split(cuda, monkeypatch, beta):
+    """DTC_WG_TAIL_SPLIT: the step's group (1887 tiles = 7 rounds + 95 on 256 CUs) with its last 95 tiles --
+    the bias-free lm_head's, sorted last -- as 2 K-pieces each, finished by wg_tail_reduce: dW against fp32
+    torch and against the unsplit launch, bias sums unchanged, and the per-tile grad-norm partials still sum
+    to sum(dW^2) over every problem."""
+    K = 8192
+    shapes = [(768, 3072), (3072, 768), (768, 768), (2304, 768)] * 12 + [(50304, 768)]
+    xs = {Nn: _r(K, Nn, seed=Nn) for Nn in (768, 3072)}
+    dys = {M: _r(K, M, seed=M + 1) for M in (768, 3072, 2304, 50304)}
+    tiles = sum(G.wgrad_tiles(M, Nn) for M, Nn in shapes)
+    out = {}
+    for tail in (1, 0):
+        monkeypatch.setattr(G, "_WG_TAIL", tail)
+        items = [(dys[M], xs[Nn], _r(M, Nn, seed=5, dtype=torch.float32),
+                  _r(M, seed=6, dtype=torch.float32) if M != 50304 else None) for (M, Nn) in shapes]
+        start = [(dw.clone(), None if db is None else db.clone()) for _, _, dw, db in items]
+        sq = torch.zeros(G.WG_SQ_SLOTS * tiles, device="cuda")
+        G.wgrad_group(items, beta, sq=sq)
+        torch.cuda.synchronize()
+        total = sum((dw.double() ** 2).sum().item() for _, _, dw, _ in items)
+        assert sq.double().sum().item() == pytest.approx(total, rel=1e-5), tail
+        for k in (0, 3, 47, 48):
+            dy, x, dw, db = items[k]
+            _close(dw, beta * start[k][0] + dy.float().t() @ x.float(), 2e-3, f"tail={tail} problem {k}")
+            if db is not None:
+                _close(db, beta * start[k][1] + dy.float().sum(0), 2e-3, f"tail={tail} bias {k}")
+        out[tail] = [dw for _, _, dw, _ in items]
+    for a, b in zip(out[1], out[0]):
+        _close(a, b, 1e-5, "tail split vs whole tiles")
