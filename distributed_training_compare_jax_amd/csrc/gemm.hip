@@ -1491,17 +1491,39 @@ __global__ void __launch_bounds__(256) wg_tail_reduce(WgBatch b) {
   const int m0 = (t % tiles_m) * BIG, n0 = (t / tiles_m) * BIG;
   const float* slab = b.tail_slab + (long)tt * b.tail_split * BIG * BIG;
   float ss = 0.f;
-  for (int k = threadIdx.x; k < 32 * 64; k += 256) {
+  constexpr int IT = 32 * 64 / 256;  // float4 per thread, all loads of a slab issued before any add
+  bool ok[IT];
+  long so[IT], co[IT];
+  f32x4 v[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int k = threadIdx.x + 256 * i;
     const int r = q * 32 + k / 64, c = (k % 64) * 4;
-    const int m = m0 + r, n = n0 + c;
-    if (m >= w.M || n >= w.N) continue;
-    f32x4 v = *(const f32x4*)(slab + (long)r * BIG + c);
-    for (int z = 1; z < b.tail_split; ++z) v += *(const f32x4*)(slab + (long)z * BIG * BIG + (long)r * BIG + c);
-    f32x4* dst = (f32x4*)(w.C + (long)m * w.N + n);
-    if (b.beta != 0.f) v += b.beta * *dst;
-    *dst = v;
-    ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    ok[i] = m0 + r < w.M && n0 + c < w.N;
+    so[i] = (long)r * BIG + c;
+    co[i] = (long)(m0 + r) * w.N + n0 + c;
+    v[i] = ok[i] ? *(const f32x4*)(slab + so[i]) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  for (int z = 1; z < b.tail_split; ++z) {
+    f32x4 u[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) u[i] = ok[i] ? *(const f32x4*)(slab + (long)z * BIG * BIG + so[i]) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < IT; ++i) v[i] += u[i];
+  }
+  if (b.beta != 0.f) {
+    f32x4 u[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) u[i] = ok[i] ? *(const f32x4*)(w.C + co[i]) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < IT; ++i) v[i] += b.beta * u[i];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+    if (ok[i]) {
+      *(f32x4*)(w.C + co[i]) = v[i];
+      ss += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+    }
   if (!b.sq) return;
   __shared__ float red[4];
   ss = warp_sum(ss);
