@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default="")
-    ap.add_argument("--variants", default="", help="comma list of plan variants: n8, n8w3, n8w4")
+    ap.add_argument("--variants", default="", help="comma list of plan variants: n8, n8w3, n8w4, n8k768")
     ap.add_argument("--cold", action="store_true",
                     help="write a 512 MB buffer before every call (operands come from HBM, as in the step)")
     a = ap.parse_args()
@@ -113,13 +113,15 @@ def main():
     # plan variants switched in-process: (gemm8n layout mask, gemm8n tile width) -- "n8" = the persistent
     # 128 x 64CB kernel for multi-round problems too (DTC_GEMM8N bit 4), "n8w4" = with 128 x 256 tiles
     L = N.lib()
-    variants = {"ours": (3, 0)}
+    # "n8k768": one-round gemm8n problems down to K = 768 (the out_proj forward / dgrad)
+    variants = {"ours": (3, 0, 1024)}
     for v in [x for x in a.variants.split(",") if x]:
-        variants[v] = {"n8": (7, 0), "n8w3": (7, 3), "n8w4": (7, 4)}[v]
+        variants[v] = {"n8": (7, 0, 1024), "n8w3": (7, 3, 1024), "n8w4": (7, 4, 1024), "n8k768": (3, 0, 768)}[v]
 
     def use(v):
         L.dtc_gemm_set_n8(v[0])
         L.dtc_gemm_set_n8_cb(v[1])
+        L.dtc_gemm_set_n8_mink(v[2])
 
     for name, _, fn, ref, _ in cases:
         want = ref().float()

@@ -2778,6 +2778,10 @@ static int g_n8_mask = [] { const char* v = getenv("DTC_GEMM8N"); return v ? ato
 // DTC_N8_CB: only this tile width (3 = 128 x 192, 4 = 128 x 256) for gemm8n plans (0 = 3 then 4; A/B)
 static int g_n8_cb = [] { const char* v = getenv("DTC_N8_CB"); return v ? atoi(v) : 0; }();
 
+// DTC_N8_MINK: smallest K of a one-round gemm8n problem (default 1024; 768 = also the out_proj forward /
+// dgrad, whose plain stores take the overlapped epilogue since the residual add moved to the LayerNorm)
+static int g_n8_mink = [] { const char* v = getenv("DTC_N8_MINK"); return v ? atoi(v) : 1024; }();
+
 static int n8_cb(int layout, int M, int N, int K, int epi) {
   // K >= 1024: at K = 768 (out_proj forward, 12 K-steps) the one-block-per-CU epilogue (fp32 residual
   // in + out, nothing to hide it under) costs more than the main loop gains (29.2 vs 26.6 us)
@@ -2789,7 +2793,7 @@ static int n8_cb(int layout, int M, int N, int K, int epi) {
     const int bn = 64 * cb;
     if (N % bn) continue;
     const long t = tm * (N / bn);
-    if ((t == 256 && K >= 1024) || ((g_n8_mask & 4) && t > 256 && t % 256 == 0)) return cb;
+    if ((t == 256 && K >= g_n8_mink) || ((g_n8_mask & 4) && t > 256 && t % 256 == 0)) return cb;
   }
   return 0;
 }
@@ -3123,6 +3127,12 @@ int dtc_gemm_set_n8(int mask) {
 int dtc_gemm_set_big_cb3(int on) {
   const int old = g_big_cb3;
   g_big_cb3 = on;
+  return old;
+}
+
+int dtc_gemm_set_n8_mink(int k) {
+  const int old = g_n8_mink;
+  g_n8_mink = k;
   return old;
 }
 
