@@ -2685,6 +2685,7 @@ static int cu_count() {
 // default on: GPT-2 small lm_head dgrad 553 -> 502 us, step 11.01-11.04 vs 11.04-11.09 ms
 // (profiles/r4_ab_big_cb3.log)
 static int g_big_cb3 = [] { const char* v = getenv("DTC_BIG_CB3"); return v ? atoi(v) : 1; }();
+static int g_big_cb3_fwd = [] { const char* v = getenv("DTC_BIG_CB3_FWD"); return v ? atoi(v) : 0; }();
 // DTC_BIG_TAIL_SPLIT: whole-tile gemm8p launches (bf16 + bias store) whose last round is <= 1/4 full run
 // those tiles as K-pieces (gemm8p_tail_kernel + big_tail_finish)
 static int g_big_tail = [] { const char* v = getenv("DTC_BIG_TAIL_SPLIT"); return v ? atoi(v) : 0; }();
@@ -2748,6 +2749,22 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
                          kps, (float*)a.workspace, e);
       DTC_CHECK_LAUNCH();
       done = true;
+    }
+  }
+  // DTC_BIG_CB3_FWD: whole-tile bf16 + bias forwards on 256 x 192 tiles when that quantises into fewer
+  // tile-times (each 0.75 of a 256^2 tile): GPT-2 small qkv, 288 tiles = 2 rounds -> 384 = 1.5 rounds
+  if constexpr (EPI == EPI_STORE && !OUTF32) {
+    const int cus = cu_count();
+    if (g_big_cb3_fwd && split == 1 && a.N % 192 == 0 && cus > 0) {
+      const int tn3 = a.N / 192;
+      const long r4 = (ntiles + cus - 1) / cus, t3 = (long)tiles_m * tn3, r3 = (t3 + cus - 1) / cus;
+      if (4 * r4 > 3 * r3 + 1) {  // 0.75 r3 < r4 tile times (strictly, with margin)
+        const int gm3 = std::max(1, std::min(tiles_m, 32 / tn3));
+        hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32, 3>), dim3(t3), dim3(NT2), 0, st, (const bf16*)a.A,
+                           a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tn3, gm3, 1, kps, nullptr, e);
+        DTC_CHECK_LAUNCH();
+        done = true;
+      }
     }
   }
   if (!done) {
@@ -3133,6 +3150,12 @@ int dtc_gemm_set_big_cb3(int on) {
 int dtc_gemm_set_n8_mink(int k) {
   const int old = g_n8_mink;
   g_n8_mink = k;
+  return old;
+}
+
+int dtc_gemm_set_big_cb3_fwd(int on) {
+  const int old = g_big_cb3_fwd;
+  g_big_cb3_fwd = on;
   return old;
 }
 

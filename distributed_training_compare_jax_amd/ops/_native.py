@@ -118,6 +118,7 @@ def _declare(lib):
         "dtc_gemm_set_n8_cb": ([i], i),
         "dtc_gemm_set_big_cb3": ([i], i),
         "dtc_gemm_set_big_tail": ([i], i),
+        "dtc_gemm_set_big_cb3_fwd": ([i], i),
         "dtc_gemm_set_n8_mink": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
         "dtc_wgrad_group": ([ctypes.POINTER(WgBatch), vp], i),

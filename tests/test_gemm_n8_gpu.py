@@ -169,3 +169,25 @@ def test_big_tail_split(cuda, M, Nn, K):
         _close(out, ref, 1e-2, f"qkv forward (tail={on})")
         outs.append(out)
     _close(outs[0], outs[1], 1e-2, "tail_vs_whole")
+
+
+@pytest.mark.parametrize("M,Nn,K", [(8192, 2304, 768), (8100, 2304, 768)])
+def test_big_cb3_forward(cuda, M, Nn, K):
+    """Whole-tile bf16 + bias forward on 256 x 192 tiles (DTC_BIG_CB3_FWD: the GPT-2 small qkv forward,
+    288 256^2 tiles = 2 rounds -> 384 = 1.5 rounds of 0.75-size tiles) against fp32 torch and the 256^2
+    launch."""
+    L = N.lib()
+    x, w = _r(M, K, seed=41), _r(Nn, K, scale=0.05, seed=42)
+    b = torch.randn(Nn, device="cuda") * 0.1
+    ref = x.float() @ w.float().t() + b
+    outs = []
+    for on in (1, 0):
+        old = L.dtc_gemm_set_big_cb3_fwd(on)
+        try:
+            out = G.linear(x, w, b)
+            torch.cuda.synchronize()
+        finally:
+            L.dtc_gemm_set_big_cb3_fwd(old)
+        _close(out, ref, 1e-2, f"qkv forward (cb3={on})")
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])  # same k order per output element, same rounding
