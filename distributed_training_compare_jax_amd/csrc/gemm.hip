@@ -3136,7 +3136,6 @@ int dtc_gemm_set_wgrad256(int on) {
   return old;
 }
 
-// 256 x 192 gemm8p plans (DTC_GEMM8P3 at load time); returns the previous value
 // gemm8n layout mask (DTC_GEMM8N at load time); returns the previous mask (tests / A/B)
 int dtc_gemm_set_n8(int mask) {
   const int old = g_n8_mask;
