@@ -88,7 +88,7 @@ struct RedTask {
   float beta;
   float weight;
 };
-constexpr int RED_MAX_TASKS = 24;
+constexpr int RED_MAX_TASKS = 48;  // RedBatch is a kernel argument: 8 + 48 x 64 B < 4 KB
 struct RedBatch {
   int ntasks;
   int nblocks;

@@ -45,7 +45,7 @@ class RedTask(ctypes.Structure):
     ]
 
 
-MAX_TASKS = 24  # RED_MAX_TASKS
+MAX_TASKS = 48  # RED_MAX_TASKS
 
 
 class RedBatch(ctypes.Structure):
