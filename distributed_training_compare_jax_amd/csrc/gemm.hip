@@ -755,7 +755,7 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
   bf16* const s1 = smem + BUF;
   // dGELU epilogue operand u (bf16, the fragment layout): loaded before the main loop so its
   // latency hides under the MFMAs instead of stalling the epilogue (measured +8.6 us at fc2 dgrad)
-  constexpr bool PRE_U = (EPI == EPI_DGELU) && (WN == 64);
+  constexpr bool PRE_U = (EPI == EPI_DGELU || EPI == EPI_DELTA) && (WN == 64);
   bf16x4 upre[PRE_U ? TN : 1][PRE_U ? TM : 1];
   if constexpr (PRE_U) {
     const int g4p = 4 * (lane >> 4);
@@ -772,8 +772,8 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
 #ifndef DTC_STAGE_STORE
 #define DTC_STAGE_STORE 1  // plain bf16 stores through the LDS stage too
 #endif
-  constexpr bool STAGED = (EPI == EPI_GELU || EPI == EPI_DGELU || (DTC_STAGE_STORE && EPI == EPI_STORE)) && !OUTF32 &&
-                          WN == 64;
+  constexpr bool STAGED = (EPI == EPI_GELU || EPI == EPI_DGELU || EPI == EPI_DELTA || (DTC_STAGE_STORE && EPI == EPI_STORE)) &&
+                          !OUTF32 && WN == 64;
 #ifndef DTC_STAGE_F32
 #define DTC_STAGE_F32 1  // fp32 outputs and split-K slabs through an fp32 LDS stage
 #endif
@@ -954,6 +954,9 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
     bf16* stg = smem + wave * (WM * 64);
     const int mb = m0 + wm * WM, nb = n0 + wn * WN;
     const f32x4(&bb)[TN] = bpre;
+    float dsum[EPI == EPI_DELTA ? TM : 1];  // EPI_DELTA: this lane's share of sum_d dO*O per fragment row
+#pragma unroll
+    for (int j = 0; j < (EPI == EPI_DELTA ? TM : 1); ++j) dsum[j] = 0.f;
 #pragma unroll
     for (int pass = 0; pass < (EPI == EPI_GELU ? 2 : 1); ++pass) {
 #pragma unroll
@@ -971,12 +974,26 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
             }
             if constexpr (EPI == EPI_DGELU) v *= (float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r];
             ob[r] = f2bf(v);
+            // the stored (bf16) dO times O, as the separate delta pass computes it
+            if constexpr (EPI == EPI_DELTA) dsum[j] += (float)ob[r] * (float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r];
           }
           stage_put(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
         }
       // GELU pass 0 = gelu'(u), read only in the backward: non-temporal
       if (EPI == EPI_GELU && pass == 0) stage_out<WM, true>(stg, (bf16*)e.C, e.ldc, mb, nb, M, N, lane);
+      else if constexpr (EPI == EPI_DELTA) stage_out<WM>(stg, (bf16*)e.C, e.ldc, mb, nb, M, N, lane);
       else stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
+    }
+    if constexpr (EPI == EPI_DELTA) {  // the wave's 64 columns are one head: sum the 4 lane groups of a row
+      const int T = e.vocab_start, H = N / 64, h = nb / 64;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        float d = dsum[j];
+        d += __shfl_xor(d, 16, 64);
+        d += __shfl_xor(d, 32, 64);
+        const int m = mb + j * 16 + (lane & 15);
+        if (lane < 16 && m < M) ((float*)e.aux_out)[((long)(m / T) * H + h) * T + m % T] = d;
+      }
     }
     return;
   }
@@ -3226,6 +3243,14 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
+  if (epi == EPI_DELTA) {  // the attention's out_proj dgrad (NT on W^T) + delta, on 128^2 tiles (64-column waves)
+    if (a->layout != 0 || f32 || a->N % 64 || !a->aux || !a->aux_out || a->ldaux % 4 || a->vocab_start <= 0 ||
+        a->M % a->vocab_start || a->alpha != 1.f || a->beta != 0.f)
+      return 1010;
+    Plan p = make_plan(a->M, a->N, a->K, 0);
+    if (p.bm != 128 || p.bk != 64 || p.split != 1 || (gemm_dma_mask() & 4)) return 1011;  // gemm_kernel's epilogue only
+    return launch_t<128, 128, true, true, EPI_DELTA, false>(*a, p, st);
+  }
   if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f) {
     const int cb = n8_cb(a->layout, a->M, a->N, a->K, epi);
     if (cb) {

@@ -78,6 +78,9 @@ _FWD_BF16 = _os.environ.get("DTC_FWD_BF16", "0") == "1"
 # batched reduce launch per 48 tasks for the whole group) instead of one reduce launch per layer: GPT-2 small
 # 10.90 vs 10.97 ms/step (profiles/r4_ab_red_batch.log)
 _RED_BATCH_LAYERS = _os.environ.get("DTC_RED_BATCH_LAYERS", "1") == "1"
+# the out_proj dgrad's epilogue computes the attention backward's delta = rowsum(dO·O) (EPI_DELTA), so the
+# backward skips its delta pass (head_dim 64, the 128^2 NT plan)
+_DELTA_EPI = _os.environ.get("DTC_DELTA_EPI", "0") == "1"
 if _CE_CHUNK < 0 or _CE_CHUNK % 256:
     # chunk offsets feed 16-byte vector loads of w[c0:], wt[:, c0:] and gw[c0:]: a ragged offset would
     # surface as an opaque native error deep in the backward
@@ -418,7 +421,16 @@ class GPTStage:
                 dy2 = self._tp_reduce(self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False))
                 dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
             wto = f.wt(p + "out.w")
-            if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
+            delta = None
+            if wto is not None and _DELTA_EPI and self.cfg.head_dim == 64:
+                # NT dgrad whose epilogue also emits the attention backward's delta = rowsum(dO·O)
+                res = G.linear_delta(dx2_c, wto, o, T, self.heads_local)
+                if res is not None:
+                    do, delta = res
+                    self._wg(dx2_c, o, p + "out")
+            if delta is not None:
+                pass
+            elif wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
                 do = G.linear(dx2_c, wto)
                 self._wg(dx2_c, o, p + "out")
             elif self._defer_wg:
@@ -428,7 +440,7 @@ class GPTStage:
                 do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
                                        out_dtype=self.act_dtype, pair=False)
             dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
-                              self.heads_local).view(batch * T, -1)
+                              self.heads_local, delta=delta).view(batch * T, -1)
             wtq = f.wt(p + "qkv.w")
             if self._fuse_bwd and wtq is not None:
                 bg = self._prev_fc2b(l)

@@ -98,6 +98,7 @@ EPI_RESID = 1       # C(f32) = aux(f32) + acc + bias
 EPI_GELU = 2        # u = acc+bias: C(bf16) = gelu_tanh'(u) ; aux_out(bf16) = gelu_tanh(u)
 EPI_DGELU = 3       # C(bf16) = acc * aux   (aux = gelu_tanh'(u) from EPI_GELU)
 EPI_LMHEAD = 4      # C(bf16) = acc+bias, pad cols -inf; per-row partial (max,sumexp); label logit
+EPI_DELTA = 7       # C(bf16) = acc (= dO) and aux_out(f32)[b,h,t] = sum_d dO*O (aux = O), vocab_start = T
 
 
 def _declare(lib):
