@@ -224,43 +224,45 @@ __global__ void __launch_bounds__(64) embed_bwd_stage1(const uint32_t* __restric
 // pairs (one 128-B line) per partial — the one-wave-per-row mapping read 8 B per line.  Two passes
 // (row max, then the rescaled sum), each combined over the 16 lanes in fixed order.
 constexpr int CC_ROWS = 16, CC_LANES = 16;
-// One pass (online max / sum-exp per thread, then a max-rescaled merge of the CC_LANES partial pairs of a
-// row): the partial array is read once (was a max pass and a sum pass, 20.7 us at GPT-2 small).
-// Partials with no mass (q[1] == 0) are skipped.
 __global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__ part, int M, int P, long srow, long spart,
                                                        float* __restrict__ lse_out, float* __restrict__ rowstat) {
   const int r = threadIdx.x % CC_ROWS, pl = threadIdx.x / CC_ROWS;
   const int row = blockIdx.x * CC_ROWS + r;
   DTC_ASSERT(P >= 1 && pl < CC_LANES && (long)blockIdx.x * CC_ROWS < M);
-  __shared__ float rm[CC_LANES][CC_ROWS], rs[CC_LANES][CC_ROWS];
-  float mx = -INFINITY, s = 0.f;
+  __shared__ float red[CC_LANES][CC_ROWS];
+  __shared__ float rmax[CC_ROWS];
+  float mx = -INFINITY;
+  if (row < M) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += CC_LANES) mx = fmaxf(mx, part[(row * srow + p * spart) * 2]);
+  }
+  red[pl][r] = mx;
+  __syncthreads();
+  if (pl == 0) {
+    float m = red[0][r];
+#pragma unroll
+    for (int q = 1; q < CC_LANES; ++q) m = fmaxf(m, red[q][r]);
+    rmax[r] = m;
+  }
+  __syncthreads();
+  mx = rmax[r];
+  float s = 0.f;
   if (row < M) {
 #pragma unroll 4
     for (int p = pl; p < P; p += CC_LANES) {
       const f32x2 q = *(const f32x2*)(part + (row * srow + p * spart) * 2);
-      if (q[1] > 0.f) {
-        if (q[0] > mx) {
-          s = s * __expf(mx - q[0]) + q[1];
-          mx = q[0];
-        } else {
-          s += q[1] * __expf(q[0] - mx);
-        }
-      }
+      if (q[1] > 0.f) s += q[1] * __expf(q[0] - mx);
     }
   }
-  rm[pl][r] = mx;
-  rs[pl][r] = s;
+  __syncthreads();
+  red[pl][r] = s;
   __syncthreads();
   if (pl == 0 && row < M) {
-    float m = rm[0][r];
-#pragma unroll
-    for (int q = 1; q < CC_LANES; ++q) m = fmaxf(m, rm[q][r]);
     float t = 0.f;
 #pragma unroll
-    for (int q = 0; q < CC_LANES; ++q)
-      if (rs[q][r] > 0.f) t += rs[q][r] * __expf(rm[q][r] - m);
-    if (lse_out) lse_out[row] = m + __logf(t);
-    if (rowstat) { rowstat[2 * row] = m; rowstat[2 * row + 1] = t; }
+    for (int q = 0; q < CC_LANES; ++q) t += red[q][r];
+    if (lse_out) lse_out[row] = mx + __logf(t);
+    if (rowstat) { rowstat[2 * row] = mx; rowstat[2 * row + 1] = t; }
   }
 }
 
