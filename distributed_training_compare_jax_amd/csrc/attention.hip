@@ -1943,8 +1943,7 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
       static const int bwd_merged = [] { const char* v = getenv("DTC_ATTN_BWD_MERGED"); return v ? atoi(v) : 1; }();
       if (bwd_merged || (flags & 8)) {
         allow_lds(attn_bwd_merged32_kernel<64>, lb);
-        // flags bit 4: ws already holds delta (the out_proj dgrad's EPI_DELTA epilogue computed it)
-        if (!(flags & 16)) launch_attn_delta<64>(o, dout, ws, B, T, H, st);
+        launch_attn_delta<64>(o, dout, ws, B, T, H, st);
         hipLaunchKernelGGL(attn_bwd_merged32_kernel<64>, dim3(2 * g32.x), dim3(FW_THREADS), lb, st, qkv, dout, lse, ws,
                            dqkv, B, T, H, scale, (int)g32.x);
       } else {

@@ -98,8 +98,6 @@ struct RedBatch {
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_DGELU = 3, EPI_LMHEAD = 4,
        EPI_RESID_LN = 5,  // x = resid + acc + bias (fp32 C) and y = LayerNorm(x) (bf16) + row mean/rstd
        EPI_LN_BWD = 6,    // acc = dy: C = dres + LayerNorm'(dy) (fp32) + bf16 copy + dgamma/dbeta/dbias partials
-       EPI_DELTA = 7,     // C (bf16) = acc (+bias) = dO, and the attention backward's delta[b][h][t] = sum_d dO*O
-                          // with O = aux (bf16, ldaux), delta = aux_out (fp32), T = vocab_start, head_dim 64
        EPI_NONE = 99 /* microbench: no store */ };
 
 // Mirror of ops/_native.py LnArgs (keep field order and types identical): a layer GEMM with the

@@ -755,7 +755,7 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
   bf16* const s1 = smem + BUF;
   // dGELU epilogue operand u (bf16, the fragment layout): loaded before the main loop so its
   // latency hides under the MFMAs instead of stalling the epilogue (measured +8.6 us at fc2 dgrad)
-  constexpr bool PRE_U = (EPI == EPI_DGELU || EPI == EPI_DELTA) && (WN == 64);
+  constexpr bool PRE_U = (EPI == EPI_DGELU) && (WN == 64);
   bf16x4 upre[PRE_U ? TN : 1][PRE_U ? TM : 1];
   if constexpr (PRE_U) {
     const int g4p = 4 * (lane >> 4);
@@ -772,8 +772,8 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
 #ifndef DTC_STAGE_STORE
 #define DTC_STAGE_STORE 1  // plain bf16 stores through the LDS stage too
 #endif
-  constexpr bool STAGED = (EPI == EPI_GELU || EPI == EPI_DGELU || EPI == EPI_DELTA || (DTC_STAGE_STORE && EPI == EPI_STORE)) &&
-                          !OUTF32 && WN == 64;
+  constexpr bool STAGED = (EPI == EPI_GELU || EPI == EPI_DGELU || (DTC_STAGE_STORE && EPI == EPI_STORE)) && !OUTF32 &&
+                          WN == 64;
 #ifndef DTC_STAGE_F32
 #define DTC_STAGE_F32 1  // fp32 outputs and split-K slabs through an fp32 LDS stage
 #endif
@@ -954,9 +954,6 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
     bf16* stg = smem + wave * (WM * 64);
     const int mb = m0 + wm * WM, nb = n0 + wn * WN;
     const f32x4(&bb)[TN] = bpre;
-    float dsum[EPI == EPI_DELTA ? TM : 1];  // EPI_DELTA: this lane's share of sum_d dO*O per fragment row
-#pragma unroll
-    for (int j = 0; j < (EPI == EPI_DELTA ? TM : 1); ++j) dsum[j] = 0.f;
 #pragma unroll
     for (int pass = 0; pass < (EPI == EPI_GELU ? 2 : 1); ++pass) {
 #pragma unroll
@@ -974,26 +971,12 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
             }
             if constexpr (EPI == EPI_DGELU) v *= (float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r];
             ob[r] = f2bf(v);
-            // the stored (bf16) dO times O, as the separate delta pass computes it
-            if constexpr (EPI == EPI_DELTA) dsum[j] += (float)ob[r] * (float)upre[PRE_U ? i : 0][PRE_U ? j : 0][r];
           }
           stage_put(stg, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
         }
       // GELU pass 0 = gelu'(u), read only in the backward: non-temporal
       if (EPI == EPI_GELU && pass == 0) stage_out<WM, true>(stg, (bf16*)e.C, e.ldc, mb, nb, M, N, lane);
-      else if constexpr (EPI == EPI_DELTA) stage_out<WM>(stg, (bf16*)e.C, e.ldc, mb, nb, M, N, lane);
       else stage_out<WM>(stg, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
-    }
-    if constexpr (EPI == EPI_DELTA) {  // the wave's 64 columns are one head: sum the 4 lane groups of a row
-      const int T = e.vocab_start, H = N / 64, h = nb / 64;
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        float d = dsum[j];
-        d += __shfl_xor(d, 16, 64);
-        d += __shfl_xor(d, 32, 64);
-        const int m = mb + j * 16 + (lane & 15);
-        if (lane < 16 && m < M) ((float*)e.aux_out)[((long)(m / T) * H + h) * T + m % T] = d;
-      }
     }
     return;
   }
@@ -1444,70 +1427,6 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   const int gm_eff = min(gm, tiles_m - grp * gm);
   const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
   gemm8p_tile<AK, BKM, EPI, OUTF32, CB>(A, lda, B, ldb, M, N, K, tm_idx, tn_idx, z, split, k_per_split, slab, e);
-}
-
-// Whole-tile gemm8p launch whose last round is nearly empty (GPT-2 small qkv forward: 288 tiles = one
-// round + 32 on 256 CUs, i.e. two tile times): the last `tail` tiles run as `tsplit` K-pieces into fp32
-// tile slabs (same kernel instantiation, split path), big_tail_finish adds them + bias -> bf16 C.
-__device__ __forceinline__ void p8_tile_coords(int tile, int tiles_m, int tiles_n, int gm, int& tm_idx, int& tn_idx) {
-  const int grp = tile / (gm * tiles_n), in_g = tile % (gm * tiles_n);
-  const int gm_eff = min(gm, tiles_m - grp * gm);
-  tm_idx = grp * gm + in_g % gm_eff;
-  tn_idx = in_g / gm_eff;
-}
-
-template <bool AK, bool BKM, int EPI, bool OUTF32>
-__global__ void __launch_bounds__(NT2, 1)
-gemm8p_tail_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
-                   int tiles_m, int tiles_n, int gm, int tail, int tsplit, float* __restrict__ tslab, Epi e) {
-  const int nmain = tiles_m * tiles_n - tail;
-  int tile, z = 0;
-  if ((int)blockIdx.x < nmain) {
-    tile = xcd_remap(blockIdx.x, nmain);
-  } else {
-    const int u = blockIdx.x - nmain;
-    tile = nmain + u / tsplit;
-    z = u % tsplit;
-  }
-  int tm_idx, tn_idx;
-  p8_tile_coords(tile, tiles_m, tiles_n, gm, tm_idx, tn_idx);
-  if (tile >= nmain) {
-    e.slab_tile = 1;
-    gemm8p_tile<AK, BKM, EPI, OUTF32, 4>(A, lda, B, ldb, M, N, K, tm_idx, tn_idx, z, tsplit, K / tsplit,
-                                         tslab + (long)(tile - nmain) * tsplit * BIG * BIG, e);
-    return;
-  }
-  gemm8p_tile<AK, BKM, EPI, OUTF32, 4>(A, lda, B, ldb, M, N, K, tm_idx, tn_idx, 0, 1, K, nullptr, e);
-}
-
-// C (bf16) = sum_z slab[z] (z ascending) + bias for the tail tiles; grid tail * 8 (32 rows each), 256 threads
-__global__ void __launch_bounds__(256) big_tail_finish(int M, int N, int tiles_m, int tiles_n, int gm, int tail,
-                                                       int tsplit, const float* __restrict__ tslab,
-                                                       bf16* __restrict__ C, long ldc, const float* __restrict__ bias) {
-  const int tt = blockIdx.x / 8, q = blockIdx.x % 8;
-  const int tile = tiles_m * tiles_n - tail + tt;
-  int tm_idx, tn_idx;
-  p8_tile_coords(tile, tiles_m, tiles_n, gm, tm_idx, tn_idx);
-  const int m0 = tm_idx * BIG, n0 = tn_idx * BIG;
-  const float* slab = tslab + (long)tt * tsplit * BIG * BIG;
-  constexpr int IT = 32 * 64 / 256;
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int k = threadIdx.x + 256 * i;
-    const int r = q * 32 + k / 64, c = (k % 64) * 4;
-    const int m = m0 + r, n = n0 + c;
-    if (m >= M || n >= N) continue;
-    f32x4 v = *(const f32x4*)(slab + (long)r * BIG + c);
-    for (int z = 1; z < tsplit; ++z) v += *(const f32x4*)(slab + (long)z * BIG * BIG + (long)r * BIG + c);
-    bf16x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j] + (bias && n + j < N ? bias[n + j] : 0.f));
-    if (n + 4 <= N) {
-      *(bf16x4*)(C + (long)m * ldc + n) = o;
-    } else {
-      for (int j = 0; j < 4 && n + j < N; ++j) C[(long)m * ldc + n + j] = o[j];
-    }
-  }
 }
 
 // Grouped weight gradients: dW_i = beta*dW_i + dY_i^T X_i (+ db_i = beta*db_i + colsum(dY_i)) for up to
@@ -2706,25 +2625,6 @@ static int cu_count() {
 // default on: GPT-2 small lm_head dgrad 553 -> 502 us, step 11.01-11.04 vs 11.04-11.09 ms
 // (profiles/r4_ab_big_cb3.log)
 static int g_big_cb3 = [] { const char* v = getenv("DTC_BIG_CB3"); return v ? atoi(v) : 1; }();
-static int g_big_cb3_fwd = [] { const char* v = getenv("DTC_BIG_CB3_FWD"); return v ? atoi(v) : 0; }();
-// DTC_BIG_TAIL_SPLIT: whole-tile gemm8p launches (bf16 + bias store) whose last round is <= 1/4 full run
-// those tiles as K-pieces (gemm8p_tail_kernel + big_tail_finish)
-static int g_big_tail = [] { const char* v = getenv("DTC_BIG_TAIL_SPLIT"); return v ? atoi(v) : 0; }();
-
-// tail tiles (and K-pieces in `split`) of a whole-tile 256^2 launch, or 0
-static int big_tail(int M, int N, int K, int& split) {
-  split = 0;
-  const int cus = cu_count();
-  const long t = (long)((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
-  if (!g_big_tail || cus <= 0 || t <= cus) return 0;
-  const int tail = (int)(t % cus);
-  if (tail == 0 || tail > cus / 4) return 0;
-  const int s = std::max(2, std::min(4, cus / tail));
-  if (K % (64 * s)) return 0;
-  split = s;
-  return tail;
-}
-
 template <bool AK, bool BKM, int EPI, bool OUTF32>
 int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   Epi e{};
@@ -2743,20 +2643,6 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, 32 / tiles_n));
   const int kps = big_kps(a.K, split);
   if (split > 1 && (a.ws_bytes < (long)split * a.M * a.N * 4 || a.N % 4)) return 1005;
-  if constexpr (EPI == EPI_STORE && !OUTF32) {
-    int ts = 0;
-    const int tail = split == 1 ? big_tail(a.M, a.N, a.K, ts) : 0;
-    if (tail && a.ws_bytes >= (long)tail * ts * BIG * BIG * 4) {
-      hipLaunchKernelGGL((gemm8p_tail_kernel<AK, BKM, EPI, OUTF32>), dim3(ntiles - tail + tail * ts), dim3(NT2), 0,
-                         st, (const bf16*)a.A, a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm,
-                         tail, ts, (float*)a.workspace, e);
-      DTC_CHECK_LAUNCH();
-      hipLaunchKernelGGL(big_tail_finish, dim3(tail * 8), dim3(256), 0, st, a.M, a.N, tiles_m, tiles_n, gm, tail, ts,
-                         (const float*)a.workspace, (bf16*)a.C, a.ldc, a.bias);
-      DTC_CHECK_LAUNCH();
-      return 0;
-    }
-  }
   // DTC_BIG_CB3: split-K problems whose 256^2 grid leaves CUs idle (the GPT-2 small lm_head dgrad: 96 tiles
   // x split 2 = 192 blocks) run 256 x 192 tiles when that grid is exactly one block per CU (128 x 2 = 256)
   const int cb3 = g_big_cb3;
@@ -2770,22 +2656,6 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
                          kps, (float*)a.workspace, e);
       DTC_CHECK_LAUNCH();
       done = true;
-    }
-  }
-  // DTC_BIG_CB3_FWD: whole-tile bf16 + bias forwards on 256 x 192 tiles when that quantises into fewer
-  // tile-times (each 0.75 of a 256^2 tile): GPT-2 small qkv, 288 tiles = 2 rounds -> 384 = 1.5 rounds
-  if constexpr (EPI == EPI_STORE && !OUTF32) {
-    const int cus = cu_count();
-    if (g_big_cb3_fwd && split == 1 && a.N % 192 == 0 && cus > 0) {
-      const int tn3 = a.N / 192;
-      const long r4 = (ntiles + cus - 1) / cus, t3 = (long)tiles_m * tn3, r3 = (t3 + cus - 1) / cus;
-      if (4 * r4 > 3 * r3 + 1) {  // 0.75 r3 < r4 tile times (strictly, with margin)
-        const int gm3 = std::max(1, std::min(tiles_m, 32 / tn3));
-        hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, EPI, OUTF32, 3>), dim3(t3), dim3(NT2), 0, st, (const bf16*)a.A,
-                           a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tn3, gm3, 1, kps, nullptr, e);
-        DTC_CHECK_LAUNCH();
-        done = true;
-      }
     }
   }
   if (!done) {
@@ -3136,11 +3006,6 @@ int dtc_gemm_wgrad_fuses_colsum(int M, int N, int K) {
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   Plan p = make_plan(M, N, K, layout == 2 ? 1 : (layout == 1 ? 2 : 0));
   const int bs = big_split(layout, M, N, K);
-  if (layout == 0 && bs == 1) {  // the K-split tail's tile slabs (bf16 + bias forwards)
-    int ts = 0;
-    const int tail = big_tail(M, N, K, ts);
-    if (tail) return (long)tail * ts * BIG * BIG * 4;
-  }
   int split = bs ? bs : p.split;
   if (layout == 2 && !bs) split = std::max(split, dmaw_plan(2, M, N, K, EPI_STORE, true, false).split);
   return split > 1 ? (long)split * M * N * 4 : 0;
@@ -3170,18 +3035,6 @@ int dtc_gemm_set_big_cb3(int on) {
 int dtc_gemm_set_n8_mink(int k) {
   const int old = g_n8_mink;
   g_n8_mink = k;
-  return old;
-}
-
-int dtc_gemm_set_big_cb3_fwd(int on) {
-  const int old = g_big_cb3_fwd;
-  g_big_cb3_fwd = on;
-  return old;
-}
-
-int dtc_gemm_set_big_tail(int on) {
-  const int old = g_big_tail;
-  g_big_tail = on;
   return old;
 }
 
@@ -3243,14 +3096,6 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
-  if (epi == EPI_DELTA) {  // the attention's out_proj dgrad (NT on W^T) + delta, on 128^2 tiles (64-column waves)
-    if (a->layout != 0 || f32 || a->N % 64 || !a->aux || !a->aux_out || a->ldaux % 4 || a->vocab_start <= 0 ||
-        a->M % a->vocab_start || a->alpha != 1.f || a->beta != 0.f)
-      return 1010;
-    Plan p = make_plan(a->M, a->N, a->K, 0);
-    if (p.bm != 128 || p.bk != 64 || p.split != 1 || (gemm_dma_mask() & 4)) return 1011;  // gemm_kernel's epilogue only
-    return launch_t<128, 128, true, true, EPI_DELTA, false>(*a, p, st);
-  }
   if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f) {
     const int cb = n8_cb(a->layout, a->M, a->N, a->K, epi);
     if (cb) {

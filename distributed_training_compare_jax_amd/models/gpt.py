@@ -67,10 +67,6 @@ _CE_CHUNK = int(_os.environ.get("DTC_CE_CHUNK", "0"))
 # residual adds of out_proj / fc2 done by the LayerNorm pass that follows (tp == 1): the GEMM epilogue
 # stores a·Wᵀ + b without reading the fp32 residual (DTC_ADD_LN=0: the fused residual epilogue)
 _ADD_LN = _os.environ.get("DTC_ADD_LN", "1") == "1"
-# qkv / fc1 input-gradient GEMMs (the LayerNorm backward's dy, tp == 1, bf16 compute) store bf16 instead
-# of fp32: half the bytes of the dgrad's store and of the LayerNorm backward's dy read (autocast-style
-# bf16 GEMM outputs; dx itself stays fp32, dx = dres + LN'(dy))
-_DGRAD_BF16 = _os.environ.get("DTC_DGRAD_BF16", "0") == "1"
 # out_proj / fc2 forwards (tp == 1, DTC_ADD_LN, bf16 compute) store a·Wᵀ + b as bf16, the LayerNorm pass
 # adds it to the fp32 residual (autocast-style bf16 GEMM outputs; the residual stream stays fp32)
 _FWD_BF16 = _os.environ.get("DTC_FWD_BF16", "0") == "1"
@@ -78,9 +74,6 @@ _FWD_BF16 = _os.environ.get("DTC_FWD_BF16", "0") == "1"
 # batched reduce launch per 48 tasks for the whole group) instead of one reduce launch per layer: GPT-2 small
 # 10.90 vs 10.97 ms/step (profiles/r4_ab_red_batch.log)
 _RED_BATCH_LAYERS = _os.environ.get("DTC_RED_BATCH_LAYERS", "1") == "1"
-# the out_proj dgrad's epilogue computes the attention backward's delta = rowsum(dO·O) (EPI_DELTA), so the
-# backward skips its delta pass (head_dim 64, the 128^2 NT plan)
-_DELTA_EPI = _os.environ.get("DTC_DELTA_EPI", "0") == "1"
 if _CE_CHUNK < 0 or _CE_CHUNK % 256:
     # chunk offsets feed 16-byte vector loads of w[c0:], wt[:, c0:] and gw[c0:]: a ragged offset would
     # surface as an opaque native error deep in the backward
@@ -421,16 +414,7 @@ class GPTStage:
                 dy2 = self._tp_reduce(self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False))
                 dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
             wto = f.wt(p + "out.w")
-            delta = None
-            if wto is not None and _DELTA_EPI and self.cfg.head_dim == 64:
-                # NT dgrad whose epilogue also emits the attention backward's delta = rowsum(dO·O)
-                res = G.linear_delta(dx2_c, wto, o, T, self.heads_local)
-                if res is not None:
-                    do, delta = res
-                    self._wg(dx2_c, o, p + "out")
-            if delta is not None:
-                pass
-            elif wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
+            if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
                 do = G.linear(dx2_c, wto)
                 self._wg(dx2_c, o, p + "out")
             elif self._defer_wg:
@@ -440,7 +424,7 @@ class GPTStage:
                 do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
                                        out_dtype=self.act_dtype, pair=False)
             dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
-                              self.heads_local, delta=delta).view(batch * T, -1)
+                              self.heads_local).view(batch * T, -1)
             wtq = f.wt(p + "qkv.w")
             if self._fuse_bwd and wtq is not None:
                 bg = self._prev_fc2b(l)
@@ -527,9 +511,6 @@ class GPTStage:
                 else:
                     dx = (G.linear(dy, wt, out_dtype=torch.bfloat16) if wt is not None
                           else G.matmul_nn(dy, f.w(dense + ".w"), out_dtype=torch.bfloat16))
-            elif _DGRAD_BF16 and self.tp.size == 1 and dy.dtype == torch.bfloat16:
-                dx = (G.linear(dy, wt, out_dtype=torch.bfloat16) if wt is not None
-                      else G.matmul_nn(dy, f.w(dense + ".w"), out_dtype=torch.bfloat16))
             else:
                 dx = G.linear_resid(dy, wt, None, None) if wt is not None else G.matmul_nn(dy, f.w(dense + ".w"))
             self._wg(dy, x, dense, bias=True)

@@ -98,7 +98,6 @@ EPI_RESID = 1       # C(f32) = aux(f32) + acc + bias
 EPI_GELU = 2        # u = acc+bias: C(bf16) = gelu_tanh'(u) ; aux_out(bf16) = gelu_tanh(u)
 EPI_DGELU = 3       # C(bf16) = acc * aux   (aux = gelu_tanh'(u) from EPI_GELU)
 EPI_LMHEAD = 4      # C(bf16) = acc+bias, pad cols -inf; per-row partial (max,sumexp); label logit
-EPI_DELTA = 7       # C(bf16) = acc (= dO) and aux_out(f32)[b,h,t] = sum_d dO*O (aux = O), vocab_start = T
 
 
 def _declare(lib):
@@ -118,8 +117,6 @@ def _declare(lib):
         "dtc_gemm_set_n8": ([i], i),
         "dtc_gemm_set_n8_cb": ([i], i),
         "dtc_gemm_set_big_cb3": ([i], i),
-        "dtc_gemm_set_big_tail": ([i], i),
-        "dtc_gemm_set_big_cb3_fwd": ([i], i),
         "dtc_gemm_set_n8_mink": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
         "dtc_wgrad_group": ([ctypes.POINTER(WgBatch), vp], i),

@@ -53,11 +53,9 @@ def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None, flags:
 
 
 def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Tensor, n_heads: int,
-             scale: float | None = None, flags: int = 0, delta: torch.Tensor | None = None) -> torch.Tensor:
+             scale: float | None = None, flags: int = 0) -> torch.Tensor:
     """Returns dqkv [B,T,3*H*hd] (same dtype as qkv).  ``flags`` bit 0 forces the two-round resident
-    kernels instead of the fused single-round one (A/B and tests).  ``delta`` (fp32 [B,H,T]): rowsum(dO·O)
-    already computed (``ops.gemm.linear_delta``); the backward then skips its delta pass where it has one
-    (any other path recomputes it into the same buffer)."""
+    kernels instead of the fused single-round one (A/B and tests)."""
     B, T, C3 = qkv.shape
     hd = C3 // (3 * n_heads)
     scale = scale if scale is not None else hd ** -0.5
@@ -85,12 +83,7 @@ def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Te
                                    n_heads, hd, scale, ws.data_ptr(), ws.numel(), N.stream_ptr(qkv.device)),
                 "dtc_attn_f32_bwd")
         return dqkv
-    nbytes = int(L.dtc_attn_bwd_workspace_bytes(B, T, n_heads, hd))
-    if delta is not None:
-        assert delta.dtype == torch.float32 and delta.is_contiguous() and delta.numel() * 4 >= nbytes
-        ws, flags = delta, flags | 16
-    else:
-        ws = _workspace(qkv.device, nbytes)
+    ws = _workspace(qkv.device, int(L.dtc_attn_bwd_workspace_bytes(B, T, n_heads, hd)))
     N.check(L.dtc_attn_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), int(flags),
                            B, T, n_heads, hd, int(flags), scale, ws.data_ptr(), ws.numel() * ws.element_size(),
                            N.stream_ptr(qkv.device)),

@@ -150,28 +150,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return y
 
 
-def linear_delta(dy: torch.Tensor, wt: torch.Tensor, o: torch.Tensor, T: int, n_heads: int):
-    """The attention's out_proj input gradient ``dO = dY·W`` (NT on the transposed weight ``wt``, bf16) and,
-    in the same epilogue, the attention backward's ``delta[b, h, t] = Σ_d dO·O`` (fp32 [B, H, T], head_dim
-    64) from the stored bf16 dO -- the separate delta pass (``attn_delta_kernel``) it replaces reads dO and O
-    again.  Returns ``(dO, delta)``, or None when the kernel plan does not take it."""
-    M, K = dy.shape
-    Nn = wt.shape[0]
-    if (N.library_path(dy) or dy.dtype != torch.bfloat16 or Nn != 64 * n_heads or M % T or not o.is_contiguous()
-            or tuple(o.shape) != (M, Nn)):
-        return None
-    _check2d(dy, "dy"); _check2d(wt, "wt")
-    out = torch.empty(M, Nn, dtype=torch.bfloat16, device=dy.device)
-    delta = torch.empty(M // T, n_heads, T, dtype=torch.float32, device=dy.device)
-    args = _gemm_args(0, M, Nn, K, dy, dy.stride(0), wt, wt.stride(0), out, Nn, epi=N.EPI_DELTA, aux=o,
-                      ldaux=o.stride(0), aux_out=delta, vocab_start=T)
-    rc = N.lib().dtc_gemm(args, N.stream_ptr(dy.device))
-    if rc in (1010, 1011):  # plan without the 64-column-wave epilogue: the caller runs the plain GEMM
-        return None
-    N.check(rc, "dtc_gemm(EPI_DELTA)")
-    return out, delta
-
-
 class RawOut:
     """A GEMM output that is not a torch tensor: a raw device pointer to a row-major [M, N] buffer
     (ldc = N) -- the own half of the P2P all-reduce buffer a row-parallel GEMM writes its partial

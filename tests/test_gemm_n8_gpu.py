@@ -146,48 +146,3 @@ def test_lmhead_dgrad_cb3(cuda):
         _close(out, ref, 2e-3, f"lm_head dgrad (cb3={on})")
         outs.append(out)
     _close(outs[0], outs[1], 1e-5, "cb3_vs_256")
-
-
-@pytest.mark.parametrize("M,Nn,K", [(8192, 2304, 768), (8100, 2304, 768)])
-def test_big_tail_split(cuda, M, Nn, K):
-    """Whole-tile 256^2 forward whose last round is nearly empty (GPT-2 small qkv: 288 tiles = 256 + 32):
-    the 32 tail tiles as 4 K-pieces + big_tail_finish (DTC_BIG_TAIL_SPLIT) -- bf16 + bias output against
-    fp32 torch and against the whole-tile launch."""
-    L = N.lib()
-    x, w = _r(M, K, seed=31), _r(Nn, K, scale=0.05, seed=32)
-    b = torch.randn(Nn, device="cuda") * 0.1
-    ref = x.float() @ w.float().t() + b
-    outs = []
-    for on in (1, 0):
-        old = L.dtc_gemm_set_big_tail(on)
-        try:
-            out = G.linear(x, w, b)
-            torch.cuda.synchronize()
-        finally:
-            L.dtc_gemm_set_big_tail(old)
-        assert out.dtype == torch.bfloat16
-        _close(out, ref, 1e-2, f"qkv forward (tail={on})")
-        outs.append(out)
-    _close(outs[0], outs[1], 1e-2, "tail_vs_whole")
-
-
-@pytest.mark.parametrize("M,Nn,K", [(8192, 2304, 768), (8100, 2304, 768)])
-def test_big_cb3_forward(cuda, M, Nn, K):
-    """Whole-tile bf16 + bias forward on 256 x 192 tiles (DTC_BIG_CB3_FWD: the GPT-2 small qkv forward,
-    288 256^2 tiles = 2 rounds -> 384 = 1.5 rounds of 0.75-size tiles) against fp32 torch and the 256^2
-    launch."""
-    L = N.lib()
-    x, w = _r(M, K, seed=41), _r(Nn, K, scale=0.05, seed=42)
-    b = torch.randn(Nn, device="cuda") * 0.1
-    ref = x.float() @ w.float().t() + b
-    outs = []
-    for on in (1, 0):
-        old = L.dtc_gemm_set_big_cb3_fwd(on)
-        try:
-            out = G.linear(x, w, b)
-            torch.cuda.synchronize()
-        finally:
-            L.dtc_gemm_set_big_cb3_fwd(old)
-        _close(out, ref, 1e-2, f"qkv forward (cb3={on})")
-        outs.append(out)
-    assert torch.equal(outs[0], outs[1])  # same k order per output element, same rounding

@@ -545,21 +545,3 @@ def test_dgrad_ln_bwd_fused(cuda, M, D, K, nslab):
     _close(dx2, dxr - dres, 1e-4, "dx_no_dres")
     torch.cuda.synchronize()
     sync.check()
-
-
-@pytest.mark.parametrize("B,T,H", [(8, 1024, 12), (16, 512, 12)])
-def test_linear_delta_epilogue(cuda, B, T, H):
-    """EPI_DELTA (ops.gemm.linear_delta): the out_proj NT dgrad dO = dY·W (bf16, bitwise the plain GEMM's) and
-    delta[b, h, t] = sum_d dO*O from the stored dO, against fp32 torch of the same bf16 values."""
-    from distributed_training_compare_jax_amd.ops import gemm as G
-    D = 64 * H
-    M = B * T
-    dy = _r(M, D, seed=51).to(torch.bfloat16)
-    wt = (_r(D, D, seed=52) * 0.05).to(torch.bfloat16)
-    o = _r(M, D, seed=53).to(torch.bfloat16)
-    res = G.linear_delta(dy, wt, o, T, H)
-    assert res is not None, "the 128^2 NT plan should take EPI_DELTA"
-    do, delta = res
-    assert torch.equal(do, G.linear(dy, wt))
-    want = (do.float() * o.float()).view(B, T, H, 64).sum(-1).permute(0, 2, 1)
-    _close(delta, want, 1e-5, "delta")
