@@ -141,6 +141,14 @@ class TrainConfig:
     ckpt_every: int = 0
     resume: bool = False
     deterministic: bool = False
+    # DP collective rehearsal: at dp == 1 on an initialised (one-rank) process group, run the DP code path
+    # anyway -- bucket all-reduces, embedding-grad all-gather, loss all-reduce, ZeRO-1 reduce-scatter /
+    # all-gather, bf16 all-to-all payloads -- on a one-member communicator (identities: same math as dp1).
+    # The one-GPU box uses it to execute the exact RCCL call sequence of a DP step (tests/test_rccl_gpu.py)
+    dp_comm_rehearsal: bool = False
+    # capture the step's collectives INTO its hipGraph (one graph per step) instead of cutting the graph at
+    # each collective and issuing it eagerly between segments (parallel/program.py)
+    capture_comms: bool = False
     device: str = "auto"  # auto | cuda | cpu
     batch_is_global: bool = True  # reference: `batch` is the global batch
 

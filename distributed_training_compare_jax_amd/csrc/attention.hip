@@ -853,6 +853,170 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd32_kernel(const bf16* _
   }
 }
 
+// ---------------------------------------------------------------------------- forward, round 5 pipeline
+// attn_fwd32_kernel's math (transposed score tile, lane-local softmax, deferred max, P straight from the
+// accumulators into PV) with the latency structure rebuilt.  PMC of the round-4 kernel: 18 % MFMA busy,
+// the waves parked on two waits per 64-key tile --
+//  * the K/V loads of tile t+1 (issued at the top of tile t, written after it) returned AFTER tile t's
+//    ~1k cycles of compute under load, so every tile ended in a vmcnt stall: here TWO register sets
+//    alternate (the loop is unrolled by 2, named sets, no runtime-indexed registers), so tile t+2's loads
+//    are issued at the top of tile t and have two compute phases + a barrier to land;
+//  * the PV MFMAs each waited on the ds_read_b64_tr_b16 pair issued right before them (2 reads in flight):
+//    here all of a tile's V^T fragments (8 x 4 VGPRs) are requested right after the QK^T MFMAs, so they
+//    land under the softmax VALU and the 8 PV MFMAs issue back to back.
+// Also: two running row sums (l) instead of one serial chain of 32 dependent adds.
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+                                                             float* __restrict__ lse, int B, int T, int H,
+                                                             float scale) {
+  static_assert(HD == 64, "round-5 forward: head_dim 64");
+  constexpr int HC = HD / 16, HB = HD / 32;
+  using L = FwLds<HD>;
+  using RS = RegStage<HD, FW_THREADS>;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (T + FW_QROWS - 1) / FW_QROWS, nbh = B * H;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);
+  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  DTC_ASSERT(qblk >= 0 && b < B && h < H);
+  const long ts = 3L * H * HD;
+  const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
+  const __amdgpu_buffer_rsrc_t rK = rows_rsrc(qkv + (long)b * T * ts + (1 * H + h) * HD, ts, T, HD);
+  const __amdgpu_buffer_rsrc_t rV = rows_rsrc(qkv + (long)b * T * ts + (2 * H + h) * HD, ts, T, HD);
+  const int q0 = qblk * FW_QROWS + 32 * w;
+  const int q = q0 + r;
+  const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + FW_KEYS - 1) / FW_KEYS;
+  RS ra, rb;  // tile it (even) / it + 1 (odd) register sets
+  ra.load(rK, ts, rV, ts, 0, tid);
+  bf16x8 qf[HC];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) qf[c] = q < T ? *(const bf16x8*)(Qb + (long)q * ts + 16 * c + 8 * hh) : bf16x8{};
+  rb.load(rK, ts, rV, ts, FW_KEYS, tid);  // younger than Q: the first tile waits for Q only
+  const float cs = scale * LOG2E;
+  float m = -1e30f, l0 = 0.f, l1 = 0.f;
+  f32x16 acc[HB];
+#pragma unroll
+  for (int i = 0; i < HB; ++i) acc[i] = f32x16{};
+  const int qlim = min(q, T - 1);
+
+  auto tile = [&](const bf16* sK, const bf16* sV, int kb, auto MASK) {
+    bf16x8 kf[2][HC];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int c = 0; c < HC; ++c) kf[k2][c] = *(const bf16x8*)(sK + (k2 * 32 + r) * L::KLD + 16 * c + 8 * hh);
+    f32x16 sc[2];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      sc[k2] = f32x16{};
+#pragma unroll
+      for (int c = 0; c < HC; ++c) sc[k2] = mfma32(kf[k2][c], qf[c], sc[k2]);
+    }
+    // every V^T fragment of the tile in flight now: they land under the softmax
+    bf16x8 vf[2][2][HB];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < HB; ++i) vf[k2][s2][i] = vt_frag32(sV, L::VLD, 32 * k2 + 16 * s2, 32 * i, lane);
+    if constexpr (decltype(MASK)::value) {
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int lim = qlim - (kb + 32 * k2 + 4 * hh);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[k2][i] = ((i & 3) + 8 * (i >> 2) <= lim) ? sc[k2][i] : -INFINITY;
+      }
+    }
+    float mt0 = sc[0][0], mt1 = sc[1][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+      mt0 = fmaxf(mt0, sc[0][i]);
+      mt1 = fmaxf(mt1, sc[1][i]);
+    }
+    float mt = fmaxf(mt0, mt1);
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * cs;
+    if (__builtin_amdgcn_ballot_w64(mt > m + FW_THR) != 0) {
+      const float mn = mt > m + FW_THR ? mt : m;
+      const float alpha = fast_exp2(m - mn);
+      m = mn;
+      l0 *= alpha;
+      l1 *= alpha;
+#pragma unroll
+      for (int i = 0; i < HB; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] *= alpha;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p0 = fast_exp2(fmaf(sc[0][i], cs, -m));
+      const float p1 = fast_exp2(fmaf(sc[1][i], cs, -m));
+      sc[0][i] = p0;
+      sc[1][i] = p1;
+      l0 += p0;
+      l1 += p1;
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = pack8(sc[k2], s2);
+#pragma unroll
+        for (int i = 0; i < HB; ++i) acc[i] = mfma32(vf[k2][s2][i], pf, acc[i]);
+      }
+  };
+  auto compute = [&](int it) {
+    const int kb = it * FW_KEYS;
+    const bf16* sK = lds + (it & 1) * L::STAGE;
+    if (kb <= q0 + 31 && q0 < T) {  // wave-uniform
+      if (kb + FW_KEYS - 1 > q0) tile(sK, sK + FW_KEYS * L::KLD, kb, std::true_type{});
+      else tile(sK, sK + FW_KEYS * L::KLD, kb, std::false_type{});
+    }
+  };
+  auto store = [&](const RS& rs, int buf) {
+    bf16* sK = lds + buf * L::STAGE;
+    bf16* sV = sK + FW_KEYS * L::KLD;
+#pragma unroll
+    for (int i = 0; i < RS::CPT; ++i) {
+      const int c = tid + FW_THREADS * i, rr = c / (HD / 8), col = (c % (HD / 8)) * 8;
+      *(u32x4*)(sK + rr * L::KLD + col) = rs.x[i];
+      *(u32x4*)(sV + rr * L::VLD + col) = rs.y[i];
+    }
+  };
+  store(ra, 0);
+  __syncthreads();
+  // the prefetch loads are unconditional (a tile past the block's last one reads rows that are never used,
+  // rows >= T read 0): a load in a branch makes hipcc's wait counting assume it may be missing and wait
+  // vmcnt(0) at the next write -- for the younger set too, which is the stall this pipeline removes
+  for (int it = 0; it < nkt; it += 2) {
+    // even tile: LDS stage 0 holds tile it, rb tile it + 1 (in flight), ra is free
+    ra.load(rK, ts, rV, ts, (it + 2) * FW_KEYS, tid);
+    compute(it);
+    if (it + 1 < nkt) store(rb, 1);
+    __syncthreads();
+    if (it + 1 >= nkt) break;
+    rb.load(rK, ts, rV, ts, (it + 3) * FW_KEYS, tid);
+    compute(it + 1);
+    if (it + 2 < nkt) store(ra, 0);
+    __syncthreads();
+  }
+  float l = l0 + l1;
+  l += __shfl_xor(l, 32, 64);
+  if (q < T) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long)b * T + q) * H * HD + h * HD;
+#pragma unroll
+    for (int i = 0; i < HB; ++i)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *(bf16x4*)(orow + 32 * i + 8 * g4 + 4 * hh) =
+            bf16x4{f2bf(acc[i][4 * g4] * inv), f2bf(acc[i][4 * g4 + 1] * inv), f2bf(acc[i][4 * g4 + 2] * inv),
+                   f2bf(acc[i][4 * g4 + 3] * inv)};
+    if (hh == 0) lse[((long)b * H + h) * T + q] = (m + __log2f(l)) * LN2;
+  }
+}
+
 // ============================================================================ backward, 32 rows per wave
 // The 32x32x16 forms of the two chunked backward kernels (head_dim 64).  Every 64-row tile they read
 // both ways -- row fragments (ds_read_b128) for one product and transposed fragments
@@ -878,7 +1042,7 @@ __device__ __forceinline__ bf16x8 sw_tr(const bf16* t, int k0, int c0, int lane)
 // Two [64][64] bf16 tiles (rows t0.., two operands, buffer-resource loads) + optionally two fp32 row vectors
 // [64] (lse, delta) for the swizzled images; ONE register set (T14: tile t+1 loaded before tile t's
 // compute, written to the other LDS buffer after it), one barrier per tile.
-template <int NTH, bool VEC>
+template <int NTH, bool VEC, bool DEEP = false>
 struct SwStage {
   static constexpr int CPT = 64 * 8 / NTH;
   u32x4 x[CPT], y[CPT];
@@ -892,7 +1056,17 @@ struct SwStage {
       x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((long)(t0 + r) * sx + 8 * ch) * 2), 0, 0));
       y[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, (int)(((long)(t0 + r) * sy + 8 * ch) * 2), 0, 0));
     }
-    if (VEC && tid < 32) {
+    if constexpr (VEC && DEEP) {
+      // branch-free (every thread, clamped addresses, zero past T): a load in a branch breaks hipcc's
+      // counted waits of the 2-deep pipeline; only threads < 32 store the vector
+      const float* src = (tid & 16) ? vb : va;
+      const int t = t0 + 4 * (tid & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = src[min(t + e, T - 1)];
+        v[e] = t + e < T ? x : 0.f;
+      }
+    } else if (VEC && tid < 32) {
       const float* src = tid < 16 ? va : vb;
       const int r = 4 * (tid & 15), t = t0 + r;
       if (t + 4 <= T) v = *(const f32x4*)(src + t);
@@ -912,15 +1086,38 @@ struct SwStage {
 constexpr int SW_STAGE = 2 * 64 * 64 + 2 * 64 * 2;  // bf16 elements per stage (2 images + 2 fp32 vectors)
 
 // body(sX, sY, sVec, it) over tiles t0_of(it)
-template <int NTH, bool VEC, typename T0, typename Body>
+// DEEP (round 5): two register sets, tile it + 2 loaded at the top of tile it (unconditionally: a load in a
+// branch makes hipcc wait vmcnt(0) at the next LDS write, younger set included), so a load has two compute
+// phases and a barrier to land instead of one (see attn_fwd5_kernel).  t0_of(it) past the last tile must
+// still be a valid row offset (rows >= T read 0 through the buffer range check).
+template <int NTH, bool VEC, bool DEEP = false, typename T0, typename Body>
 __device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, __amdgpu_buffer_rsrc_t rx, long sx,
                                                    __amdgpu_buffer_rsrc_t ry, long sy, const float* va,
                                                    const float* vb, int T, bf16* lds, int tid, Body body) {
   if (n <= 0) return;
-  SwStage<NTH, VEC> st;
   auto X = [&](int k) { return lds + k * SW_STAGE; };
   auto Y = [&](int k) { return lds + k * SW_STAGE + 64 * 64; };
   auto Vv = [&](int k) { return (float*)(lds + k * SW_STAGE + 2 * 64 * 64); };
+  if constexpr (DEEP) {
+    SwStage<NTH, VEC, true> sa, sb;
+    sa.load(rx, sx, ry, sy, va, vb, t0_of(0), T, tid);
+    sb.load(rx, sx, ry, sy, va, vb, t0_of(1), T, tid);
+    sa.store(X(0), Y(0), Vv(0), tid);
+    __syncthreads();
+    for (int it = 0; it < n; it += 2) {
+      sa.load(rx, sx, ry, sy, va, vb, t0_of(it + 2), T, tid);
+      body(X(0), Y(0), Vv(0), it);
+      if (it + 1 < n) sb.store(X(1), Y(1), Vv(1), tid);
+      __syncthreads();
+      if (it + 1 >= n) break;
+      sb.load(rx, sx, ry, sy, va, vb, t0_of(it + 3), T, tid);
+      body(X(1), Y(1), Vv(1), it + 1);
+      if (it + 2 < n) sa.store(X(0), Y(0), Vv(0), tid);
+      __syncthreads();
+    }
+    return;
+  }
+  SwStage<NTH, VEC> st;
   st.load(rx, sx, ry, sy, va, vb, t0_of(0), T, tid);
   st.store(X(0), Y(0), Vv(0), tid);
   __syncthreads();
@@ -937,7 +1134,7 @@ __device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, __amdgpu_buf
 // dO stationary in registers), dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K transposed
 // fragments, dS^T straight from the accumulators).
 // DELTA_IN (the merged launch): delta comes precomputed (attn_delta_kernel) instead of from O here.
-template <int HD, bool DELTA_IN>
+template <int HD, bool DELTA_IN, bool DEEP = false>
 __device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ o,
                                           const bf16* __restrict__ dout, const float* __restrict__ lse,
                                           float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
@@ -1017,7 +1214,7 @@ __device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv,
     }
   };
   const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + 63) / 64;
-  sw_pipelined_tiles<FW_THREADS, false>(nkt, [](int it) { return it * 64; }, rows_rsrc(Kb, ts, T, HD), ts,
+  sw_pipelined_tiles<FW_THREADS, false, DEEP>(nkt, [](int it) { return it * 64; }, rows_rsrc(Kb, ts, T, HD), ts,
                                         rows_rsrc(Vb, ts, T, HD), ts, nullptr, nullptr, T, lds, tid, body);
   if (q < T) {
     bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
@@ -1043,7 +1240,7 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
 // S = Q K^T and dP = dO V^T (Q / dO row fragments, K / V stationary), P and dS = P (dP - delta) with the
 // key on the lane, dV^T += dO^T P and dK^T += Q^T dS (Q / dO transposed fragments of the same images,
 // P / dS straight from the accumulators).  The heaviest key block (0: every query) goes first.
-template <int HD>
+template <int HD, bool DEEP = false>
 __device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                             const float* __restrict__ lse, const float* __restrict__ delta,
                                             bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
@@ -1124,7 +1321,7 @@ __device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qk
     }
   };
   const int nqt = (T - qt0 * 64 + 63) / 64;
-  sw_pipelined_tiles<FW_THREADS, true>(nqt, [qt0](int it) { return (qt0 + it) * 64; }, rows_rsrc(Qb, ts, T, HD), ts,
+  sw_pipelined_tiles<FW_THREADS, true, DEEP>(nqt, [qt0](int it) { return (qt0 + it) * 64; }, rows_rsrc(Qb, ts, T, HD), ts,
                                        rows_rsrc(dOb, dts, T, HD), dts, lseb, delb, T, lds, tid, body);
   if (key < T) {
     bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
@@ -1159,6 +1356,16 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_merged32_kernel(
   const int bid = (int)blockIdx.x;
   if (bid < nk) dkdv32_body<HD>(bid, qkv, dout, lse, delta, dqkv, B, T, H, scale);
   else dq32_body<HD, true>(bid - nk, qkv, nullptr, dout, lse, delta, dqkv, B, T, H, scale);
+}
+
+// the merged launch on the round-5 2-deep K/V (dQ) and Q/dO (dK/dV) prefetch (flags bit 4)
+template <int HD>
+__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_merged5_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale, int nk) {
+  const int bid = (int)blockIdx.x;
+  if (bid < nk) dkdv32_body<HD, true>(bid, qkv, dout, lse, delta, dqkv, B, T, H, scale);
+  else dq32_body<HD, true, true>(bid - nk, qkv, nullptr, dout, lse, delta, dqkv, B, T, H, scale);
 }
 
 // Chunked backward for T > RES_MAXT / head_dim 64 (the tiled kernels above with 16 waves = 256
@@ -1874,6 +2081,14 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
     DTC_CHECK_LAUNCH();
     return 0;
   }
+  // flags bit 4: the round-5 forward (2-deep K/V prefetch, V^T fragments ahead of the softmax)
+  if (HD == 64 && (flags & 16)) {
+    allow_lds(attn_fwd5_kernel<64>, fw_lds_bytes<64>());
+    hipLaunchKernelGGL(attn_fwd5_kernel<64>, dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
+                       fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale);
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
   // flags bit 2: the 16-query-row chunked kernel instead of the 32-row one (A/B)
   if (HD == 64 && !(flags & 4) && attn_chunk_enabled()) {
     allow_lds(attn_fwd32_kernel<64>, fw_lds_bytes<64>());
@@ -1941,7 +2156,12 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
       // DTC_ATTN_BWD_MERGED (default 1; flags bit 3 forces it): delta pass + one launch of dK/dV and dQ
       // blocks -- 82.9 vs 85.3 us per layer, step 11.35-11.37 vs 11.40-11.42 ms (profiles/r4_attn_merged.log)
       static const int bwd_merged = [] { const char* v = getenv("DTC_ATTN_BWD_MERGED"); return v ? atoi(v) : 1; }();
-      if (bwd_merged || (flags & 8)) {
+      if (flags & 16) {
+        allow_lds(attn_bwd_merged5_kernel<64>, lb);
+        launch_attn_delta<64>(o, dout, ws, B, T, H, st);
+        hipLaunchKernelGGL(attn_bwd_merged5_kernel<64>, dim3(2 * g32.x), dim3(FW_THREADS), lb, st, qkv, dout, lse, ws,
+                           dqkv, B, T, H, scale, (int)g32.x);
+      } else if (bwd_merged || (flags & 8)) {
         allow_lds(attn_bwd_merged32_kernel<64>, lb);
         launch_attn_delta<64>(o, dout, ws, B, T, H, st);
         hipLaunchKernelGGL(attn_bwd_merged32_kernel<64>, dim3(2 * g32.x), dim3(FW_THREADS), lb, st, qkv, dout, lse, ws,

@@ -50,8 +50,12 @@ def _free_port() -> int:
 # every gloo collective on GPU tensors where it is issued (the Engine sets it), and the queue count
 # is left at the box default.  The in-launch LayerNorm statistics exchange (ops/ln_fused.py) waits
 # only on blocks of its own grid and is enabled for single-rank runs only.
-def init_distributed(device: str = "auto", timeout_s: float = 600.0) -> DistInfo:
-    """Initialise (or reuse) the default process group from the environment."""
+def init_distributed(device: str = "auto", timeout_s: float = 600.0, single_rank_pg: bool = False) -> DistInfo:
+    """Initialise (or reuse) the default process group from the environment.
+
+    ``single_rank_pg`` (or ``DTC_WORLD1_PG=1``): create the process group at world size 1 too, so a one-GPU
+    run can drive real RCCL communicators (``TrainConfig.dp_comm_rehearsal``: the DP collective sequence
+    issued on a one-rank group)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -67,7 +71,8 @@ def init_distributed(device: str = "auto", timeout_s: float = 600.0) -> DistInfo
     # DTC_DIST_BACKEND=gloo runs several GPU ranks on ONE GPU (RCCL refuses duplicate devices):
     # the 1-GPU test box uses it to exercise the multi-rank GPU code paths (graphs + collectives).
     backend = os.environ.get("DTC_DIST_BACKEND", backend)
-    if world > 1 and not dist.is_initialized():
+    single_rank_pg = single_rank_pg or os.environ.get("DTC_WORLD1_PG", "0") == "1"
+    if (world > 1 or single_rank_pg) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))

@@ -51,10 +51,12 @@ class GradBuckets:
     backward, its all-reduce fully exposed)."""
 
     def __init__(self, flat: FlatParams, group, dp: int, program, bucket_mb: float = 64.0, tail_mb: float = 16.0,
-                 local_names=(), boundaries=None, payload: str = "fp32"):
+                 local_names=(), boundaries=None, payload: str = "fp32", active: bool = None):
         self.flat = flat
         self.group = group
         self.dp = dp
+        # issue the collectives: dp > 1, or the one-member rehearsal group (TrainConfig.dp_comm_rehearsal)
+        self.active = (dp > 1) if active is None else bool(active)
         self.program = program
         if payload not in ("fp32", "bf16"):
             raise ValueError(f"dp_grad_dtype={payload!r}: expected 'fp32' or 'bf16'")
@@ -117,7 +119,7 @@ class GradBuckets:
 
     def ready_upto(self, offset: int):
         """All grads in flat[0:offset] are final → launch every complete, un-issued bucket."""
-        if self.dp == 1:
+        if not self.active:
             return
         for i, (a, b) in enumerate(self.buckets):
             if not self.issued[i] and b <= offset:
@@ -181,7 +183,7 @@ class GradBuckets:
         self.program.comm(fn, name=f"dp_bucket{i}", sig=csig("all_to_all", g, send) + csig("all_gather", g, red))
 
     def wait_all(self):
-        if self.dp == 1:
+        if not self.active:
             return
         for i in range(len(self.buckets)):
             if self.issued[i]:

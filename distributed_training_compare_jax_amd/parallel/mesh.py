@@ -72,13 +72,15 @@ def resolve_degrees(parallel: str, world: int, dp: Optional[int], tp: Optional[i
     raise ValueError(f"Unsupported strategy `{parallel}`")
 
 
-def build_mesh(rank: int, world: int, dp: int, tp: int, pp: int) -> Mesh:
+def build_mesh(rank: int, world: int, dp: int, tp: int, pp: int, dp_group_always: bool = False) -> Mesh:
+    """``dp_group_always``: give a dp == 1 rank a one-member DP group anyway (the DP collective rehearsal
+    of ``TrainConfig.dp_comm_rehearsal``; needs an initialised process group)."""
     assert dp * tp * pp == world, (dp, tp, pp, world)
     tp_idx = rank % tp
     dp_idx = (rank // tp) % dp
     pp_idx = rank // (tp * dp)
     m = Mesh(dp, tp, pp, rank, dp_idx, tp_idx, pp_idx)
-    if world > 1 and dist.is_initialized():
+    if (world > 1 or dp_group_always) and dist.is_initialized():
         # every rank must create every group, in the same order
         for p in range(pp):
             for d in range(dp):
@@ -89,7 +91,7 @@ def build_mesh(rank: int, world: int, dp: int, tp: int, pp: int) -> Mesh:
         for p in range(pp):
             for t in range(tp):
                 ranks = [m.rank_of(d, t, p) for d in range(dp)]
-                g = dist.new_group(ranks) if dp > 1 else None
+                g = dist.new_group(ranks) if (dp > 1 or dp_group_always) else None
                 if p == pp_idx and t == tp_idx:
                     m.dp_group = g
         for d in range(dp):

@@ -162,10 +162,22 @@ class P2PAllReduce:
         return out
 
     def check(self):
-        """Raise if a barrier timed out (a peer never arrived); call at a host sync point."""
+        """Raise if a barrier timed out (a peer never arrived); call at a host sync point.
+
+        Also checks the buffer-half invariant :meth:`staged_out` relies on: every call advances the
+        device epoch by 2, replays included, while the host counter only sees calls issued from Python
+        (eager or captured), so the device half ``(epoch >> 1) & 1`` must equal the host half ``calls & 1``
+        (true as long as every captured step is padded to an even count by :meth:`end_step`).  A P2P call
+        outside the step (eval, a debug all-reduce) without its own :meth:`end_step` flips it, after which
+        graph replays would reduce the stale half: raise instead."""
         e = int(self.err.item())
         if e:
             raise RuntimeError(f"P2P all-reduce: rank {self.rank} timed out waiting for rank {e - 1000}")
+        dev_half = (int(self.epoch.item()) >> 1) & 1
+        if dev_half != (self.calls & 1):
+            raise RuntimeError(f"P2P all-reduce: rank {self.rank} buffer-half mismatch (device epoch "
+                               f"{int(self.epoch.item())}, host calls {self.calls}): a P2P call outside the step "
+                               "left an odd call count; call end_step() after out-of-step P2P use")
 
     def close(self):
         L = N.lib()

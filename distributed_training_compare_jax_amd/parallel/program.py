@@ -24,6 +24,12 @@ branch, or a PP schedule whose two sides disagree) raises on every rank instead 
 ``mode="eager"`` the same step code just executes (CPU/gloo path, first warmup steps).
 All segments share one memory pool and are replayed in capture order, so activations
 produced in one segment and consumed in a later one stay valid.
+
+``capture_comms=True`` (``TrainConfig.capture_comms``, RCCL groups only): the recording pass runs every
+collective INSIDE the capture instead of cutting the graph there -- RCCL's kernels (on its internal
+stream, joined back by the captured event waits of ``Work.wait``) become nodes of the ONE step graph,
+so a step replays with a single host call and no eager collective.  The recording pass then does move
+(stale) bytes once, like the eager warmup step.
 """
 
 from __future__ import annotations
@@ -110,9 +116,10 @@ def _graph_nodes(g) -> int:
 
 
 class StepProgram:
-    def __init__(self, device: torch.device, use_graph: bool):
+    def __init__(self, device: torch.device, use_graph: bool, capture_comms: bool = False):
         self.device = torch.device(device)
         self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        self.capture_comms = bool(capture_comms) and self.use_graph
         self.items: List[Tuple[str, Any, Optional[str]]] = []
         self.recording = False
         self.recorded = False
@@ -186,6 +193,11 @@ class StepProgram:
             h()
         if self.sigs is not None and sig:
             self.sigs.extend(sig)
+        if self.recording and self.capture_comms and not self.sync_comms:
+            res = fn()  # captured into the current graph segment
+            if name is not None:
+                self._handles[name] = res
+            return res
         if self.recording:
             self._cut()
             self.items.append(("comm", fn, name))
@@ -202,6 +214,9 @@ class StepProgram:
     def wait(self, name: str):
         for h in self.before_comm:
             h()
+        if self.recording and self.capture_comms and not self.sync_comms:
+            self._wait(name)  # the stream-side join is captured too
+            return
         if self.recording:
             self._cut()
             self.items.append(("wait", None, name))

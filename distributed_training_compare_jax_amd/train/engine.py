@@ -50,8 +50,12 @@ class Engine:
             if mult != model_cfg.vocab_pad_multiple:
                 model_cfg = replace(model_cfg, vocab_pad_multiple=mult)
                 self.mcfg = model_cfg
-        self.mesh: Mesh = build_mesh(dinfo.rank, dinfo.world, dp, tp, pp)
+        rehearse = bool(train_cfg.dp_comm_rehearsal and dp == 1 and dist.is_available() and dist.is_initialized())
+        self.mesh: Mesh = build_mesh(dinfo.rank, dinfo.world, dp, tp, pp, dp_group_always=rehearse)
         m = self.mesh
+        # the DP code path (bucketed all-reduces, embedding gather, loss all-reduce, ZeRO-1 collectives) runs
+        # when there is more than one replica -- or, as a rehearsal, on a one-member DP group
+        self.dp_comm = dp > 1 or (rehearse and m.dp_group is not None)
         on_gpu = self.device.type == "cuda"
         self.act_dtype = torch.bfloat16 if (on_gpu and train_cfg.dtype == "bf16") else torch.float32
 
@@ -88,11 +92,12 @@ class Engine:
         self.flat.init_canonical(train_cfg.seed)
 
         # ---- step program, comms, model, optimizer
-        self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu)
+        self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu,
+                                   capture_comms=train_cfg.capture_comms)
         # gloo on GPU tensors (the one-GPU multi-rank rig): collectives complete where they are issued,
         # so no copy-back from gloo's worker thread can queue behind a later cross-process wait
         # (parallel/dist.py explains the ordering argument)
-        self.program.sync_comms = bool(on_gpu and dinfo.world > 1 and dinfo.backend == "gloo")
+        self.program.sync_comms = bool(on_gpu and dinfo.backend == "gloo" and (dinfo.world > 1 or self.dp_comm))
         self.p2p = None
         mode = train_cfg.tp_comm
         if tp > 1 and on_gpu and (mode == "p2p" or (mode == "auto" and dinfo.backend == "nccl")):
@@ -113,7 +118,9 @@ class Engine:
         # layers so each group's DP buckets go out under the next group's backward
         wg = train_cfg.wgrad_group
         if wg is None:
-            wg = 0 if dp == 1 else 2
+            wg = 0 if not self.dp_comm else 2
+            if wg == 0:
+                wg = self._wgrad_group_for_memory(model_cfg, len(self.layout.layers))
         self.stage.set_wgrad_group(wg)
         # DP embedding-grad gather (pp == 1): instead of all-reducing the dense wte/wpe grads
         # (103 MB fp32 for the reference vocab, issued last -> fully exposed), all-gather the
@@ -122,14 +129,19 @@ class Engine:
         if train_cfg.zero_stage not in (0, 1):
             raise ValueError(f"zero_stage={train_cfg.zero_stage}: only 0 (replicated Adam state) and 1 (ZeRO-1) "
                              "are implemented")
-        self.zero = bool(train_cfg.zero_stage == 1 and dp > 1)
+        self.zero = bool(train_cfg.zero_stage == 1 and self.dp_comm)
         if self.zero and (tp > 1 or pp > 1):
             raise ValueError("zero_stage=1 is implemented for pure data parallelism (tp = pp = 1)")
-        if train_cfg.zero_stage == 1 and dp == 1 and dinfo.rank == 0:
+        if train_cfg.zero_stage == 1 and not self.dp_comm and dinfo.rank == 0:
             warnings.warn("zero_stage=1 ignored: dp == 1 (nothing to shard); running the replicated AdamW")
         if self.zero and train_cfg.defer_optimizer and dinfo.rank == 0:
             warnings.warn("defer_optimizer ignored under zero_stage=1 (the sharded update ends the step)")
-        self.embed_gather = bool(dp > 1 and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed
+        if self.zero and train_cfg.dp_grad_dtype == "bf16" and dinfo.rank == 0:
+            warnings.warn("dp_grad_dtype=bf16 ignored under zero_stage=1: ShardedAdamW reduce-scatters the fp32 grads")
+        if self.stage.tp_bf16 and self.stage.wg_group < 0 and dinfo.rank == 0:
+            warnings.warn("tp_comm_dtype=bf16 with wgrad_group=-1 (or the backward side stream): the row-parallel "
+                          "partials travel as bf16, the input-gradient partials stay fp32")
+        self.embed_gather = bool(self.dp_comm and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed
                                  and not self.zero)
         bnd = None
         if pp == 1 and len(self.layout.layers):
@@ -140,7 +152,7 @@ class Engine:
         self.buckets = GradBuckets(self.flat, m.dp_group, dp, self.program, train_cfg.dp_bucket_mb,
                                    tail_mb=train_cfg.dp_tail_mb,
                                    local_names=("wte", "wpe") if self.embed_gather else (), boundaries=bnd,
-                                   payload=train_cfg.dp_grad_dtype)
+                                   payload=train_cfg.dp_grad_dtype, active=self.dp_comm)
         if self.zero:
             self.opt = ShardedAdamW(self.flat, opt_cfg, self.program, m.dp_group, dp, m.dp_idx)
         else:
@@ -153,7 +165,7 @@ class Engine:
             # incremental Σg²: with dp == 1 each layer's grads are final when its backward ends
             # (norm chunk per layer, reduced on the side stream); with dp > 1 only the locally
             # built embedding grads are final before the all-reduces finish
-            if dp == 1:
+            if not self.dp_comm:
                 bk = self.buckets
                 cuts = [bk.head_end_offset()] + [bk.layer_end_offset(l) for l in reversed(self.layout.layers)]
                 self.opt.set_chunks(sorted(set(c for c in cuts if 0 < c < self.flat.numel)) + [self.flat.numel])
@@ -249,7 +261,7 @@ class Engine:
         lnf = int(os.environ.get("DTC_LN_FUSE", "2"))
         # dp == 1 too: under DP the bucket all-reduces (RCCL kernels on other CUs) run during the
         # backward, and the in-launch row-statistics exchange needs all of its blocks co-resident.
-        if (lnf and on_gpu and self.act_dtype == torch.bfloat16 and tp == 1 and pp == 1 and dp == 1
+        if (lnf and on_gpu and self.act_dtype == torch.bfloat16 and tp == 1 and pp == 1 and not self.dp_comm
                 and not self.defer_opt and self.stage.side.stream is None):
             has_wt = len(self.layout.layers) > 0 and self.flat.wt(f"h.{self.layout.layers[0]}.fc1.w") is not None
             self.stage.enable_ln_fusion(self.b_local * T, self.opt.step_t, fwd=bool(lnf & 1),
@@ -258,6 +270,30 @@ class Engine:
             self._reserve_workspaces()
 
     # ------------------------------------------------------------------ helpers
+    def _wgrad_group_for_memory(self, mc: ModelConfig, n_layers: int) -> int:
+        """Auto ``wgrad_group`` at dp == 1: one grouped launch for the whole stage (0) keeps every layer's
+        weight-gradient operands alive until the end of the backward -- per layer the bf16 dY tensors
+        (dx3, du, dx2, dqkv) and the X operands that would otherwise be freed after its backward (y1, o,
+        y2, gelu(u)), (8·D + 2·F)·tokens·2 bytes (GPT-2 small at 8k tokens: 201 MB/layer, 2.4 GB in all).
+        When the whole stage's share exceeds the budget (``DTC_WGRAD_MEM_MB``, default 10 % of the
+        device's memory, 1 GiB on CPU) the groups shrink to what fits (at least one layer)."""
+        if n_layers == 0:
+            return 0
+        tokens = self.b_local * self.T
+        esize = 2 if self.act_dtype == torch.bfloat16 else 4
+        D, F = mc.d_model, mc.d_ff
+        per_layer = (8 * D + 2 * F) * tokens * esize
+        env = os.environ.get("DTC_WGRAD_MEM_MB")
+        if env is not None:
+            budget = float(env) * (1 << 20)
+        elif self.device.type == "cuda":
+            budget = 0.10 * torch.cuda.get_device_properties(self.device).total_memory
+        else:
+            budget = float(1 << 30)
+        if per_layer * n_layers <= budget:
+            return 0
+        return max(1, int(budget // per_layer))
+
     def _reserve_workspaces(self):
         from ..ops.gemm import reserve_workspace
 
@@ -366,6 +402,7 @@ class Engine:
         st, T, b = self.stage, self.T, self.b_local
         self._launch_deferred_update()
         dp = self.mesh.dp
+        dpc = self.dp_comm
         ctx: Dict = {}
         step = self.opt.step_t
         hk = self.keys if self.host_keys else None
@@ -376,11 +413,11 @@ class Engine:
             gathered = (self.ids_all, 0, (hk, None) if hk is not None else st.embed_keys(self.ids_all))
         h = st.stage_forward(h, b, ctx)
         st.head_forward(h, self.labels, 1.0 / (b * T), ctx, loss_out=self.loss)
-        if dp > 1:
+        if dpc:
             # the loss is final here: its DP mean goes out now, under the whole backward, instead of
             # as an exposed collective at the end of the step (joined before the optimizer)
             self._loss_allreduce(name="loss_dp")  # (pp == 1 here)
-        with self._CommSafeGemms(dp > 1 and self.stage.flat.device.type == "cuda"):  # bucket all-reduces overlap it
+        with self._CommSafeGemms(dpc and self.stage.flat.device.type == "cuda"):  # bucket all-reduces overlap it
             return self._backward_dp_tp(ctx, dp, step, gathered)
 
     def _backward_dp_tp(self, ctx, dp, step, gathered):
@@ -391,7 +428,7 @@ class Engine:
         # deferred weight gradients: the head's grads are final only after the first grouped launch, so
         # what would follow the head backward runs at the first layer hook (which fires after it)
         head_later = [st._defer_wg]
-        if dp == 1:
+        if not self.dp_comm:
             if not head_later[0]:
                 opt.ready_upto(bk.head_end_offset(), side)
 
@@ -446,7 +483,7 @@ class Engine:
         if not self.zero:
             bk.ready_all()
             bk.wait_all()
-        if dp > 1:
+        if self.dp_comm:
             self.program.wait("loss_dp")
         self._finish_optimizer()
         return self.loss
@@ -457,7 +494,7 @@ class Engine:
         later (the loss is read by the host only, nothing in the step consumes it)."""
         m = self.mesh
         groups = []
-        if m.dp > 1:
+        if self.dp_comm:
             groups.append(m.dp_group)
         if m.pp > 1 and pp:
             groups.append(m.pp_group)

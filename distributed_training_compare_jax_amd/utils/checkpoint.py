@@ -2,10 +2,13 @@
 ``train/train.py:98-102``; SURVEY §5 plan).
 
 Layout: ``<output_dir>/ckpt/step_<N>/rank<r>.pt`` (flat fp32 params, Adam m and v, the
-device step counter) + ``meta.json`` (mesh, per-rank partition map: every parameter's
-name, flat offset, local shape and TP rule).  The partition map lets
-:func:`consolidate` rebuild the full unsharded model from any DP/TP/PP layout, so a run
-can be converted between strategies.  Files are loaded with ``weights_only=True``.
+device step counter) + ``meta_rank<r>.json`` (mesh, this rank's layer range, the padded and
+canonical vocab, and the partition map: every parameter's name, flat offset, local shape and TP
+rule).  The partition map lets :func:`consolidate` rebuild the full unsharded model from any
+DP/TP/PP layout (vocab rows trimmed to the canonical ``vocab_size``, whatever TP padding wrote
+them), so a run can be converted between strategies.  Resume compares the map with this rank's
+flat-buffer slots before touching any buffer, and every rank fails together when one rank's check
+fails.  Files are loaded with ``weights_only=True``.
 """
 
 from __future__ import annotations
@@ -34,9 +37,12 @@ def save(eng, output_dir: str, step: int):
                 "step_t": eng.opt.step_t.cpu(), "step": step}, os.path.join(d, f"rank{m.rank}.pt"))
     slots = {n: dict(offset=s.offset, shape=list(s.shape), tp=s.spec.tp, full=list(s.spec.shape))
              for n, s in f.slots.items()}
+    lr = getattr(eng, "layout", None)
     meta = dict(step=step, dp=m.dp, tp=m.tp, pp=m.pp, rank=m.rank, dp_idx=m.dp_idx, tp_idx=m.tp_idx,
                 pp_idx=m.pp_idx, slots=slots, model=eng.mcfg.name,
-                zero_stage=int(getattr(eng, "zero", False)))
+                zero_stage=int(getattr(eng, "zero", False)),
+                layers=[lr.layers.start, lr.layers.stop] if lr is not None else None,
+                vocab_size=int(eng.mcfg.vocab_size), padded_vocab=int(eng.mcfg.padded_vocab))
     with open(os.path.join(d, f"meta_rank{m.rank}.json"), "w") as fh:
         json.dump(meta, fh)
 
@@ -78,24 +84,76 @@ def source_rank(eng, metas: Dict[int, dict]) -> int:
         raise ValueError(f"zero_stage=1 checkpoint was written at dp={m0['dp']}, this run has dp={mesh.dp}: "
                          "each rank's Adam shard resumes only at the same dp")
     want = (mesh.dp_idx, mesh.tp_idx, mesh.pp_idx)
+    src = None
     for r, m in metas.items():
         if (m["dp_idx"], m["tp_idx"], m["pp_idx"]) == want:
-            return r
-    if not zero_now:
+            src = r
+            break
+    if src is None and not zero_now:
         for r, m in metas.items():
             if (m["dp_idx"], m["tp_idx"], m["pp_idx"]) == (0, mesh.tp_idx, mesh.pp_idx):
-                return r
-    raise ValueError(f"checkpoint (world {len(metas)}) has no rank file for dp/tp/pp index {want}")
+                src = r
+                break
+    if src is None:
+        raise ValueError(f"checkpoint (world {len(metas)}) has no rank file for dp/tp/pp index {want}")
+    _check_slots(eng, metas[src])
+    return src
+
+
+def _check_slots(eng, meta: dict):
+    """The source rank's partition map must equal this rank's flat-buffer layout slot by slot (name,
+    offset, local shape).  Equal element counts are not enough: two PP splits can give a stage the same
+    number of identically shaped layers starting at a different index (``pp_split``/``pp_head_cost``
+    changed), and those weights would load into the wrong layers without any size error."""
+    mine = eng.flat.slots
+    theirs = meta.get("slots", {})
+    lay = meta.get("layers")
+    layout = getattr(eng, "layout", None)
+    if lay is not None and layout is not None and list(lay) != [layout.layers.start, layout.layers.stop]:
+        raise ValueError(f"checkpoint stage {meta['pp_idx']} holds layers [{lay[0]}, {lay[1]}) but this run's stage "
+                         f"holds [{layout.layers.start}, {layout.layers.stop}): the PP layer split differs "
+                         "(pp_split / pp_head_cost); resume with the split that wrote it, or consolidate() and re-shard")
+    if list(theirs) != list(mine):
+        extra = sorted(set(theirs) - set(mine))[:3]
+        missing = sorted(set(mine) - set(theirs))[:3]
+        raise ValueError(f"checkpoint partition map differs from this rank's parameters (only in the checkpoint: "
+                         f"{extra}, only in this run: {missing}): the layer split or model differs")
+    for n, s in mine.items():
+        t = theirs[n]
+        if int(t["offset"]) != s.offset or list(t["shape"]) != list(s.shape):
+            raise ValueError(f"checkpoint slot {n!r} is at offset {t['offset']} shape {t['shape']}, this run has "
+                             f"offset {s.offset} shape {list(s.shape)} (vocab padding or layout differs)")
+
+
+def _agree(ok: bool, err, device):
+    """All ranks learn whether any rank's checkpoint check failed (so no rank walks into the next
+    collective alone); raise here on every rank if one did."""
+    import torch.distributed as dist
+
+    failed = not ok
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([1.0 if failed else 0.0], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if float(t.item()) > 0 and ok:
+            raise ValueError("checkpoint resume failed on another rank (see its error); nothing was loaded")
+    if failed:
+        raise err
 
 
 def load_into(eng, output_dir: str, step: int):
     d = _dir(output_dir, step)
-    src = source_rank(eng, _read_metas(d))
-    st = torch.load(os.path.join(d, f"rank{src}.pt"), map_location="cpu", weights_only=True)
     f = eng.flat
-    for k, have in (("params", f.params), ("exp_avg", f.exp_avg), ("exp_avg_sq", f.exp_avg_sq)):
-        if st[k].shape != have.shape:
-            raise ValueError(f"checkpoint {k} has {st[k].numel()} elements, this rank holds {have.numel()}")
+    st, err = None, None
+    try:
+        src = source_rank(eng, _read_metas(d))
+        st = torch.load(os.path.join(d, f"rank{src}.pt"), map_location="cpu", weights_only=True)
+        for k, have in (("params", f.params), ("exp_avg", f.exp_avg), ("exp_avg_sq", f.exp_avg_sq)):
+            if st[k].shape != have.shape:
+                raise ValueError(f"checkpoint {k} has {st[k].numel()} elements, this rank holds {have.numel()}")
+    except (ValueError, FileNotFoundError, KeyError) as e:
+        err = e
+    _agree(err is None, err, f.device)
     f.params.copy_(st["params"].to(f.device))
     f.exp_avg.copy_(st["exp_avg"].to(f.device))
     f.exp_avg_sq.copy_(st["exp_avg_sq"].to(f.device))
@@ -124,8 +182,16 @@ def maybe_save(eng, tcfg, step: int):
         save(eng, tcfg.output_dir, step)
 
 
-def consolidate(output_dir: str, step: int) -> Dict[str, torch.Tensor]:
-    """Full (unsharded) fp32 parameters from every rank file of a checkpoint."""
+_VOCAB_ROWS = ("wte", "lm_head.w", "lm_head.b")  # params whose leading dim is the (padded) vocab
+
+
+def consolidate(output_dir: str, step: int, vocab_size: int = None) -> Dict[str, torch.Tensor]:
+    """Full (unsharded) fp32 parameters from every rank file of a checkpoint.
+
+    Vocab-indexed tensors (wte rows, lm_head rows and bias) come back with exactly ``vocab_size`` rows
+    (default: the canonical vocab recorded in the checkpoint) whatever padding the writing layout used
+    (TP >= 4 pads to a multiple of 64·tp), so checkpoints of different strategies consolidate to the same
+    shapes; :func:`pad_vocab` re-pads for a target layout."""
     from ..models.params import ParamSpec
 
     d = _dir(output_dir, step)
@@ -145,8 +211,25 @@ def consolidate(output_dir: str, step: int) -> Dict[str, torch.Tensor]:
             pieces.setdefault(n, {})[meta["tp_idx"]] = t
             tp_rule[n] = s["tp"]
             full_shape[n] = tuple(s["full"])
+    if vocab_size is None:
+        vocab_size = next((int(m["vocab_size"]) for m in metas if "vocab_size" in m), None)
     out = {}
     for n, parts in pieces.items():
         spec = ParamSpec(n, full_shape[n], "zeros", 1, tp_rule[n], 0, False)
-        out[n] = unshard(spec, [parts[k] for k in sorted(parts)])
+        t = unshard(spec, [parts[k] for k in sorted(parts)])
+        if vocab_size is not None and n in _VOCAB_ROWS and t.shape[0] > vocab_size:
+            t = t[:vocab_size].clone()
+        out[n] = t
+    return out
+
+
+def pad_vocab(full: Dict[str, torch.Tensor], padded_vocab: int) -> Dict[str, torch.Tensor]:
+    """Re-pad consolidated vocab-indexed tensors with zero rows to ``padded_vocab`` (a target layout's
+    ``ModelConfig.padded_vocab``); pad rows are zero and masked in every layout."""
+    out = dict(full)
+    for n in _VOCAB_ROWS:
+        if n in out and out[n].shape[0] < padded_vocab:
+            t = out[n]
+            pad = torch.zeros((padded_vocab - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype)
+            out[n] = torch.cat([t, pad])
     return out

@@ -1,0 +1,148 @@
+"""One-GPU RCCL rehearsal of the data-parallel step's collective sequence.
+
+The pool's GPU boxes have one MI355X, and RCCL refuses two ranks on one device, so the multi-rank GPU
+tests run over gloo (``tests/test_dist_gpu.py``).  This module closes the remaining gap: it creates a
+ONE-rank RCCL communicator (``DTC_WORLD1_PG=1``) and runs the engine with
+``TrainConfig.dp_comm_rehearsal``, i.e. the DP code path of a dp > 1 run -- the same graph segments,
+the same comm-safe GEMM plans, the same calls in the same order:
+
+* bucketed async ``all_reduce`` of the flat fp32 grads (``parallel/dp.py``), issued between hipGraph
+  segments while the next backward segment replays;
+* ``all_gather_into_tensor`` of the embedding-output grads (the DP embedding gather);
+* the bf16 payload chain ``all_to_all_single`` → fp32 shard sum → ``all_gather_into_tensor``
+  (``dp_grad_dtype: bf16``);
+* ZeRO-1's ``reduce_scatter_tensor`` / ``all_gather_into_tensor`` (``zero_stage: 1``);
+* the async loss ``all_reduce``;
+
+plus, standalone, ``batch_isend_irecv`` to self (the PP transport of ``parallel/pp.py``).  On a
+one-member group every collective is an identity, so each configuration must reproduce a reference
+run BIT FOR BIT: the same rehearsal over gloo (host-staged collectives, identical math) and, for the
+collective-free parts, direct checks.  ``capture_comms`` additionally records the whole step --
+collectives included -- as one hipGraph (reference analog: every collective inside the one jitted
+program, ``train/create_train_step.py:28-50``).
+
+    DTC_WORLD1_PG=1 WORLD_SIZE=1 RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=<p> \\
+        python -m distributed_training_compare_jax_amd.utils.rccl_rehearsal <out.pt> [case ...]
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+
+import torch
+
+CASES = {
+    # name: TrainConfig overrides (every case: dp1 + dp_comm_rehearsal unless "plain")
+    "plain": dict(dp_comm_rehearsal=False),
+    "fp32": dict(),
+    "fp32_captured": dict(capture_comms=True),
+    "no_gather": dict(dp_embed_gather=False),
+    "bf16": dict(dp_grad_dtype="bf16"),
+    "bf16_captured": dict(dp_grad_dtype="bf16", capture_comms=True),
+    "zero1": dict(zero_stage=1),
+}
+STEPS = 5
+
+
+def _model():
+    from ..config.schema import model_config_from_preset
+
+    return model_config_from_preset("tiny", vocab_size=1000, n_layers=4)
+
+
+def run_case(name: str, dinfo) -> dict:
+    from ..config.schema import OptimConfig, TrainConfig
+    from ..train.loop import train
+
+    kw = dict(dp_comm_rehearsal=True)
+    kw.update(CASES[name])
+    tc = TrainConfig(seed=0, parallel="dp", batch=4, steps=STEPS, log_every=1000, output_dir="/tmp/unused",
+                     device="cuda", warmup_steps=2, **kw)
+    oc = OptimConfig(lr=3e-3, weight_decay=0.1, grad_clip=1.0)
+    r = train(tc, _model(), oc, dinfo, quiet=True, write_csv=False)
+    eng = r["engine"]
+    eng.flush_optimizer()
+    torch.cuda.synchronize()
+    return {"losses": list(r["history"]), "params": eng.flat.params.detach().cpu().clone(),
+            "graphs": eng.program.n_graphs, "comms": eng.program.n_comms, "dp_comm": bool(eng.dp_comm),
+            "zero": bool(eng.zero), "embed_gather": bool(eng.embed_gather)}
+
+
+def primitive_checks(dev) -> dict:
+    """Every collective primitive the engine uses, on the one-rank group: results must equal the
+    inputs exactly (identity reductions), eager and replayed from a captured hipGraph."""
+    import torch.distributed as dist
+
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(4096 * 3, generator=g).to(dev)
+    out = {}
+    t = x.clone()
+    dist.all_reduce(t)
+    out["all_reduce"] = bool(torch.equal(t, x))
+    h = x.clone()
+    w = dist.all_reduce(h, async_op=True)
+    w.wait()
+    out["all_reduce_async"] = bool(torch.equal(h, x))
+    o = torch.empty_like(x)
+    dist.all_gather_into_tensor(o, x)
+    out["all_gather_into_tensor"] = bool(torch.equal(o, x))
+    o2 = torch.empty_like(x)
+    dist.reduce_scatter_tensor(o2, x)
+    out["reduce_scatter_tensor"] = bool(torch.equal(o2, x))
+    xb = x.to(torch.bfloat16)
+    ob = torch.empty_like(xb)
+    dist.all_to_all_single(ob, xb)
+    out["all_to_all_single_bf16"] = bool(torch.equal(ob, xb))
+    r = torch.empty_like(x)
+    reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, x, 0), dist.P2POp(dist.irecv, r, 0)])
+    for q in reqs:
+        q.wait()
+    out["batch_isend_irecv_self"] = bool(torch.equal(r, x))
+    # captured: an all-reduce + all-gather inside one graph, replayed on new inputs
+    src = torch.zeros_like(x)
+    dst = torch.empty_like(x)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        gr.capture_begin()
+        dist.all_reduce(src)
+        dist.all_gather_into_tensor(dst, src)
+        gr.capture_end()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    ok = True
+    for k in range(3):
+        src.copy_(x * float(k + 1))
+        gr.replay()
+        torch.cuda.synchronize(dev)
+        ok = ok and bool(torch.equal(dst, x * float(k + 1)))
+    out["captured_replay"] = ok
+    return out
+
+
+def main(argv):
+    from ..parallel.dist import destroy, init_distributed
+
+    path = argv[0]
+    cases = argv[1:] or list(CASES)
+    d = init_distributed("cuda", single_rank_pg=True)
+    import torch.distributed as dist
+
+    res = {"backend": dist.get_backend(), "cases": {}}
+    if dist.get_backend() == "nccl":
+        res["primitives"] = primitive_checks(d.device)
+        try:
+            res["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception:
+            res["rccl_version"] = None
+    for c in cases:
+        res["cases"][c] = run_case(c, d)
+        print(f"[rehearsal] {c}: {res['cases'][c]['graphs']} graph segments, {res['cases'][c]['comms']} eager "
+              f"collectives, last loss {res['cases'][c]['losses'][-1]:.5f}", flush=True)
+    torch.save(res, path)
+    destroy()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -43,10 +43,13 @@ def test_consolidate_tp_checkpoint_equals_single_process(tmp_path):
     out_tp = str(tmp_path / "tp")
     spawn(_tp_worker, 2, args=(out_tp,))
     full = C.consolidate(out_tp, 2)
+    # vocab-indexed tensors come back at the canonical vocab whatever the writer's TP padding
+    assert full["lm_head.w"].shape[0] == MC.vocab_size and full["lm_head.b"].shape[0] == MC.vocab_size
+    assert C.pad_vocab(full, MC.padded_vocab)["lm_head.w"].shape[0] == MC.padded_vocab
     r = train(_tc(str(tmp_path / "dp"), 2), MC, OC, CPU, quiet=True)
     eng = r["engine"]
     for n in eng.flat.slots:
-        a, b = full[n], eng.flat.p(n)
+        a, b = full[n], eng.flat.p(n)[: full[n].shape[0]]
         if n.endswith("qkv.b"):  # zero-gradient key bias: Adam amplifies rounding noise (see parallel tests)
             a, b = a.view(3, -1)[[0, 2]], b.view(3, -1)[[0, 2]]
         # Adam's first steps turn near-zero gradients into +-lr updates, so compare in norm
@@ -93,7 +96,10 @@ def _edit_meta(out, step, **kw):
 
 
 @pytest.mark.parametrize("edit,msg", [(dict(zero_stage=1, dp=2), "zero_stage"), (dict(tp=2), "tp=2"),
-                                      (dict(model="gpt2-medium"), "model")])
+                                      (dict(model="gpt2-medium"), "model"),
+                                      # same element count, different layer range (a changed PP split)
+                                      (dict(layers=[1, 3]), "layer split"),
+                                      (dict(slots={}), "partition map")])
 def test_resume_layout_mismatch_fails_before_touching_buffers(tmp_path, edit, msg):
     out = str(tmp_path / "c")
     train(_tc(out, 2, ckpt_every=2), MC, OC, CPU, quiet=True)

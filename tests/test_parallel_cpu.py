@@ -177,3 +177,33 @@ def test_bf16_payloads_match_single_process(parallel, world, kw):
         for r in res[1:]:
             for n in ref:
                 assert torch.equal(r["params"][n], res[0]["params"][n]), n
+
+
+def _rehearsal_worker(kw, out_dir):
+    from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
+    from distributed_training_compare_jax_amd.train.loop import train
+
+    torch.set_num_threads(1)
+    mc, tc, oc = _cfgs("dp", dp_comm_rehearsal=True, **kw)
+    d = init_distributed("cpu", single_rank_pg=True)  # a ONE-rank gloo group
+    r = train(tc, mc, oc, d, quiet=True, write_csv=False)
+    eng = r["engine"]
+    torch.save({"losses": r["history"], "params": {n: eng.flat.p(n).clone() for n in eng.flat.slots},
+                "dp_comm": eng.dp_comm, "zero": eng.zero, "gather": eng.embed_gather},
+               os.path.join(out_dir, "rank0.pt"))
+    destroy()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kw", [{}, {"dp_embed_gather": False}, {"zero_stage": 1}, {"dp_grad_dtype": "bf16"}])
+def test_dp_comm_rehearsal_on_one_rank_group(single, kw):
+    """dp_comm_rehearsal: the DP code path (buckets, embedding gather, ZeRO-1, bf16 payload chain) on a
+    one-member group is the dp1 math (every collective an identity; bf16 payload: grads rounded once)."""
+    with tempfile.TemporaryDirectory() as td:
+        spawn(_rehearsal_worker, 1, args=(kw, td))
+        r = torch.load(os.path.join(td, "rank0.pt"), weights_only=False)
+    assert r["dp_comm"] and r["zero"] == (kw.get("zero_stage") == 1)
+    if not r["zero"]:  # (ZeRO-1 reduce-scatters every grad: no embedding gather)
+        assert r["gather"] == kw.get("dp_embed_gather", True)
+    tol = 2e-2 if kw.get("dp_grad_dtype") == "bf16" else 1e-5
+    assert r["losses"] == pytest.approx(single[0]["losses"], rel=tol, abs=tol)
