@@ -15,7 +15,7 @@ B, T, H, hd = {"gpt2s": (8, 1024, 12, 64), "medium": (8, 1024, 16, 64), "ref": (
 g = torch.Generator().manual_seed(0)
 qkv = torch.randn(B, T, 3 * H * hd, generator=g).to("cuda").to(torch.bfloat16)
 do = torch.randn(B, T, H * hd, generator=g).to("cuda").to(torch.bfloat16)
-for flags in ((0, 4, 16) if hd == 64 else (0,)):  # 16: the round-5 pipelined forward / merged backward
+for flags in ((0, 4, 16) if hd == 64 else (0,)):  # 16: the round-4 forward
     for _ in range(5):
         o, lse = A.attn_fwd(qkv, H, flags=flags)
         dq = A.attn_bwd(qkv, o, lse, do, H, flags=flags)

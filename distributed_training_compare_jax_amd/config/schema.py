@@ -11,7 +11,9 @@ are optional and default to the reference behaviour:
 * ``TrainConfig.dtype`` — ``bf16`` (MFMA bf16, fp32 master/accum) or ``fp32``.
 * ``TrainConfig.dp/tp/pp`` — explicit mesh degrees for hybrid runs (reference: one
   1-D axis, ``train/train.py:29``).
-* ``TrainConfig.pp_schedule`` (``gpipe`` | ``1f1b``), ``pp_clip`` (``local`` is the
+* ``TrainConfig.pp_schedule`` (``gpipe`` | ``1f1b`` | ``zb``: 1F1B with the backward split into the
+  input-gradient chain and the deferred weight gradients, the latter placed in the pipeline's idle gaps,
+  ``parallel/pp.py``), ``pp_clip`` (``local`` is the
   reference's stage-local global-norm clip, ``create_train_step.py:190``; ``global``
   all-reduces the norm across stages).
 * ``TrainConfig.data`` (``synthetic`` | ``fineweb``), ``use_graph``, ``profile`` (roctx
@@ -147,8 +149,10 @@ class TrainConfig:
     # The one-GPU box uses it to execute the exact RCCL call sequence of a DP step (tests/test_rccl_gpu.py)
     dp_comm_rehearsal: bool = False
     # capture the step's collectives INTO its hipGraph (one graph per step) instead of cutting the graph at
-    # each collective and issuing it eagerly between segments (parallel/program.py)
-    capture_comms: bool = False
+    # each collective and issuing it eagerly between segments (parallel/program.py).  None = auto: on for an
+    # RCCL process group (DTC_CAPTURE_COMMS=0 turns it off), off for gloo.  GPT-2 small, one-rank RCCL
+    # rehearsal of the DP path: 11.39-11.41 ms/step captured vs 11.62-11.64 cut (profiles/r5_rccl_rehearsal.md)
+    capture_comms: Optional[bool] = None
     device: str = "auto"  # auto | cuda | cpu
     batch_is_global: bool = True  # reference: `batch` is the global batch
 

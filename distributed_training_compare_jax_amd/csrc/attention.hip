@@ -855,16 +855,15 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd32_kernel(const bf16* _
 
 // ---------------------------------------------------------------------------- forward, round 5 pipeline
 // attn_fwd32_kernel's math (transposed score tile, lane-local softmax, deferred max, P straight from the
-// accumulators into PV) with the latency structure rebuilt.  PMC of the round-4 kernel: 18 % MFMA busy,
-// the waves parked on two waits per 64-key tile --
-//  * the K/V loads of tile t+1 (issued at the top of tile t, written after it) returned AFTER tile t's
-//    ~1k cycles of compute under load, so every tile ended in a vmcnt stall: here TWO register sets
-//    alternate (the loop is unrolled by 2, named sets, no runtime-indexed registers), so tile t+2's loads
-//    are issued at the top of tile t and have two compute phases + a barrier to land;
-//  * the PV MFMAs each waited on the ds_read_b64_tr_b16 pair issued right before them (2 reads in flight):
-//    here all of a tile's V^T fragments (8 x 4 VGPRs) are requested right after the QK^T MFMAs, so they
-//    land under the softmax VALU and the 8 PV MFMAs issue back to back.
-// Also: two running row sums (l) instead of one serial chain of 32 dependent adds.
+// accumulators into PV) with a deeper load pipeline:
+//  * TWO register sets alternate (the loop is unrolled by 2, named sets, no runtime-indexed registers), so
+//    tile t+2's K/V loads are issued at the top of tile t and have two compute phases + a barrier to land;
+//    the loads are unconditional (a load in a branch makes hipcc wait vmcnt(0) at the next LDS write);
+//  * all of a tile's V^T fragments (8 x 4 VGPRs) are requested right after the QK^T MFMAs, so they land
+//    under the softmax and the 8 PV MFMAs issue back to back;
+//  * two running row sums instead of one serial chain of 32 dependent adds.
+// Measured (profiles/r5_attention.md): 27.5-28.0 vs 28.2-28.4 us per GPT-2-small layer; the PMC wave-cycle
+// total is unchanged -- the round-4 kernel's stalls were not dominated by these two waits.
 template <int HD>
 __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
                                                              float* __restrict__ lse, int B, int T, int H,
@@ -1042,7 +1041,7 @@ __device__ __forceinline__ bf16x8 sw_tr(const bf16* t, int k0, int c0, int lane)
 // Two [64][64] bf16 tiles (rows t0.., two operands, buffer-resource loads) + optionally two fp32 row vectors
 // [64] (lse, delta) for the swizzled images; ONE register set (T14: tile t+1 loaded before tile t's
 // compute, written to the other LDS buffer after it), one barrier per tile.
-template <int NTH, bool VEC, bool DEEP = false>
+template <int NTH, bool VEC>
 struct SwStage {
   static constexpr int CPT = 64 * 8 / NTH;
   u32x4 x[CPT], y[CPT];
@@ -1056,17 +1055,7 @@ struct SwStage {
       x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((long)(t0 + r) * sx + 8 * ch) * 2), 0, 0));
       y[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, (int)(((long)(t0 + r) * sy + 8 * ch) * 2), 0, 0));
     }
-    if constexpr (VEC && DEEP) {
-      // branch-free (every thread, clamped addresses, zero past T): a load in a branch breaks hipcc's
-      // counted waits of the 2-deep pipeline; only threads < 32 store the vector
-      const float* src = (tid & 16) ? vb : va;
-      const int t = t0 + 4 * (tid & 15);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x = src[min(t + e, T - 1)];
-        v[e] = t + e < T ? x : 0.f;
-      }
-    } else if (VEC && tid < 32) {
+    if (VEC && tid < 32) {
       const float* src = tid < 16 ? va : vb;
       const int r = 4 * (tid & 15), t = t0 + r;
       if (t + 4 <= T) v = *(const f32x4*)(src + t);
@@ -1086,11 +1075,7 @@ struct SwStage {
 constexpr int SW_STAGE = 2 * 64 * 64 + 2 * 64 * 2;  // bf16 elements per stage (2 images + 2 fp32 vectors)
 
 // body(sX, sY, sVec, it) over tiles t0_of(it)
-// DEEP (round 5): two register sets, tile it + 2 loaded at the top of tile it (unconditionally: a load in a
-// branch makes hipcc wait vmcnt(0) at the next LDS write, younger set included), so a load has two compute
-// phases and a barrier to land instead of one (see attn_fwd5_kernel).  t0_of(it) past the last tile must
-// still be a valid row offset (rows >= T read 0 through the buffer range check).
-template <int NTH, bool VEC, bool DEEP = false, typename T0, typename Body>
+template <int NTH, bool VEC, typename T0, typename Body>
 __device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, __amdgpu_buffer_rsrc_t rx, long sx,
                                                    __amdgpu_buffer_rsrc_t ry, long sy, const float* va,
                                                    const float* vb, int T, bf16* lds, int tid, Body body) {
@@ -1098,25 +1083,6 @@ __device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, __amdgpu_buf
   auto X = [&](int k) { return lds + k * SW_STAGE; };
   auto Y = [&](int k) { return lds + k * SW_STAGE + 64 * 64; };
   auto Vv = [&](int k) { return (float*)(lds + k * SW_STAGE + 2 * 64 * 64); };
-  if constexpr (DEEP) {
-    SwStage<NTH, VEC, true> sa, sb;
-    sa.load(rx, sx, ry, sy, va, vb, t0_of(0), T, tid);
-    sb.load(rx, sx, ry, sy, va, vb, t0_of(1), T, tid);
-    sa.store(X(0), Y(0), Vv(0), tid);
-    __syncthreads();
-    for (int it = 0; it < n; it += 2) {
-      sa.load(rx, sx, ry, sy, va, vb, t0_of(it + 2), T, tid);
-      body(X(0), Y(0), Vv(0), it);
-      if (it + 1 < n) sb.store(X(1), Y(1), Vv(1), tid);
-      __syncthreads();
-      if (it + 1 >= n) break;
-      sb.load(rx, sx, ry, sy, va, vb, t0_of(it + 3), T, tid);
-      body(X(1), Y(1), Vv(1), it + 1);
-      if (it + 2 < n) sa.store(X(0), Y(0), Vv(0), tid);
-      __syncthreads();
-    }
-    return;
-  }
   SwStage<NTH, VEC> st;
   st.load(rx, sx, ry, sy, va, vb, t0_of(0), T, tid);
   st.store(X(0), Y(0), Vv(0), tid);
@@ -1134,7 +1100,7 @@ __device__ __forceinline__ void sw_pipelined_tiles(int n, T0 t0_of, __amdgpu_buf
 // dO stationary in registers), dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K transposed
 // fragments, dS^T straight from the accumulators).
 // DELTA_IN (the merged launch): delta comes precomputed (attn_delta_kernel) instead of from O here.
-template <int HD, bool DELTA_IN, bool DEEP = false>
+template <int HD, bool DELTA_IN>
 __device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ o,
                                           const bf16* __restrict__ dout, const float* __restrict__ lse,
                                           float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H,
@@ -1214,7 +1180,7 @@ __device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv,
     }
   };
   const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + 63) / 64;
-  sw_pipelined_tiles<FW_THREADS, false, DEEP>(nkt, [](int it) { return it * 64; }, rows_rsrc(Kb, ts, T, HD), ts,
+  sw_pipelined_tiles<FW_THREADS, false>(nkt, [](int it) { return it * 64; }, rows_rsrc(Kb, ts, T, HD), ts,
                                         rows_rsrc(Vb, ts, T, HD), ts, nullptr, nullptr, T, lds, tid, body);
   if (q < T) {
     bf16* pq = dqkv + ((long)b * T + q) * ts + (0 * H + h) * HD;
@@ -1240,7 +1206,7 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_dq32_kernel(
 // S = Q K^T and dP = dO V^T (Q / dO row fragments, K / V stationary), P and dS = P (dP - delta) with the
 // key on the lane, dV^T += dO^T P and dK^T += Q^T dS (Q / dO transposed fragments of the same images,
 // P / dS straight from the accumulators).  The heaviest key block (0: every query) goes first.
-template <int HD, bool DEEP = false>
+template <int HD>
 __device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                             const float* __restrict__ lse, const float* __restrict__ delta,
                                             bf16* __restrict__ dqkv, int B, int T, int H, float scale) {
@@ -1321,7 +1287,7 @@ __device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qk
     }
   };
   const int nqt = (T - qt0 * 64 + 63) / 64;
-  sw_pipelined_tiles<FW_THREADS, true, DEEP>(nqt, [qt0](int it) { return (qt0 + it) * 64; }, rows_rsrc(Qb, ts, T, HD), ts,
+  sw_pipelined_tiles<FW_THREADS, true>(nqt, [qt0](int it) { return (qt0 + it) * 64; }, rows_rsrc(Qb, ts, T, HD), ts,
                                        rows_rsrc(dOb, dts, T, HD), dts, lseb, delb, T, lds, tid, body);
   if (key < T) {
     bf16* pk = dqkv + ((long)b * T + key) * ts + (1 * H + h) * HD;
@@ -1356,16 +1322,6 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_merged32_kernel(
   const int bid = (int)blockIdx.x;
   if (bid < nk) dkdv32_body<HD>(bid, qkv, dout, lse, delta, dqkv, B, T, H, scale);
   else dq32_body<HD, true>(bid - nk, qkv, nullptr, dout, lse, delta, dqkv, B, T, H, scale);
-}
-
-// the merged launch on the round-5 2-deep K/V (dQ) and Q/dO (dK/dV) prefetch (flags bit 4)
-template <int HD>
-__global__ void __launch_bounds__(FW_THREADS, 2) attn_bwd_merged5_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int T, int H, float scale, int nk) {
-  const int bid = (int)blockIdx.x;
-  if (bid < nk) dkdv32_body<HD, true>(bid, qkv, dout, lse, delta, dqkv, B, T, H, scale);
-  else dq32_body<HD, true, true>(bid - nk, qkv, nullptr, dout, lse, delta, dqkv, B, T, H, scale);
 }
 
 // Chunked backward for T > RES_MAXT / head_dim 64 (the tiled kernels above with 16 waves = 256
@@ -2081,8 +2037,10 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
     DTC_CHECK_LAUNCH();
     return 0;
   }
-  // flags bit 4: the round-5 forward (2-deep K/V prefetch, V^T fragments ahead of the softmax)
-  if (HD == 64 && (flags & 16)) {
+  // default at head_dim 64: the round-5 forward (2-deep K/V prefetch, V^T fragments ahead of the softmax;
+  // 27.5-28.0 vs 28.2-28.4 us per layer, profiles/r5_attention.md); flags bit 4 = the round-4 kernel (A/B),
+  // bit 2 = the 16-row chunked kernel
+  if (HD == 64 && !(flags & 16) && !(flags & 4) && attn_chunk_enabled()) {
     allow_lds(attn_fwd5_kernel<64>, fw_lds_bytes<64>());
     hipLaunchKernelGGL(attn_fwd5_kernel<64>, dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
                        fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale);
@@ -2156,12 +2114,7 @@ int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* d
       // DTC_ATTN_BWD_MERGED (default 1; flags bit 3 forces it): delta pass + one launch of dK/dV and dQ
       // blocks -- 82.9 vs 85.3 us per layer, step 11.35-11.37 vs 11.40-11.42 ms (profiles/r4_attn_merged.log)
       static const int bwd_merged = [] { const char* v = getenv("DTC_ATTN_BWD_MERGED"); return v ? atoi(v) : 1; }();
-      if (flags & 16) {
-        allow_lds(attn_bwd_merged5_kernel<64>, lb);
-        launch_attn_delta<64>(o, dout, ws, B, T, H, st);
-        hipLaunchKernelGGL(attn_bwd_merged5_kernel<64>, dim3(2 * g32.x), dim3(FW_THREADS), lb, st, qkv, dout, lse, ws,
-                           dqkv, B, T, H, scale, (int)g32.x);
-      } else if (bwd_merged || (flags & 8)) {
+      if (bwd_merged || (flags & 8)) {
         allow_lds(attn_bwd_merged32_kernel<64>, lb);
         launch_attn_delta<64>(o, dout, ws, B, T, H, st);
         hipLaunchKernelGGL(attn_bwd_merged32_kernel<64>, dim3(2 * g32.x), dim3(FW_THREADS), lb, st, qkv, dout, lse, ws,

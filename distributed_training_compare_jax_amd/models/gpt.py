@@ -675,9 +675,27 @@ class GPTStage:
         if self.red is not None:
             self.red.flush()
 
-    def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None, dx_hook=None):
+    def take_wgrads(self):
+        """Hand over the queued weight gradients (zero-bubble pipeline: the W item of a microbatch runs
+        them later, :meth:`run_wgrads`); the queue is empty afterwards."""
+        q, self.wg_queue = self.wg_queue, []
+        return q
+
+    def run_wgrads(self, q, beta: float):
+        """The W item of a microbatch: its queued weight gradients (+ fused bias gradients) as one grouped
+        launch, accumulated into the grads with ``beta`` (0 for the first W of the step)."""
+        self.wg_queue = list(q)
+        self.flush_wgrads(beta)
+        self.flush_reductions()
+
+    def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None, dx_hook=None,
+                       keep_wgrads: bool = False):
         """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist,
-        ``dx_hook(dx)`` as soon as the stage's input gradient is final (inside the first layer)."""
+        ``dx_hook(dx)`` as soon as the stage's input gradient is final (inside the first layer).
+        ``keep_wgrads`` (deferred weight gradients only): the input-gradient chain (B) alone -- the weight
+        gradients stay queued for :meth:`take_wgrads` (the zero-bubble pipeline's W item)."""
+        if keep_wgrads and not self._defer_wg:
+            raise ValueError("keep_wgrads needs deferred weight gradients (wgrad_group >= 0, no side stream)")
         first = self.layout.layers[0] if len(self.layout.layers) else None
         waiting = []  # layers whose weight gradients are still queued (deferred mode)
         for l in reversed(list(self.layout.layers)):
@@ -685,6 +703,10 @@ class GPTStage:
             self.side.flush()
             if self._defer_wg:
                 waiting.append(l)
+                if keep_wgrads:
+                    if l == first:
+                        self.flush_reductions()  # the B part's LayerNorm / bias partials
+                    continue
                 if l == first or (self.wg_group > 0 and len(waiting) >= self.wg_group):
                     self.flush_wgrads(beta)
                     self.flush_reductions()  # the group's grads are final after these launches
@@ -700,7 +722,7 @@ class GPTStage:
                 hook(l)
             if not _SIDE_INTERLEAVE:
                 self.side.flush()  # one fork per layer: its wgrads (+ anything the hook queued)
-        if self.wg_queue:  # a stage without layers: the lm_head's weight gradient alone
+        if self.wg_queue and not keep_wgrads:  # a stage without layers: the lm_head's weight gradient alone
             self.flush_wgrads(beta)
             self.flush_reductions()
         return dx, dx_c

@@ -180,7 +180,11 @@ class GradBuckets:
             ev.record(self._cs)
             return _StreamJoin(ev)
 
-        self.program.comm(fn, name=f"dp_bucket{i}", sig=csig("all_to_all", g, send) + csig("all_gather", g, red))
+        # not captured under capture_comms: the bf16 chain (side-stream fork + all_to_all_single) crashed the
+        # one-rank RCCL rehearsal inside a hipGraph capture (segfault, tests/test_rccl_gpu.py); it stays an
+        # eager item between segments
+        self.program.comm(fn, name=f"dp_bucket{i}", sig=csig("all_to_all", g, send) + csig("all_gather", g, red),
+                          capturable=False)
 
     def wait_all(self):
         if not self.active:

@@ -15,6 +15,13 @@ PROGRAM (:func:`pp_program`) of compute items and communication entries:
   Megatron's paired exchanges: in the steady state the send of a forward output and the receive of
   a backward gradient — both with the next stage — are ONE grouped RCCL call
   (``batch_isend_irecv``), and likewise send-gradient/receive-activation with the previous stage.
+* ``zb`` = zero-bubble-style 1F1B (Qi et al., "Zero Bubble Pipeline Parallelism", ZB-H1 memory): the
+  backward splits into B (the input-gradient chain: every dgrad GEMM, attention and LayerNorm backward
+  -- what the previous stage waits for) and W (the stage's deferred weight gradients, one grouped launch,
+  ``models/gpt.py`` wgrad queue).  The communication program is exactly 1F1B's (so its deadlock freedom
+  carries over); W items carry no messages and are placed by :func:`zb_program` where a timed replay of
+  the pipeline (:func:`timeline`, per-item costs) shows the stage idle waiting for a message -- the
+  cool-down bubble fills with weight gradients instead of idle time.
 
 Why the pairing matters on RCCL: all p2p traffic between two ranks runs, in issue order, on that
 pair's communicator stream, and a send completes only against the matching receive.  Two stages
@@ -41,7 +48,7 @@ from .dist import staged_p2p
 from .program import psig
 
 # ------------------------------------------------------------------------------ static programs
-# items: ("F", i) / ("B", i)                         compute of microbatch i
+# items: ("F", i) / ("B", i) / ("W", i)              compute of microbatch i (W: zb only)
 #        ("post", name, peer, sends, recvs)          one (grouped) p2p call with stage s+peer;
 #                                                    sends/recvs: tuples of tags ("f"|"b", i)
 #        ("wait", names)                              the compute stream waits for these entries
@@ -68,7 +75,9 @@ def _schedule(kind: str, S: int, s: int, M: int) -> List[tuple]:
     return ops
 
 
-def pp_program(kind: str, S: int, s: int, M: int) -> List[tuple]:
+def pp_program(kind: str, S: int, s: int, M: int, costs=None) -> List[tuple]:
+    if kind == "zb":
+        return zb_programs(S, M, costs)[s]
     first, last = s == 0, s == S - 1
     prog: List[tuple] = []
     sends: List[str] = []
@@ -145,6 +154,149 @@ def pp_program(kind: str, S: int, s: int, M: int) -> List[tuple]:
     return prog
 
 
+# ------------------------------------------------------------------------------ zero bubble (B/W split)
+def stage_item_costs(S: int, stage_cost=None, split=(1.0, 1.0, 1.0)) -> List[Dict[str, float]]:
+    """Per-stage cost of one microbatch's F, B (input-gradient chain) and W (weight gradients), in any
+    unit.  ``stage_cost[s]``: the stage's relative size (``mesh.stage_costs``: its layers + the head's
+    block-equivalents on the last stage); ``split``: the F : B : W ratio of a block (a block's backward is
+    ~2x its forward, half of it the dgrads, half the weight gradients)."""
+    stage_cost = [1.0] * S if stage_cost is None else list(stage_cost)
+    tot = float(sum(split))
+    return [{k: c * v / tot for k, v in zip("FBW", split)} for c in stage_cost]
+
+
+def timeline(progs: List[List[tuple]], costs: List[Dict[str, float]], comm: float = 0.0,
+             model: str = "rank") -> Dict[str, object]:
+    """Timed replay of the stages' programs: every stage runs its items in order on one clock (compute
+    items take ``costs[s][kind]``, a post records its time, a wait advances the clock to its entries'
+    completion); an entry completes when it and its complement head their queues (same queue models as
+    :func:`simulate`), ``comm`` after the later of the two posts.  Returns the makespan, per-stage busy
+    time, the bubble fraction 1 - busy / (S * makespan), and every wait's idle gap (stage, item index,
+    clock before the wait, completion time)."""
+    S = len(progs)
+    pc = [0] * S
+    clock = [0.0] * S
+    busy = [0.0] * S
+    queues: Dict[Tuple[int, int], List[tuple]] = {}
+    done: Dict[Tuple[int, str], float] = {}
+    gaps: List[tuple] = []
+    while True:
+        progressed = False
+        for s in range(S):
+            while pc[s] < len(progs[s]):
+                it = progs[s][pc[s]]
+                if it[0] == "post":
+                    _, name, peer, snd, rcv = it
+                    key = (s, s + peer) if model == "pair" else (s, -1)
+                    queues.setdefault(key, []).append((name, frozenset(snd), frozenset(rcv), s + peer, clock[s]))
+                elif it[0] == "wait":
+                    if not all((s, n) in done for n in it[1]):
+                        break
+                    t = max(done[(s, n)] for n in it[1])
+                    if t > clock[s]:
+                        gaps.append((s, pc[s], clock[s], t))
+                    clock[s] = max(clock[s], t)
+                else:
+                    c = costs[s][it[0]]
+                    clock[s] += c
+                    busy[s] += c
+                pc[s] += 1
+                progressed = True
+        for (a, _), qa in list(queues.items()):
+            while qa:
+                b = qa[0][3]
+                qb = queues.get((b, a) if model == "pair" else (b, -1), [])
+                if not qb or qb[0][3] != a:
+                    break
+                na, sa, ra, _, ta = qa[0]
+                nb, sb, rb, _, tb = qb[0]
+                if sa != rb or ra != sb:
+                    raise RuntimeError(f"timeline: message order mismatch at stages {a}/{b} ({na} vs {nb})")
+                qa.pop(0)
+                qb.pop(0)
+                t = max(ta, tb) + comm
+                done[(a, na)] = t
+                done[(b, nb)] = t
+                progressed = True
+        if all(pc[s] == len(progs[s]) for s in range(S)):
+            span = max(clock)
+            bubble = 1.0 - sum(busy) / (S * span) if span > 0 else 0.0
+            return {"makespan": span, "busy": busy, "bubble": bubble, "gaps": gaps, "end": clock}
+        if not progressed:
+            raise RuntimeError("timeline: deadlock")
+
+
+def _place_w(progs, base, s, costs, comm, M):
+    """Stage s's program with its W's moved out of the steady state into the idle gaps the timed replay
+    shows (the other stages as in ``progs``), the ones that fit nowhere at the end."""
+    prog = base[s]
+    trial = list(progs)
+    trial[s] = prog + [("W", i) for i in range(M)]
+    tl = timeline(trial, costs, comm)
+    gap_at = {idx: (t0, t1) for (st, idx, t0, t1) in tl["gaps"] if st == s}
+    wcost = costs[s]["W"]
+    ws: List[int] = []
+    out: List[tuple] = []
+    delay = 0.0  # how far the W's placed so far pushed this stage's clock past the replay's
+    for idx, it in enumerate(prog):
+        if it[0] == "wait" and idx in gap_at:
+            t0, t1 = gap_at[idx]
+            room = (t1 - t0) - delay
+            while ws and wcost <= room + 1e-9:
+                out.append(("W", ws.pop(0)))
+                room -= wcost
+            delay = max(0.0, delay - (t1 - t0))
+        out.append(it)
+        if it[0] == "B":
+            ws.append(it[1])
+    tail = [("W", i) for i in ws]
+    if out and out[-1][0] == "wait":  # before the final wait on the stage's sends
+        return out[:-1] + tail + [out[-1]]
+    return out + tail
+
+
+def zb_programs(S: int, M: int, costs=None, comm: float = 0.0) -> List[List[tuple]]:
+    """ZB-H1-style programs: 1F1B's items with every B split into B (input gradients) and W (weight
+    gradients), W placed to fill idle time.  Start from 1F1B with a split backward (each W right after
+    its B: 1F1B's timing); then stage by stage the W's leave the steady state for the idle gaps of the
+    timed replay (:func:`_place_w`).  The placement depends on the order the stages are visited in (a
+    placed W changes when its stage posts later messages): first-to-last, last-to-first and a second
+    pass of each are tried and the programs with the shortest replayed makespan are kept.  Memory stays
+    1F1B's: a W never moves before its own B, and its B already holds the activations it reads."""
+    costs = stage_item_costs(S) if costs is None else costs
+    base = [pp_program("1f1b", S, s, M) for s in range(S)]
+    inline = [[x for it in b for x in ((it, ("W", it[1])) if it[0] == "B" else (it,))] for b in base]
+    if S == 1:
+        return inline
+    best, best_t = inline, timeline(inline, costs, comm)["makespan"]
+    # starting states: 1F1B timing (W inline) and the W-free pipeline (the other stages' W's not yet
+    # placed count as free while a stage is placed)
+    for start, order in ((inline, list(range(S))), (inline, list(reversed(range(S)))), (base, list(range(S))),
+                         (base, list(reversed(range(S))))):
+        progs = [list(p) for p in start]
+        for _ in range(2):
+            for s in order:
+                progs[s] = _place_w(progs, base, s, costs, comm, M)
+            t = timeline(progs, costs, comm)["makespan"]
+            if t < best_t - 1e-9:
+                best, best_t = [list(p) for p in progs], t
+    return best
+
+
+def estimate(kind: str, S: int, M: int, costs=None, comm: float = 0.0) -> Dict[str, float]:
+    """Predicted step (makespan) and bubble of a schedule under per-item costs (``stage_item_costs``):
+    the 1F1B / GPipe B items cost B + W (their backward runs the weight gradients inline)."""
+    costs = stage_item_costs(S) if costs is None else costs
+    if kind == "zb":
+        progs = zb_programs(S, M, costs, comm)
+        c = costs
+    else:
+        progs = [pp_program(kind, S, s, M) for s in range(S)]
+        c = [{"F": x["F"], "B": x["B"] + x["W"], "W": 0.0} for x in costs]
+    tl = timeline(progs, c, comm)
+    return {"makespan": tl["makespan"], "bubble": tl["bubble"], "ideal": max(M * sum(x.values()) for x in costs)}
+
+
 def simulate(kind: str, S: int, M: int, model: str = "pair") -> Dict[str, int]:
     """Run every stage's :func:`pp_program` under RCCL p2p semantics and return counters.
 
@@ -163,7 +315,7 @@ def simulate(kind: str, S: int, M: int, model: str = "pair") -> Dict[str, int]:
     Raises RuntimeError on a deadlock or on a head pair that does not match (wrong message order)."""
     if model not in ("pair", "rank"):
         raise ValueError(model)
-    progs = [pp_program(kind, S, s, M) for s in range(S)]
+    progs = zb_programs(S, M) if kind == "zb" else [pp_program(kind, S, s, M) for s in range(S)]
     pc = [0] * S
     queues: Dict[Tuple[int, int], List[tuple]] = {}
     done = set()
@@ -324,9 +476,14 @@ def run_pipeline(eng) -> None:
                 _, _, peer, snd, rcv = st_
                 rank = m.pp_next if peer > 0 else m.pp_prev
                 sig += [x for t in snd for x in psig("send", rank, t)] + [x for t in rcv for x in psig("recv", rank, t)]
-        prog.comm(fn, sig=sig)
+        # PP point-to-point stays eager between segments (RCCL p2p inside a capture is unexercised here)
+        prog.comm(fn, sig=sig, capturable=False)
 
-    items = pp_program(eng.tcfg.pp_schedule, S, s, M)
+    kind = eng.tcfg.pp_schedule
+    zb = kind == "zb"
+    items = pp_program(kind, S, s, M, costs=eng.pp_item_costs() if zb else None)
+    wq: Dict[int, list] = {}  # zb: microbatch -> its queued weight gradients (run by its W item)
+    n_w_done = 0
     sent_tags = {it[1]: it[3] for it in items if it[0] == "post"}  # post name -> tags it sends
     dx_out: Dict[int, torch.Tensor] = {}
     k = 0
@@ -339,6 +496,11 @@ def run_pipeline(eng) -> None:
             k = j
             continue
         kind, i = items[k]
+        if kind == "W":
+            st.run_wgrads(wq.pop(i), 0.0 if n_w_done == 0 else 1.0)
+            n_w_done += 1
+            k += 1
+            continue
         ids = eng.ids[i * rows:(i + 1) * rows]
         labels = eng.labels[i * rows:(i + 1) * rows]
         row0 = eng.row0 + i * rows
@@ -368,7 +530,9 @@ def run_pipeline(eng) -> None:
                         dx_c = eng.recv_dx_bf[i]
                 elif dx_c is not dx:
                     cast_to_bf16(dx, dx_c)
-            dx, dx_c = st.stage_backward(ctx, dx, dx_c, beta)
+            dx, dx_c = st.stage_backward(ctx, dx, dx_c, beta, keep_wgrads=zb)
+            if zb:
+                wq[i] = st.take_wgrads()
             if first:
                 st.embed_backward(ctx, dx, step, beta)
             else:

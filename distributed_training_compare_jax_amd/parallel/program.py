@@ -127,6 +127,7 @@ class StepProgram:
         self._pool = None
         self._empty: List[Any] = []  # captured-empty segments (see _cut)
         self._handles: Dict[str, Any] = {}
+        self._eager_names = set()  # named collectives issued eagerly between captured segments
         self._stream = torch.cuda.Stream(self.device) if self.use_graph else None
         # called before every cut/collective: forked streams (e.g. the backward side stream)
         # must re-join the capture stream before a graph segment ends / a collective reads data
@@ -186,19 +187,23 @@ class StepProgram:
         return ms
 
     # -------------------------------------------------------------- step-code API
-    def comm(self, fn: Callable[[], Any], name: Optional[str] = None, sig: Optional[List[Tuple]] = None):
+    def comm(self, fn: Callable[[], Any], name: Optional[str] = None, sig: Optional[List[Tuple]] = None,
+             capturable: bool = True):
         """Issue a collective.  ``fn`` may return an async Work handle, retrievable by ``wait(name)``;
-        ``sig`` (:func:`csig` / :func:`psig` entries) describes what it moves, for the cross-rank check."""
+        ``sig`` (:func:`csig` / :func:`psig` entries) describes what it moves, for the cross-rank check.
+        ``capturable=False``: never captured (``capture_comms``), always a graph cut + eager issue."""
         for h in self.before_comm:
             h()
         if self.sigs is not None and sig:
             self.sigs.extend(sig)
-        if self.recording and self.capture_comms and not self.sync_comms:
+        if self.recording and self.capture_comms and not self.sync_comms and capturable:
             res = fn()  # captured into the current graph segment
             if name is not None:
                 self._handles[name] = res
             return res
         if self.recording:
+            if name is not None:
+                self._eager_names.add(name)
             self._cut()
             self.items.append(("comm", fn, name))
             self._begin()
@@ -214,7 +219,7 @@ class StepProgram:
     def wait(self, name: str):
         for h in self.before_comm:
             h()
-        if self.recording and self.capture_comms and not self.sync_comms:
+        if self.recording and self.capture_comms and not self.sync_comms and name not in self._eager_names:
             self._wait(name)  # the stream-side join is captured too
             return
         if self.recording:

@@ -73,6 +73,8 @@ class Engine:
         self.row0 = m.dp_idx * self.b_local
 
         # ---- ownership
+        if train_cfg.pp_schedule not in ("gpipe", "1f1b", "zb"):
+            raise ValueError(f"pp_schedule={train_cfg.pp_schedule!r}: expected 'gpipe', '1f1b' or 'zb'")
         if train_cfg.pp_split not in ("cost", "even"):
             raise ValueError(f"pp_split={train_cfg.pp_split!r}: expected 'cost' or 'even'")
         weights = None
@@ -92,8 +94,10 @@ class Engine:
         self.flat.init_canonical(train_cfg.seed)
 
         # ---- step program, comms, model, optimizer
-        self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu,
-                                   capture_comms=train_cfg.capture_comms)
+        cap = train_cfg.capture_comms
+        if cap is None:
+            cap = dinfo.backend == "nccl" and os.environ.get("DTC_CAPTURE_COMMS", "1") == "1"
+        self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu, capture_comms=cap)
         # gloo on GPU tensors (the one-GPU multi-rank rig): collectives complete where they are issued,
         # so no copy-back from gloo's worker thread can queue behind a later cross-process wait
         # (parallel/dist.py explains the ordering argument)
@@ -293,6 +297,17 @@ class Engine:
         if per_layer * n_layers <= budget:
             return 0
         return max(1, int(budget // per_layer))
+
+    def pp_item_costs(self):
+        """Per-stage F / B / W costs of one microbatch for the zero-bubble placement (``parallel/pp.py``):
+        the stage sizes of the layer split (layers + the head's block-equivalents, ``mesh.stage_costs``).
+        Identical on every rank (the programs of all stages must agree)."""
+        from ..parallel.mesh import stage_costs
+        from ..parallel.pp import stage_item_costs
+
+        hc = self.tcfg.pp_head_cost
+        w = (0.05, head_cost_blocks(self.mcfg) if hc is None else float(hc))
+        return stage_item_costs(self.mesh.pp, stage_costs(self.layer_ranges, w))
 
     def _reserve_workspaces(self):
         from ..ops.gemm import reserve_workspace

@@ -33,14 +33,16 @@ import sys
 import torch
 
 CASES = {
-    # name: TrainConfig overrides (every case: dp1 + dp_comm_rehearsal unless "plain")
+    # name: TrainConfig overrides (every case: dp1 + dp_comm_rehearsal unless "plain"); the cut-graph cases
+    # set capture_comms=False explicitly (the RCCL default captures)
     "plain": dict(dp_comm_rehearsal=False),
-    "fp32": dict(),
+    "fp32": dict(capture_comms=False),
     "fp32_captured": dict(capture_comms=True),
-    "no_gather": dict(dp_embed_gather=False),
-    "bf16": dict(dp_grad_dtype="bf16"),
+    "no_gather": dict(dp_embed_gather=False, capture_comms=False),
+    "bf16": dict(dp_grad_dtype="bf16", capture_comms=False),
     "bf16_captured": dict(dp_grad_dtype="bf16", capture_comms=True),
-    "zero1": dict(zero_stage=1),
+    "zero1": dict(zero_stage=1, capture_comms=False),
+    "zero1_captured": dict(zero_stage=1, capture_comms=True),
 }
 STEPS = 5
 
@@ -67,6 +69,49 @@ def run_case(name: str, dinfo) -> dict:
     return {"losses": list(r["history"]), "params": eng.flat.params.detach().cpu().clone(),
             "graphs": eng.program.n_graphs, "comms": eng.program.n_comms, "dp_comm": bool(eng.dp_comm),
             "zero": bool(eng.zero), "embed_gather": bool(eng.embed_gather)}
+
+
+def bench_case(name: str, dinfo, model: str = "gpt2-small", steps: int = 20, warmup: int = 4) -> dict:
+    """ms/step of one case on a real model (bench.py's timing: graph replays back to back, one loss
+    read per step one step late): ``plain`` vs the rehearsals measures what the DP code path costs at
+    dp1 before any communication (comm-safe GEMM plans, grouped weight gradients of 2 layers, the
+    embedding gather, the graph cuts) and what capturing the collectives saves."""
+    import time
+
+    from ..config.schema import OptimConfig, TrainConfig, model_config_from_preset
+    from ..data.synthetic import get_batch_iterator
+    from ..parallel.dist import barrier
+    from ..train.engine import Engine
+
+    kw = dict(dp_comm_rehearsal=True)
+    kw.update(CASES[name])
+    mc = model_config_from_preset(model)
+    tc = TrainConfig(seed=0, parallel="dp", batch=8, steps=steps, log_every=10 ** 9, output_dir="/tmp/unused",
+                     device="cuda", **kw)
+    eng = Engine(mc, tc, OptimConfig(lr=3e-4, weight_decay=0.1, grad_clip=1.0), dinfo)
+    data = get_batch_iterator(8, mc.max_seq_len + 1, seed=0, row0=eng.feed_row0, nrows=eng.feed_rows)
+    for _ in range(max(warmup, 2)):
+        eng.set_batch(next(data))
+        eng.run_step()
+        eng.loss_value()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pending = None
+    for _ in range(steps):
+        eng.set_batch(next(data))
+        eng.run_step()
+        h = eng.loss_handle()
+        if pending is not None:
+            eng.read_loss(pending)
+        pending = h
+    loss = eng.read_loss(pending)
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    out = {"ms_per_step": ms, "graphs": eng.program.n_graphs, "comms": eng.program.n_comms, "loss": loss}
+    del eng
+    torch.cuda.empty_cache()
+    return out
 
 
 def primitive_checks(dev) -> dict:
@@ -124,6 +169,9 @@ def primitive_checks(dev) -> dict:
 def main(argv):
     from ..parallel.dist import destroy, init_distributed
 
+    bench = argv[0] == "--bench"
+    if bench:
+        argv = argv[1:]
     path = argv[0]
     cases = argv[1:] or list(CASES)
     d = init_distributed("cuda", single_rank_pg=True)
@@ -136,6 +184,17 @@ def main(argv):
             res["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
         except Exception:
             res["rccl_version"] = None
+    if bench:
+        res["bench"] = {}
+        for rnd in range(2):  # interleaved rounds (box clock drift)
+            for c in cases:
+                r = bench_case(c, d)
+                res["bench"].setdefault(c, []).append(r)
+                print(f"[bench] round {rnd} {c}: {r['ms_per_step']:.3f} ms/step ({r['graphs']} graph segments, "
+                      f"{r['comms']} eager collectives)", flush=True)
+        torch.save(res, path)
+        destroy()
+        return
     for c in cases:
         res["cases"][c] = run_case(c, d)
         print(f"[rehearsal] {c}: {res['cases'][c]['graphs']} graph segments, {res['cases'][c]['comms']} eager "

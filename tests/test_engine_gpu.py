@@ -72,7 +72,9 @@ def test_gpt2_small_step_vs_oracle(cuda):
             g, go = g.view(3, -1)[[0, 2]], go.view(3, -1)[[0, 2]]
         err = ((g - go).norm() / (go.norm() + 1e-12)).item()
         worst.append((err, n))
-        assert err < 5e-2, f"{n}: relative grad error {err:.3e}"
+        # bf16 GEMM operands over K = 768..50304: observed worst 7.1e-3 (profiles/r4_oracle.log); 2e-2 leaves
+        # < 3x headroom so a real regression fails
+        assert err < 2e-2, f"{n}: relative grad error {err:.3e}"
     print("worst relative grad errors:", sorted(worst)[-5:])
 
 

@@ -266,9 +266,9 @@ def test_attention_fwd32_vs_chunk_and_reference(cuda, B, T, H, spike):
     _close(o.cpu(), oc, 2e-2, "attn32_o")
     _close(lse.cpu(), lsec, 1e-3, "attn32_lse")
     _close(o.float(), o4.float(), 2e-2, "attn32_vs_chunk")
-    o5, lse5 = A.attn_fwd(qkv, H, flags=16)  # round-5 pipeline (same math)
-    _close(o5.cpu(), oc, 2e-2, "attn5_o")
-    _close(lse5.cpu(), lsec, 1e-3, "attn5_lse")
+    o4r, lse4r = A.attn_fwd(qkv, H, flags=16)  # the round-4 32-row kernel (the default is the round-5 pipeline)
+    _close(o4r.cpu(), oc, 2e-2, "attn32r4_o")
+    _close(lse4r.cpu(), lsec, 1e-3, "attn32r4_lse")
     assert torch.equal(o, A.attn_fwd(qkv, H)[0])  # deterministic
     # backward: the 32x32x16 dQ and dK/dV kernels (default) vs the 16-row chunked ones vs fp32
     do = _r(B, T, H * hd, seed=41)
@@ -284,8 +284,6 @@ def test_attention_fwd32_vs_chunk_and_reference(cuda, B, T, H, spike):
         _close(m3[:, :, i], r3[:, :, i], 3e-2, f"attn32_merged_d{n}")
     assert torch.equal(d, A.attn_bwd(qkv, o, lse, do, H))  # deterministic
     assert torch.equal(d8, A.attn_bwd(qkv, o, lse, do, H, flags=8))
-    # round-5 pipeline: identical arithmetic in identical order -> bitwise equal to the merged launch
-    assert torch.equal(d8, A.attn_bwd(qkv, o, lse, do, H, flags=16))
 
 
 @pytest.mark.parametrize("B,T,H", [(2, 512, 4), (1, 200, 3), (2, 64, 2)])

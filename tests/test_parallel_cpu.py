@@ -86,6 +86,8 @@ def single():
     ("pp", 4, {"dp": 2, "pp_microbatches": 2, "pp_clip": "global"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "gpipe"}),
+    ("pp", 2, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),
+    ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),
 ])
 def test_layout_matches_single_process(single, parallel, world, kw):
     res = _run(parallel, world, **kw)

@@ -13,14 +13,36 @@ from distributed_training_compare_jax_amd.parallel import pp as PP
 
 
 @pytest.mark.parametrize("model", ["pair", "rank"])
-@pytest.mark.parametrize("kind", ["gpipe", "1f1b"])
+@pytest.mark.parametrize("kind", ["gpipe", "1f1b", "zb"])
 @pytest.mark.parametrize("S", [1, 2, 3, 4, 8])
 def test_programs_never_deadlock(kind, S, model):
     """Both queue models: per-pair streams, and one serialised stream per rank (PyTorch's coalesced
     p2p on RCCL runs every grouped call of a rank on its group communicator's single stream)."""
     for M in range(1, 17):
         c = PP.simulate(kind, S, M, model=model)
-        assert c["compute"] == 2 * M * S  # every stage: one forward and one backward per microbatch
+        per = 3 if kind == "zb" else 2  # zb: forward, input-gradient backward and weight-gradient items
+        assert c["compute"] == per * M * S
+
+
+@pytest.mark.parametrize("S,M", [(2, 2), (4, 4), (4, 8), (8, 8), (8, 16)])
+def test_zero_bubble_programs(S, M):
+    """zb = 1F1B's messages in 1F1B's order plus W items: every W after its own B, each microbatch's F, B
+    and W exactly once; the timed replay (equal F / B / W costs) shortens the step and the bubble, to at
+    most 25 % at 8 stages x 8 microbatches (1F1B: 47 %)."""
+    for s, prog in enumerate(PP.zb_programs(S, M)):
+        base = PP.pp_program("1f1b", S, s, M)
+        assert [it for it in prog if it[0] != "W"] == base  # communication program unchanged
+        seen_b = set()
+        for it in prog:
+            if it[0] == "B":
+                seen_b.add(it[1])
+            if it[0] == "W":
+                assert it[1] in seen_b, (s, it)
+        assert sorted(it[1] for it in prog if it[0] == "W") == list(range(M))
+    z, o = PP.estimate("zb", S, M), PP.estimate("1f1b", S, M)
+    assert z["makespan"] < o["makespan"] and z["bubble"] < o["bubble"]
+    if (S, M) == (8, 8):
+        assert z["bubble"] <= 0.25, z
 
 
 def test_simulator_catches_the_ungrouped_1f1b_order(monkeypatch):
