@@ -114,14 +114,19 @@ def main():
     # 128 x 64CB kernel for multi-round problems too (DTC_GEMM8N bit 4), "n8w4" = with 128 x 256 tiles
     L = N.lib()
     # "n8k768": one-round gemm8n problems down to K = 768 (the out_proj forward / dgrad)
-    variants = {"ours": (3, 0, 1024)}
+    # "r8": the mixed-width 256-row plan (DTC_GEMM8R=1, bf16 epilogues), "r8f": also fp32 outputs (=3)
+    r8_default = L.dtc_gemm_set_r8(0)
+    variants = {"ours": (3, 0, 1024, r8_default)}
     for v in [x for x in a.variants.split(",") if x]:
-        variants[v] = {"n8": (7, 0, 1024), "n8w3": (7, 3, 1024), "n8w4": (7, 4, 1024), "n8k768": (3, 0, 768)}[v]
+        variants[v] = {"n8": (7, 0, 1024, 0), "n8w3": (7, 3, 1024, 0), "n8w4": (7, 4, 1024, 0),
+                       "n8k768": (3, 0, 768, 0), "r8": (3, 0, 1024, 1), "r8f": (3, 0, 1024, 3),
+                       "nor8": (3, 0, 1024, 0)}[v]
 
     def use(v):
         L.dtc_gemm_set_n8(v[0])
         L.dtc_gemm_set_n8_cb(v[1])
         L.dtc_gemm_set_n8_mink(v[2])
+        L.dtc_gemm_set_r8(v[3])
 
     for name, _, fn, ref, _ in cases:
         want = ref().float()

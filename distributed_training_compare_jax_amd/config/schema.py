@@ -138,6 +138,10 @@ class TrainConfig:
     dp_grad_dtype: str = "fp32"  # fp32 | bf16: DP gradient payload (bf16: all-to-all + fp32 shard sums)
     pp_comm_dtype: str = "fp32"  # fp32 | bf16: PP activation / gradient messages
     tp_comm_dtype: str = "fp32"  # fp32 | bf16: TP row-parallel / input-gradient partials (fp32 sums)
+    # Megatron-style sequence parallelism over the TP group (pp == 1, batch % tp == 0): the residual stream,
+    # LayerNorms and embedding output on batch/tp sequences per rank; reduce-scatter + all-gather in place of
+    # each TP all-reduce (models/gpt.py enable_sequence_parallel)
+    tp_sequence_parallel: bool = False
     pp_head_cost: Optional[float] = None  # lm_head + CE in blocks (None: parallel/mesh.py head_cost_blocks)
     warmup_steps: int = 5
     ckpt_every: int = 0

@@ -278,6 +278,67 @@ __device__ __forceinline__ void stage_out(const bf16* st, bf16* C, long ldc, int
   }
 }
 
+// stage_out for a wave tile COLS (16, 32 or 64) columns wide in the same [ROWS][64] stage image: LPR = COLS/8
+// lanes per row, 64/LPR rows per store instruction
+// EDGE = false: the caller guarantees the tile lies inside M x N (no bounds code at all)
+template <int ROWS, int COLS, bool NT = false, bool EDGE = true>
+__device__ __forceinline__ void stage_out_w(const bf16* st, bf16* C, long ldc, int m_base, int n_base, int M, int N,
+                                            int lane) {
+  static_assert(COLS % 16 == 0 && COLS <= 64, "16-B pieces of a 64-column stage row");
+  if constexpr (COLS == 64 && EDGE) {
+    stage_out<ROWS, NT>(st, C, ldc, m_base, n_base, M, N, lane);
+    return;
+  }
+  constexpr int LPR = COLS / 8, RPI = 64 / LPR;
+  const bool interior = !EDGE || (m_base + ROWS <= M && n_base + COLS <= N);  // wave-uniform
+#pragma unroll 4
+  for (int it = 0; it < ROWS / RPI; ++it) {
+    const int row = it * RPI + lane / LPR, p = lane % LPR;
+    u32x4 v = *(const u32x4*)(st + row * 64 + ((p ^ ((row >> 1) & 7)) << 3));
+    if (row & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+    const int m = m_base + row, n = n_base + p * 8;
+    bf16* c = C + (long)m * ldc + n;
+    if (interior || (m < M && n + 8 <= N)) {
+      if (NT) __builtin_nontemporal_store(v, (u32x4*)c);
+      else DTC_OUT_STORE((u32x4*)c, v);
+    } else if (m < M) {
+      const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+      for (int r = 0; r < 8; ++r) if (n + r < N) c[r] = b[r];
+    }
+  }
+}
+
+// the inverse: rows [m_base, +ROWS) x columns [n_base, +COLS) of a bf16 matrix into the stage image (zeros
+// outside M x N), so fragment-order reads (stage_get) see it in the accumulator layout
+template <int ROWS, int COLS, bool EDGE = true>
+__device__ __forceinline__ void stage_in(const bf16* __restrict__ src, long ld, bf16* st, int m_base, int n_base,
+                                         int M, int N, int lane) {
+  constexpr int LPR = COLS / 8, RPI = 64 / LPR, NIT = ROWS / RPI, G = NIT < 4 ? NIT : 4;
+  // groups of 4 rows-passes (4 x 16 B in flight per lane): the accumulators are live around this call
+#pragma unroll 1
+  for (int it0 = 0; it0 < NIT; it0 += G)
+#pragma unroll
+  for (int it = it0; it < it0 + G; ++it) {
+    const int row = it * RPI + lane / LPR, p = lane % LPR;
+    const int m = m_base + row, n = n_base + p * 8;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (!EDGE || (m < M && n + 8 <= N)) {
+      v = *(const u32x4*)(src + (long)m * ld + n);
+    } else if (m < M) {
+      bf16x8 b = {};
+      for (int r = 0; r < 8; ++r) if (n + r < N) b[r] = src[(long)m * ld + n + r];
+      v = __builtin_bit_cast(u32x4, b);
+    }
+    if (row & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+    *(u32x4*)(st + row * 64 + ((p ^ ((row >> 1) & 7)) << 3)) = v;
+  }
+}
+
+// the 4 values of fragment (row, 8-byte chunk) as stage_put wrote them
+__device__ __forceinline__ bf16x4 stage_get(const bf16* st, int row, int chunk) {
+  return *(const bf16x4*)(st + row * 64 + ((chunk ^ (row & 15)) << 2));
+}
+
 // fp32 per-wave stage [ROWS][COLS] (COLS = 32 or 64): 16-B chunk c of row r at c ^ (r % (COLS/4)),
 // conflict-free for the fragment writes (8 rows per lane group) and the row reads.  stage_out_f32
 // writes whole rows (128/256 B per row, 8/4 rows per instruction) and adds the fp32 residual
@@ -1211,6 +1272,19 @@ __device__ __forceinline__ void p8_lgkm_wait(bf16x8 (&fa)[2][2], bf16x8 (&fb)[3]
                :
                : "memory");
 }
+__device__ __forceinline__ void p8_lgkm_wait(bf16x8 (&fa)[2][2], bf16x8 (&fb)[2][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1]),
+                 "+v"(fb[1][0]), "+v"(fb[1][1])
+               :
+               : "memory");
+}
+__device__ __forceinline__ void p8_lgkm_wait(bf16x8 (&fa)[2][2], bf16x8 (&fb)[1][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[0][0]), "+v"(fb[0][1])
+               :
+               : "memory");
+}
 
 #define P8_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
@@ -1221,14 +1295,17 @@ __device__ __forceinline__ void vmcnt_c() { asm volatile("s_waitcnt vmcnt(%0)" :
 // whose N = 3072 makes exactly 2 rounds of 256 x 192 tiles (GPT-2 small fc1 forward / fc2 dgrad)
 // One 256 x 64*CB output tile (tm_idx, tn_idx) of split z: the body of gemm8p_kernel and of the
 // grouped weight-gradient kernel (gemm8p_group_kernel).  All LDS is the one array below.
-template <bool AK, bool BKM, int EPI, bool OUTF32, int CB>
-__device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb,
-                                            int M, int N, int K, int tm_idx, int tn_idx, int z, int split,
-                                            int k_per_split, float* __restrict__ slab, const Epi& e) {
+// smem: the kernel's ONE LDS array, >= 2 * (4 + CB) * P8_CHUNK elements ([buf][A img | B img]); a kernel
+// that runs tiles of two widths (gemm8r_kernel) passes the same array to both
+template <bool AK, bool BKM, int EPI, bool OUTF32, int CB, bool EDGE = true>
+__device__ __forceinline__ void gemm8p_tile_s(bf16* smem, const bf16* __restrict__ A, long lda,
+                                              const bf16* __restrict__ B, long ldb, int M, int N, int K, int tm_idx,
+                                              int tn_idx, int z, int split, int k_per_split, float* __restrict__ slab,
+                                              const Epi& e) {
   constexpr int TM = 8, TN = CB;  // 16x16 fragments per wave: 128 (m) x 16*CB (n)
   constexpr int WN = 16 * CB;     // columns per wave
   static_assert(CB == 4 || (EPI != EPI_LMHEAD), "the CE epilogue assumes 64-column waves");
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (4 + CB) * P8_CHUNK];  // [buf][A img | B img] (the only LDS object)
+  static_assert(CB >= 1 && CB <= 4, "1..4 column chunks of 64");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;  // M half (= wave group), 64-column slice
   const int m0 = tm_idx * BIG, n0 = tn_idx * (64 * CB);
@@ -1248,8 +1325,11 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
   auto dmaA = [&](int t, int q) { p8_dma<AK>(A, lda, m0, M, kbeg + t * 64, imgA(t), q, wave, lane); };
   auto dmaB = [&](int t, int q) { p8_dma<BKM>(B, ldb, n0, N, kbeg + t * 64, imgB(t), q, wave, lane); };
 
+  // the 256^2 kernels (EDGE) prefetch the bias of a plain store with the LM-head operands; gemm8r's tiles load
+  // it in the epilogue (16 fewer registers live through the main loop)
+  constexpr bool PRE_BIAS = EDGE && CB == 4 && EPI == EPI_STORE && !OUTF32;
   EpiPre<TN, TM> pre;  // epilogue operands: loaded ahead of every DMA, retired by the prologue wait
-  if (split == 1 && (EPI == EPI_LMHEAD || EPI == EPI_STORE))
+  if (split == 1 && (EPI == EPI_LMHEAD || PRE_BIAS))
     epi_prefetch<TN, TM>(e, m0 + wr * 128, n0 + wc * WN, lane, EPI == EPI_LMHEAD, pre);
   // prologue: B(0), A(0), B(1) in flight; wait for the first two
 #pragma unroll
@@ -1326,7 +1406,8 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
       if (p == 0) {
         if (more1) vmcnt_c<CB + 2>(); else P8_VMCNT(0);  // A chunks 1,3 of t landed (B(t+1), A(t+1) 0,2 younger)
       } else if (p == 2) {
-        if (more2) P8_VMCNT(4); else if (more1) P8_VMCNT(2); else P8_VMCNT(0);
+        // younger than A(t+1) chunks 0,2 and B(t+1): A(t+1) 1,3 + the B(t+2) chunks issued in phase 2
+        if (more2) vmcnt_c<2 + (CB < 2 ? CB : 2)>(); else if (more1) P8_VMCNT(2); else P8_VMCNT(0);
       }
       __builtin_amdgcn_s_barrier();
     }
@@ -1373,25 +1454,89 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
     lmhead_epilogue<TN, TM, true, true>(acc, e, m0 + wr * 128, n0 + wc * 64, tn_idx * 4 + wc, lane, pre, stage);
     return;
   }
-  if constexpr (CB == 4 && EPI == EPI_STORE && !OUTF32) {
+  // staged bf16 epilogue: the 256^2 kernels' plain stores, gemm8r's plain, GELU-pair and dGELU stores
+  constexpr bool STAGED = !OUTF32 && ((EPI == EPI_STORE && (CB == 4 || !EDGE)) ||
+                                      (!EDGE && (EPI == EPI_DGELU || EPI == EPI_GELU)));
+  if constexpr (STAGED) {
+    // bf16 outputs through the wave's LDS stage (128 rows x 64 columns, WN of them used): whole-row
+    // 16-B stores instead of 16 rows x 8 B per fragment store.  GELU: two passes (C = gelu'(u), then
+    // aux_out = gelu(u)).  DGELU: the wave's u tile is staged first (row loads, fragment-order LDS reads)
+    const int mb = m0 + wr * 128, nb = n0 + wc * WN;
     f32x4 bb[TN];
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wc * 64 + i * 16 + g4;
-      bb[i] = pre.bb[i];
-      if (e.bias && n < N && n + 4 > N)
-        for (int r = 0; r < 4; ++r) bb[i][r] = n + r < N ? e.bias[n + r] : 0.f;
+      const int n = nb + i * 16 + g4;
+      bb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (PRE_BIAS) {
+        bb[i] = pre.bb[i];
+        if (e.bias && n < N && n + 4 > N)
+          for (int r = 0; r < 4; ++r) bb[i][r] = n + r < N ? e.bias[n + r] : 0.f;
+      } else if (e.bias) {
+        if (!EDGE || n + 4 <= N) bb[i] = *(const f32x4*)(e.bias + n);
+        else for (int r = 0; r < 4; ++r) bb[i][r] = n + r < N ? e.bias[n + r] : 0.f;
+      }
+    }
+    if constexpr (EPI == EPI_DGELU) {
+      // the wave's u tile into its own stage (LDS ops of one wave complete in order: no barrier); each
+      // fragment below reads its u values from the very slot its result then overwrites
+      stage_in<128, WN, EDGE>((const bf16*)e.aux, e.ldaux, stage, mb, nb, M, N, lane);
+    }
+    if constexpr (EPI == EPI_GELU) {
+      // two halves of 64 rows: the pair (gelu'(u), gelu(u)) of each fragment computed once and staged as
+      // stage rows [0, 64) and [64, 128), then both 64-row slabs stored (two full passes over the 128
+      // accumulators spilled: the compiler kept the first pass's GELU values for the second)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+        for (int jj = 0; jj < TM / 2; ++jj)
+#pragma unroll
+          for (int i = 0; i < TN; ++i) {
+            const int j = hf * (TM / 2) + jj;
+            bf16x4 od, og;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float gv, dgv;
+              gelu_tanh_and_grad_f(e.alpha * acc[i][j][r] + bb[i][r], gv, dgv);
+              od[r] = f2bf(dgv);
+              og[r] = f2bf(gv);
+            }
+            stage_put(stage, jj * 16 + (lane & 15), i * 4 + (lane >> 4), od);
+            stage_put(stage, 64 + jj * 16 + (lane & 15), i * 4 + (lane >> 4), og);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        // gelu'(u) is read only in the backward: non-temporal
+        stage_out_w<64, WN, true, EDGE>(stage, (bf16*)e.C, e.ldc, mb + hf * 64, nb, M, N, lane);
+        stage_out_w<64, WN, false, EDGE>(stage + 64 * 64, (bf16*)e.aux_out, e.ldc, mb + hf * 64, nb, M, N, lane);
+      }
+      return;
     }
 #pragma unroll
-    for (int j = 0; j < TM; ++j)
+    for (int pass = 0; pass < 1; ++pass) {
 #pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        bf16x4 ob;
+      for (int j = 0; j < TM; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ob[r] = f2bf(e.alpha * acc[i][j][r] + bb[i][r]);
-        stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
-      }
-    stage_out<128>(stage, (bf16*)e.C, e.ldc, m0 + wr * 128, n0 + wc * 64, M, N, lane);
+        for (int i = 0; i < TN; ++i) {
+          bf16x4 ob, uf = {};
+          if constexpr (EPI == EPI_DGELU) uf = stage_get(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = e.alpha * acc[i][j][r] + bb[i][r];
+            if constexpr (EPI == EPI_GELU) {
+              float gv, dgv;
+              gelu_tanh_and_grad_f(v, gv, dgv);
+              v = pass == 1 ? gv : dgv;
+            }
+            if constexpr (EPI == EPI_DGELU) v *= (float)uf[r];
+            ob[r] = f2bf(v);
+          }
+          stage_put(stage, j * 16 + (lane & 15), i * 4 + (lane >> 4), ob);
+          // GELU / dGELU: one fragment at a time (the scheduler otherwise interleaves all 32 fragments' GELU
+          // temporaries or u reads next to the 128 accumulator registers and spills)
+          if constexpr (EPI == EPI_DGELU || EPI == EPI_GELU) __builtin_amdgcn_sched_barrier(0);
+        }
+      if (EPI == EPI_GELU && pass == 0) stage_out_w<128, WN, true, EDGE>(stage, (bf16*)e.C, e.ldc, mb, nb, M, N, lane);
+      else stage_out_w<128, WN, false, EDGE>(stage, (bf16*)(pass == 0 ? e.C : e.aux_out), e.ldc, mb, nb, M, N, lane);
+    }
     return;
   }
   if (EPI == EPI_NONE) {  // microbenchmark: main loop only (keep the accumulators live)
@@ -1416,6 +1561,15 @@ __device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda
   }
 }
 
+template <bool AK, bool BKM, int EPI, bool OUTF32, int CB>
+__device__ __forceinline__ void gemm8p_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb,
+                                            int M, int N, int K, int tm_idx, int tn_idx, int z, int split,
+                                            int k_per_split, float* __restrict__ slab, const Epi& e) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (4 + CB) * P8_CHUNK];  // the only LDS object
+  gemm8p_tile_s<AK, BKM, EPI, OUTF32, CB>(smem, A, lda, B, ldb, M, N, K, tm_idx, tn_idx, z, split, k_per_split, slab,
+                                          e);
+}
+
 template <bool AK, bool BKM, int EPI, bool OUTF32, int CB = 4>
 __global__ void __launch_bounds__(NT2, 1)
 gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, int M, int N, int K,
@@ -1427,6 +1581,57 @@ gemm8p_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, 
   const int gm_eff = min(gm, tiles_m - grp * gm);
   const int tm_idx = grp * gm + in_g % gm_eff, tn_idx = in_g / gm_eff;
   gemm8p_tile<AK, BKM, EPI, OUTF32, CB>(A, lda, B, ldb, M, N, K, tm_idx, tn_idx, z, split, k_per_split, slab, e);
+}
+
+// ============================================================================================
+// gemm8r: the 256-row tiles of gemm8p_kernel in ONE launch of two column widths, for the layer GEMMs
+// whose 256^2 grid is a full round plus a remainder (GPT-2 small at 8192 tokens: qkv forward 288 tiles =
+// 1.125 rounds, fc1 forward / fc2 NT dgrad 384 = 1.5 rounds) or less than a round (N = 768: 96 tiles):
+// columns [0, n_split) run as 256 x 256 tiles (whole rounds of 256 blocks), columns [n_split, N) as
+// 256 x 64*CB2 tiles, sized so the remainder is at most one round of narrower tiles.  The remainder
+// blocks take the higher block ids: the hardware dispatches them as the CUs of the first round free up.
+// No cross-block exchange (no split-K slabs): every output element is summed in one block in K order.
+// One LDS array for both widths (the 256^2 tile's 128 KB).
+struct R8Args {
+  const bf16* A; long lda;
+  const bf16* B; long ldb;
+  int M, N, K, n_split;
+  int tm, tn1, gm1, nb1;  // part 1: tiles_m x tn1 tiles of 256 x 256 (nb1 blocks)
+  int tn2, gm2;           // part 2: tiles_m x tn2 tiles of 256 x 64*CB2
+};
+
+template <bool AK, bool BKM, int EPI, bool OUTF32, int CB2>
+__global__ void __launch_bounds__(NT2, 1) gemm8r_kernel(R8Args a, Epi e) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (4 + 4) * P8_CHUNK];  // the only LDS object
+  const int b = (int)blockIdx.x;
+  auto order = [](int lid, int tm, int tn, int gm, int& tm_idx, int& tn_idx) {
+    const int grp = lid / (gm * tn), in_g = lid % (gm * tn);
+    const int gm_eff = min(gm, tm - grp * gm);
+    tm_idx = grp * gm + in_g % gm_eff;
+    tn_idx = in_g / gm_eff;
+  };
+  int tm_idx, tn_idx;
+  if (b < a.nb1) {
+    order(xcd_remap(b, a.nb1), a.tm, a.tn1, a.gm1, tm_idx, tn_idx);
+    Epi e1 = e;
+    e1.N = a.n_split;
+    gemm8p_tile_s<AK, BKM, EPI, OUTF32, 4, false>(smem, a.A, a.lda, a.B, a.ldb, a.M, a.n_split, a.K, tm_idx, tn_idx,
+                                                   0, 1, a.K, nullptr, e1);
+    return;
+  }
+  const int nb2 = a.tm * a.tn2;
+  order(xcd_remap(b - a.nb1, nb2), a.tm, a.tn2, a.gm2, tm_idx, tn_idx);
+  // part 2 as its own problem: columns n_split.. of B / C / bias / aux
+  const int ns = a.n_split;
+  Epi e2 = e;
+  e2.N = a.N - ns;
+  e2.C = OUTF32 ? (void*)((float*)e.C + ns) : (void*)((bf16*)e.C + ns);
+  if (e.bias) e2.bias = e.bias + ns;
+  if (e.aux) e2.aux = (const void*)((const bf16*)e.aux + ns);
+  if (e.aux_out) e2.aux_out = (void*)((bf16*)e.aux_out + ns);
+  const bf16* B2 = BKM ? a.B + (long)ns * a.ldb : a.B + ns;
+  gemm8p_tile_s<AK, BKM, EPI, OUTF32, CB2, false>(smem, a.A, a.lda, B2, a.ldb, a.M, a.N - ns, a.K, tm_idx, tn_idx, 0,
+                                                   1, a.K, nullptr, e2);
 }
 
 // Grouped weight gradients: dW_i = beta*dW_i + dY_i^T X_i (+ db_i = beta*db_i + colsum(dY_i)) for up to
@@ -2413,10 +2618,11 @@ struct Plan {
   int bm, bn, bk, split;
 };
 
-// DTC_GEMM_DMA bit mask: 1 = 64x64 forward layout (default: measured fc2/out_proj fwd 22 -> 18.6
-// us), 2 = 64x64 dgrad/wgrad layouts (measured slower: off), 4 = 128x128 (measured no gain: off)
-inline int gemm_dma_mask() {
-  static const int m = [] { const char* v = getenv("DTC_GEMM_DMA"); return v ? atoi(v) : 1; }();
+// LDS-DMA variant of the 64x64 forward-layout tiles (measured fc2/out_proj fwd 22 -> 18.6 us; the
+// dgrad / wgrad layouts and the 128x128 tiles measured slower or equal on it and stay register-staged).
+// DTC_GEMM_DMA=0: register-staged everywhere (diagnostic)
+inline bool gemm_dma_fwd64() {
+  static const bool m = [] { const char* v = getenv("DTC_GEMM_DMA"); return v ? atoi(v) != 0 : true; }();
   return m;
 }
 
@@ -2434,18 +2640,13 @@ Plan make_plan(int M, int N, int K, int allow_split) {
     p.split = (int)std::max(1L, std::min((long)nk / 64, (512 + t128 - 1) / t128));
     return p;
   }
-  static const int wgrad_tile = [] { const char* v = getenv("DTC_WGRAD_TILE"); return v ? atoi(v) : 128; }();  // single-stream A/B: 128 (256 blocks) 5.99 vs 64 6.05 ms
-  if (allow_split == 1 && wgrad_tile == 128 && t128 < 256) {  // weight gradients: 128^2 tiles + split-K
+  // weight gradients: 128^2 tiles + split-K (A/B: 5.99 vs 6.05 ms on 64^2 tiles)
+  if (allow_split == 1 && t128 < 256) {
     static const int target = [] { const char* v = getenv("DTC_WGRAD_BLOCKS"); return v ? atoi(v) : 256; }();
     while (t128 * p.split < target && nk / (p.split * 2) >= 8) p.split *= 2;
     return p;
   }
-  if (t128 >= 256) {
-    // DTC_BK128=32: 128^2 tiles with BK 32 (40 KB LDS instead of 80 -> up to 4 blocks per CU)
-    static const int bk128 = [] { const char* v = getenv("DTC_BK128"); return v ? atoi(v) : 64; }();
-    if (bk128 == 32) p.bk = 32;
-    return p;
-  }
+  if (t128 >= 256) return p;
   {
     p.bm = p.bn = 64;
     const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
@@ -2522,24 +2723,23 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
   if (tiles_n <= 16) gm = std::max(1, std::min(tiles_m, (ntiles / 8 + tiles_n - 1) / tiles_n));
   dim3 grid(ntiles * p.split);
   const int ab = operand_bytes(AK, a.M, a.K, a.lda), bb = operand_bytes(BKM, a.N, a.K, a.ldb);
-  // DMA-pipelined variant when gemm_dma_mask() allows (128x128 stages from DTC_DMA_STAGES128)
-  const int dma_mask = gemm_dma_mask();
-  static const int st128 = [] { const char* v = getenv("DTC_DMA_STAGES128"); return v ? atoi(v) : 2; }();
-  const int dma_bit = BM == 64 ? ((AK && BKM) ? 1 : 2) : 4;
-  if (p.bk == 64 && (dma_mask & dma_bit)) {
-    if constexpr (BM == 64)
+  if constexpr (BM == 64 && AK && BKM) {
+    if (p.bk == 64 && gemm_dma_fwd64()) {
       hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, 4, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A,
                          a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
                          (float*)a.workspace, e);
-    else if (st128 >= 3)
-      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, 3, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A,
-                         a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
-                         (float*)a.workspace, e);
-    else
-      hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, 2, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A,
-                         a.lda, (const bf16*)a.B, a.ldb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
-                         (float*)a.workspace, e);
-  } else if (p.bk == 32)
+      DTC_CHECK_LAUNCH();
+      if (p.split > 1 && !a.defer_reduce) {
+        long MN = (long)a.M * a.N;
+        int blocks = (int)((MN / 4 + 255) / 256);
+        hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, p.split, MN,
+                           (float*)a.C, a.ldc, a.N, a.beta);
+        DTC_CHECK_LAUNCH();
+      }
+      return 0;
+    }
+  }
+  if (p.bk == 32)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKM, EPI, OUTF32>), grid, dim3(NT), 0, st, (const bf16*)a.A, a.lda,
                        ab, (const bf16*)a.B, a.ldb, bb, a.M, a.N, a.K, tiles_m, tiles_n, gm, p.split, kps,
                        (float*)a.workspace, e);
@@ -2674,6 +2874,70 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
   return 0;
 }
 
+// ---- gemm8r plans (layer GEMMs on 256-row tiles of two widths, one launch) ---------------------------
+// DTC_GEMM8R: 1 = use the plan for NT problems (forwards, dgrads on transposed weights) with a bf16 staged
+// epilogue (plain + bias, GELU pair, dGELU) whose 256^2 grid is not whole rounds; 2 = also fp32 outputs;
+// 0 = off.
+static int g_r8_mask = [] { const char* v = getenv("DTC_GEMM8R"); return v ? atoi(v) : 0; }();
+
+struct R8Plan {
+  int n_split = -1, cb2 = 0;
+};
+
+static R8Plan r8_plan(int layout, int M, int N, int K, int epi, bool f32) {
+  R8Plan r;
+  if (!g_r8_mask || layout != 0 || M % BIG || N % 64 || K % 64 || K < 256 || K > 4096 || N > 16384) return r;
+  if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU)) return r;
+  if (f32 && (epi != EPI_STORE || !(g_r8_mask & 2))) return r;
+  const int tm = M / BIG, q = N / BIG, cus = cu_count();
+  if ((long)tm * q % cus == 0 && q > 0 && N % BIG == 0) return r;  // whole rounds of 256^2 tiles: launch_big
+  int c1 = q;
+  while (c1 > 0 && ((long)tm * c1) % cus) --c1;  // whole rounds of 256^2 tiles
+  const int u = (N - BIG * c1) / 64;
+  int best = 0;
+  long best_cost = 0;
+  for (int cb : {4, 2, 1}) {
+    if (u % cb) continue;
+    const long blocks = (long)tm * (u / cb);
+    const long cost = ((blocks + cus - 1) / cus) * cb;  // rounds x tile width
+    if (!best || cost < best_cost) {
+      best = cb;
+      best_cost = cost;
+    }
+  }
+  if (!best) return r;
+  r.n_split = BIG * c1;
+  r.cb2 = best;
+  return r;
+}
+
+template <bool AK, bool BKM, int EPI, bool OUTF32, int CB2>
+int launch_r8_cb(const GemmArgs& a, const R8Plan& pl, hipStream_t st) {
+  Epi e{};
+  e.M = a.M; e.N = a.N; e.C = a.C; e.ldc = a.ldc; e.bias = a.bias; e.aux = a.aux; e.ldaux = a.ldaux;
+  e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
+  R8Args r;
+  r.A = (const bf16*)a.A; r.lda = a.lda; r.B = (const bf16*)a.B; r.ldb = a.ldb;
+  r.M = a.M; r.N = a.N; r.K = a.K; r.n_split = pl.n_split;
+  r.tm = a.M / BIG;
+  r.tn1 = pl.n_split / BIG;
+  r.nb1 = r.tm * r.tn1;
+  r.gm1 = r.tn1 > 0 ? std::max(1, std::min(r.tm, 32 / r.tn1)) : 1;
+  r.tn2 = (a.N - pl.n_split) / (64 * CB2);
+  r.gm2 = std::max(1, std::min(r.tm, 32 / std::max(1, r.tn2)));
+  const int grid = r.nb1 + r.tm * r.tn2;
+  hipLaunchKernelGGL((gemm8r_kernel<AK, BKM, EPI, OUTF32, CB2>), dim3(grid), dim3(NT2), 0, st, r, e);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int EPI, bool OUTF32>
+int launch_r8(const GemmArgs& a, const R8Plan& pl, hipStream_t st) {
+  if (pl.cb2 == 4) return launch_r8_cb<true, true, EPI, OUTF32, 4>(a, pl, st);
+  if (pl.cb2 == 2) return launch_r8_cb<true, true, EPI, OUTF32, 2>(a, pl, st);
+  return launch_r8_cb<true, true, EPI, OUTF32, 1>(a, pl, st);
+}
+
 // ---- gemm8n_kernel plans (layer GEMMs, 128 x 64*CB tiles) ----------------------------------------
 // DTC_GEMM8N bit mask: 1 = forwards and NT dgrads (layout 0), 2 = NN dgrads (layout 1), 4 = also
 // multi-round problems.  A problem takes it when its tile count on 128x192 (CB 3) or 128x256 (CB 4)
@@ -2754,10 +3018,9 @@ int launch_pair_t(const GemmArgs& a1, const Plan& p1, const GemmArgs& a2, const 
   const GemmLaunch g1 = make_launch<BM1, BM1, true, BKM1>(a1, p1);
   const GemmLaunch g2 = make_launch<BM2, BM2, false, false>(a2, p2);
   if (g1.nblocks % 8 && g2.nblocks % 8) return 1100;  // XCD maps would disagree: not pairable
-  // DTC_PAIR_WGRAD_FIRST=1: dispatch the weight-gradient blocks first (when their count keeps the XCD
-  // maps aligned).  Measured slower (interleaved A/B, min of 4: 5.348 vs 5.284 ms/step): off
-  static const int wf = [] { const char* v = getenv("DTC_PAIR_WGRAD_FIRST"); return v ? atoi(v) : 0; }();
-  const int second_first = (wf && g2.nblocks % 8 == 0) || g1.nblocks % 8 ? 1 : 0;
+  // the dgrad blocks dispatch first unless only the weight-gradient count keeps the XCD maps aligned
+  // (weight gradients first measured slower: 5.348 vs 5.284 ms/step, round 2)
+  const int second_first = g1.nblocks % 8 ? 1 : 0;
   hipLaunchKernelGGL((gemm_pair_kernel<C1, C2>), dim3(g1.nblocks + g2.nblocks), dim3(NT), 0, st, g1, g2,
                      second_first);
   DTC_CHECK_LAUNCH();
@@ -2905,8 +3168,6 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   const Plan p2 = make_plan(a2->M, a2->N, a2->K, 1);
   if (p1.split != 1 || p1.bk != 64 || p2.bk != 64) return 1100;
   if (p2.split > 1 && (!a2->defer_reduce || a2->ws_bytes < (long)p2.split * a2->M * a2->N * 4)) return 1100;
-  const int dma = gemm_dma_mask();
-  if ((dma & (p1.bm == 64 ? 2 : 4)) || (dma & (p2.bm == 64 ? 2 : 4))) return 1100;
   if (a1->epi == EPI_DGELU && !a1->c_f32) return launch_pair_w<EPI_DGELU, false>(*a1, p1, *a2, p2, st);
   if (a1->epi == EPI_STORE && a1->c_f32) return launch_pair_w<EPI_STORE, true>(*a1, p1, *a2, p2, st);
   if (a1->epi == EPI_STORE && !a1->c_f32) return launch_pair_w<EPI_STORE, false>(*a1, p1, *a2, p2, st);
@@ -2998,9 +3259,7 @@ int dtc_gemm_wgrad_split(int M, int N, int K, int has_db) {
 // gradient (GemmArgs.colsum); the 256^2 and DMA kernels cannot
 int dtc_gemm_wgrad_fuses_colsum(int M, int N, int K) {
   if (big_split(2, M, N, K)) return g_wgrad_cs256 ? 1 : 0;  // gemm8p_kernel sums it with MFMAs
-  const Plan p = make_plan(M, N, K, 1);
-  if (p.bk != 64) return 1;
-  return (gemm_dma_mask() & (p.bm == 64 ? 2 : 4)) ? 0 : 1;
+  return 1;  // the register-staged 64^2 / 128^2 weight-gradient plans (never the DMA variant)
 }
 
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
@@ -3090,12 +3349,28 @@ int dtc_wgrad_group(const WgBatch* in, hipStream_t st) {
   return 0;
 }
 
+// gemm8r plan mask (DTC_GEMM8R at load time); returns the previous value (tests / A/B)
+int dtc_gemm_set_r8(int mask) {
+  const int old = g_r8_mask;
+  g_r8_mask = mask;
+  return old;
+}
+
 int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->K % 32 != 0) return 1001;               // K must be a multiple of 32 (BK = 64, or 32)
   if (a->lda % 8 || a->ldb % 8 || a->ldc % 4) return 1002;  // 16-B row alignment
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
+  if (a->layout == 0 && !a->colsum && a->alpha == 1.f && a->beta == 0.f &&
+      !n8_cb(a->layout, a->M, a->N, a->K, epi)) {
+    const R8Plan pl = r8_plan(a->layout, a->M, a->N, a->K, epi, f32);
+    if (pl.cb2) {
+      if (epi == EPI_STORE) return f32 ? launch_r8<EPI_STORE, true>(*a, pl, st) : launch_r8<EPI_STORE, false>(*a, pl, st);
+      if (epi == EPI_GELU) return launch_r8<EPI_GELU, false>(*a, pl, st);
+      if (epi == EPI_DGELU) return launch_r8<EPI_DGELU, false>(*a, pl, st);
+    }
+  }
   if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f) {
     const int cb = n8_cb(a->layout, a->M, a->N, a->K, epi);
     if (cb) {
@@ -3127,6 +3402,7 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
     if (bs0 == 1) {
       if (epi == EPI_LMHEAD) return launch_big<true, true, EPI_LMHEAD, false>(*a, 1, st);
       if (epi == EPI_GELU) return launch_big<true, true, EPI_GELU, false>(*a, 1, st);
+      if (epi == EPI_DGELU && !f32) return launch_big<true, true, EPI_DGELU, false>(*a, 1, st);
       if (epi == EPI_RESID) return launch_big<true, true, EPI_RESID, true>(*a, 1, st);
       if (epi == EPI_STORE)
         return f32 ? launch_big<true, true, EPI_STORE, true>(*a, 1, st) : launch_big<true, true, EPI_STORE, false>(*a, 1, st);

@@ -193,6 +193,59 @@ __global__ void p2p_all_gather_bf16_kernel(PeerTable t, int world, long n8, long
   }
 }
 
+// ---------------------------------------------------------------- sequence parallelism (tp_sequence_parallel)
+// The residual stream is split by rows over the TP ranks, so the row-parallel GEMMs' partial sums are
+// REDUCE-SCATTERED (each rank only needs its own rows) and the LayerNorm outputs / residual gradients
+// that feed the column-parallel GEMMs are ALL-GATHERED.  Both are one barrier each: the payload (the
+// whole [rows, cols] partial, or this rank's slice at its row offset) is in every rank's buffer half
+// before the barrier; afterwards rank r reads what it needs straight from the peers' halves.
+//
+// reduce-scatter: out[i] (fp32, this rank's n_loc elements) = resid[i] + bias[col] + sum_p partial_p[lo + i],
+// summed in rank order (the same order on every rank: a row's value does not depend on who owns it)
+template <bool BF16>
+__global__ void p2p_rs_kernel(PeerTable t, int rank, int world, long n8_loc, long half_bytes, float* __restrict__ out,
+                              const float* __restrict__ resid, const float* __restrict__ bias, int ncols,
+                              const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 2) >> 1) & 1;
+  const long off = FLAG_BYTES + h * half_bytes;
+  const long lo8 = (long)rank * n8_loc;
+  DTC_ASSERT(rank < world && (BF16 ? 16 : 32) * n8_loc * world <= half_bytes && (!bias || ncols % 8 == 0));
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8_loc; i += (long)gridDim.x * blockDim.x) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < world; ++p) {
+      if constexpr (BF16) {
+        add8(a, ((const bf16x8*)(t.base[p] + off))[lo8 + i]);
+      } else {
+        const f32x4* src = (const f32x4*)(t.base[p] + off) + 2 * (lo8 + i);
+        const f32x4 v0 = src[0], v1 = src[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { a[e] += v0[e]; a[e + 4] += v1[e]; }
+      }
+    }
+    finish8(a, i, out, resid, bias, ncols);  // i indexes this rank's rows: column = (8 i) % ncols
+  }
+}
+
+// stage n16 16-byte pieces of x into own half at piece offset `at` (the all-gather's slot / a full partial)
+__global__ void p2p_stage16_kernel(const u32x4* __restrict__ x, PeerTable t, int rank, long at, long n16,
+                                   long half_bytes, const uint32_t* __restrict__ epoch) {
+  const int h = (epoch[0] >> 1) & 1;
+  DTC_ASSERT(16 * (at + n16) <= half_bytes && rank >= 0);
+  u32x4* dst = (u32x4*)(t.base[rank] + FLAG_BYTES + h * half_bytes) + at;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x) dst[i] = x[i];
+}
+
+// all-gather: out[q * n16_loc + i] = rank q's slot (16-byte pieces, any element type); own slot local
+__global__ void p2p_ag_kernel(PeerTable t, int world, long n16_loc, long half_bytes, u32x4* __restrict__ out,
+                              const uint32_t* __restrict__ epoch) {
+  const int h = ((epoch[0] - 2) >> 1) & 1;
+  const long off = FLAG_BYTES + h * half_bytes;
+  const long n = n16_loc * world;
+  DTC_ASSERT(16 * n <= half_bytes && world >= 1);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = ((const u32x4*)(t.base[(int)(i / n16_loc)] + off))[i];
+}
+
 // ---------------------------------------------------------------- intra-device stream flags
 // Cross-stream dependencies between two separately captured hipGraphs (main / side) on the SAME
 // device: a producer stream bumps flags[k] to its replay epoch (agent-scope release, after all of
@@ -362,6 +415,63 @@ int dtc_p2p_allreduce_bf16(const bf16* x, float* out, long n, void* const* bases
   DTC_CHECK_LAUNCH();
   hipLaunchKernelGGL(p2p_all_gather_bf16_kernel, dim3(blocks), dim3(256), 0, st, t, world, n8, half_bytes, out, resid,
                      bias, ncols, epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- sequence-parallel collectives (one barrier each, epoch + 2 per call like the one-shot all-reduce)
+// reduce-scatter of a [W * n_loc] partial (bf16 if bf16 else fp32) into this rank's n_loc fp32 elements:
+// out = resid + bias + sum_ranks partial[rank * n_loc .. +n_loc].  x == nullptr: the producer wrote the
+// partial into this call's buffer half (staged_out).  n_loc % 8 == 0; bias by column (ncols % 8 == 0,
+// n_loc % ncols == 0: whole rows per rank).
+int dtc_p2p_reduce_scatter(const void* x, int bf16, float* out, long n_loc, void* const* bases, int rank, int world,
+                           long half_bytes, uint32_t* epoch, int* err, const float* resid, const float* bias,
+                           int ncols, hipStream_t st) {
+  const long esz = bf16 ? 2 : 4;
+  if (world < 1 || world > P2P_MAX || n_loc % 8 || n_loc * world * esz > half_bytes ||
+      (bias && (ncols <= 0 || ncols % 8 || n_loc % ncols)))
+    return 4001;
+  PeerTable t;
+  for (int p = 0; p < P2P_MAX; ++p) t.base[p] = (unsigned char*)(p < world ? bases[p] : nullptr);
+  if (x) {
+    const long n16 = n_loc * world * esz / 16;
+    const int sb = (int)std::min(1024L, std::max(1L, (n16 + 255) / 256));
+    hipLaunchKernelGGL(p2p_stage16_kernel, dim3(sb), dim3(256), 0, st, (const u32x4*)x, t, rank, 0L, n16, half_bytes,
+                       epoch);
+    DTC_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 2);
+  DTC_CHECK_LAUNCH();
+  const long n8 = n_loc / 8;
+  const int blocks = (int)std::min(1024L, std::max(1L, (n8 + 255) / 256));
+  if (bf16)
+    hipLaunchKernelGGL(p2p_rs_kernel<true>, dim3(blocks), dim3(256), 0, st, t, rank, world, n8, half_bytes, out, resid,
+                       bias, ncols, epoch);
+  else
+    hipLaunchKernelGGL(p2p_rs_kernel<false>, dim3(blocks), dim3(256), 0, st, t, rank, world, n8, half_bytes, out,
+                       resid, bias, ncols, epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// all-gather of this rank's loc_bytes (x, a multiple of 16) into out [W * loc_bytes], rank-major.
+// x == nullptr: the producer already wrote the slot (staged_out at offset rank * loc_bytes).
+int dtc_p2p_all_gather(const void* x, void* out, long loc_bytes, void* const* bases, int rank, int world,
+                       long half_bytes, uint32_t* epoch, int* err, hipStream_t st) {
+  if (world < 1 || world > P2P_MAX || loc_bytes % 16 || loc_bytes * world > half_bytes) return 4001;
+  PeerTable t;
+  for (int p = 0; p < P2P_MAX; ++p) t.base[p] = (unsigned char*)(p < world ? bases[p] : nullptr);
+  const long n16 = loc_bytes / 16;
+  if (x) {
+    const int sb = (int)std::min(1024L, std::max(1L, (n16 + 255) / 256));
+    hipLaunchKernelGGL(p2p_stage16_kernel, dim3(sb), dim3(256), 0, st, (const u32x4*)x, t, rank, rank * n16, n16,
+                       half_bytes, epoch);
+    DTC_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(p2p_barrier_kernel, dim3(1), dim3(64), 0, st, t, rank, world, epoch, err, 2);
+  DTC_CHECK_LAUNCH();
+  const int blocks = (int)std::min(1024L, std::max(1L, (n16 * world + 255) / 256));
+  hipLaunchKernelGGL(p2p_ag_kernel, dim3(blocks), dim3(256), 0, st, t, world, n16, half_bytes, (u32x4*)out, epoch);
   DTC_CHECK_LAUNCH();
   return 0;
 }

@@ -37,14 +37,8 @@ from .params import head_split
 from ..parallel.buffers import FlatParams
 
 
-# where the lm_head weight gradient runs: on the backward side stream (default, overlaps the
-# last layers' backward) or on the main stream right after the dgrad (A/B knob)
 import os as _os
 
-_LMHEAD_WGRAD_MAIN = _os.environ.get("DTC_LMHEAD_WGRAD", "side") == "main"
-# side-stream schedule: 1 = the previous layer's weight gradients are forked one at a time between
-# this layer's dgrad GEMMs; 0 = one fork per layer after its dgrad chain
-_SIDE_INTERLEAVE = _os.environ.get("DTC_SIDE_INTERLEAVE", "0") == "1"  # measured: 1 is slower
 # ops/xent.py ce_dgrad_fused: "1" / "0", or "auto" (default) = fused for lm_head dgrads of at most
 # 4096 x 512 outputs (the reference model: 382 -> 341 us, profiles/r2_ab_ce_fused_dgrad.log); at GPT-2
 # small (8192 x 768: 96 tiles x split 2 = 192 blocks on 256 CUs) the separate CE pass + the DMA-staged
@@ -102,57 +96,6 @@ class NoComm:
         return t.unsqueeze(0)
 
 
-class SideStream:
-    """Runs weight-gradient work (wgrad GEMMs, bias column sums) on a second HIP stream.
-
-    In backward only the dgrad chain is on the critical path; each layer's 4 wgrad GEMMs and 4
-    bias reductions are independent of it, so they overlap the next dgrad kernels (these small
-    GEMMs fill only part of the 256 CUs).  Inputs are kept referenced until :meth:`join`, so the
-    caching allocator cannot hand their memory to the main stream while the side stream reads it.
-    Under hipGraph capture the fork/join become graph edges."""
-
-    def __init__(self, device, enabled: bool):
-        self.stream = torch.cuda.Stream(device) if (enabled and torch.device(device).type == "cuda") else None
-        self.keep = []
-        self._pending = []
-
-    def run(self, fn, *keep):
-        if self.stream is None:
-            fn()
-            return
-        self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream), G.workspace_role("side"):
-            fn()
-        self.keep.extend(keep)
-
-    def defer(self, fn, *keep):
-        """Queue side-stream work; :meth:`flush` forks once for everything queued.  In a replayed
-        hipGraph every fork/join is a cross-queue dependency costing ~10-15 us of idle time, so
-        a layer's four weight-gradient GEMMs (+ its norm chunk) go out as ONE fork after the
-        layer's dgrad chain instead of four forks interleaved with it."""
-        self._pending.append(fn)  # queued even without a stream: CPU runs keep the same ordering
-        if self.stream is not None:
-            self.keep.extend(keep)
-
-    def flush(self):
-        if not self._pending:
-            return
-        fns, self._pending = self._pending, []
-        self.run(lambda: [f() for f in fns])
-
-    def flush_one(self):
-        """Fork just the oldest queued item (interleaves the previous layer's weight gradients with
-        this layer's dgrad chain in capture order, which is what lets hipGraph replay overlap them)."""
-        if self._pending:
-            self.run(self._pending.pop(0))
-
-    def join(self):
-        self.flush()
-        if self.stream is not None:
-            torch.cuda.current_stream().wait_stream(self.stream)
-            self.keep.clear()
-
-
 @dataclass
 class StageLayout:
     layers: range
@@ -164,18 +107,18 @@ class GPTStage:
     """The slice of the GPT owned by one rank (all of it, a TP shard, or a PP stage)."""
 
     def __init__(self, cfg: ModelConfig, flat: FlatParams, layout: StageLayout, tp=None,
-                 dropout_seed: int = 0, act_dtype: torch.dtype = torch.bfloat16, side_stream: bool = True):
+                 dropout_seed: int = 0, act_dtype: torch.dtype = torch.bfloat16):
         self.cfg = cfg
-        self.side = SideStream(flat.device, side_stream)
-        # single-stream GPU backward: every off-critical-path reduction of a layer (split-K weight
-        # gradient slabs, LN dgamma/dbeta partials, bias column partials, grad-norm chunks) goes
-        # into ONE batched launch per layer (ops/reduce.py); with the side stream, per-op kernels
+        # one-stream GPU backward: every off-critical-path reduction of a layer (split-K weight gradient
+        # slabs, LN dgamma/dbeta partials, bias column partials, grad-norm chunks) goes into ONE batched
+        # launch per layer (ops/reduce.py).  (A second stream for the weight gradients measured slower on
+        # one GPU -- 6.00 vs 5.44 ms, round 2 -- and was removed: the grouped launches fill the chip instead.)
         dev = torch.device(flat.device)
         # 512 MB window: a layer's split-K weight-gradient slabs (GPT-2 medium: 4 x ~67 MB) + LN partials
-        self.red = GradReducer(dev, arena_mb=512) if (dev.type == "cuda" and self.side.stream is None) else None
+        self.red = GradReducer(dev, arena_mb=512) if dev.type == "cuda" else None
         self._bias_fused = set()  # layers whose fc2.b grad an upstream LN backward already produced
         # deferred optimizer (train/engine.py): params of layer l / "head" become valid when this
-        # side-stream event fires; the forward waits on it right before first use
+        # event fires; the forward waits on it right before first use
         self.param_ready: Dict = {}
         self.flat = flat
         self.layout = layout
@@ -195,7 +138,7 @@ class GPTStage:
         self.eps = cfg.layernorm_eps
         # Deferred weight gradients (set_wgrad_group): the dgrad chain runs alone and every (dY, X, dW, db)
         # of wgrad_group consecutive layers (0 = the whole stage, + the lm_head) goes out as ONE grouped
-        # launch of whole 256^2 tiles (ops/gemm.py wgrad_group) -- single-stream backward only
+        # launch of whole 256^2 tiles (ops/gemm.py wgrad_group)
         self.wg_group = -1  # -1 = off
         self.wg_queue = []
         # grad-norm partials from the grouped launch (engine: dp == 1 and one launch per step): the first
@@ -207,12 +150,16 @@ class GPTStage:
         # LayerNorm fused into the layer GEMMs (ops/ln_fused.py), set up by enable_ln_fusion
         self.ln_sync: Optional[LF.LnSync] = None
         self._fuse_fwd = self._fuse_bwd = False
+        # sequence parallelism (enable_sequence_parallel): residual stream / LayerNorms / embedding output on
+        # rows/tp rows per rank; the LN and row-parallel-bias grads are then per-rank partials (_sp_sum)
+        self.sp = False
+        self._sp_idx: Dict = {}
 
     def set_wgrad_group(self, layers: int):
         """Defer weight gradients to grouped launches of ``layers`` consecutive layers (0 = all layers of
         the stage in one launch, with the lm_head's; -1 = off: each Dense's weight gradient right after
-        its dgrad).  Needs the single-stream backward (no side stream)."""
-        self.wg_group = int(layers) if self.side.stream is None else -1
+        its dgrad)."""
+        self.wg_group = int(layers)
         return self.wg_group
 
     @property
@@ -260,6 +207,54 @@ class GPTStage:
         self._fuse_fwd, self._fuse_bwd = bool(fwd), bool(bwd)
         return True
 
+    def enable_sequence_parallel(self, batch: int) -> bool:
+        """Megatron-style sequence parallelism over the TP group (``TrainConfig.tp_sequence_parallel``):
+        each rank holds ``batch / tp`` whole sequences of the residual stream.  Forward per block: LN1 on
+        the own rows → all-gather → qkv / attention / out_proj (full rows, local heads) → reduce-scatter
+        (+ residual + bias) → LN2 → all-gather → fc1 / fc2 → reduce-scatter; the backward mirrors it.
+        Same xGMI bytes as the four all-reduces (an all-reduce IS a reduce-scatter + an all-gather), while
+        the LayerNorms, the residual adds and the embedding run on 1/tp of the rows.  Needs tp > 1,
+        ``batch % tp == 0`` and a single pipeline stage."""
+        tp = self.tp.size
+        if tp == 1 or batch % tp or not (self.layout.has_embed and self.layout.has_head):
+            return False
+        self.sp = True
+        dev = self.flat.grads.device
+        for key, names in self._sp_groups().items():
+            self._sp_idx[(key,)] = self._sp_index(names, dev)
+        return True
+
+    def _sp_groups(self) -> Dict:
+        """Per layer (and "head"): the grads that are per-rank partial sums under sequence parallelism --
+        the LayerNorm params and the row-parallel biases (out_proj, fc2), replicated over TP but produced
+        from the own rows only."""
+        out = {l: [f"h.{l}.{n}" for n in ("ln1.g", "ln1.b", "ln2.g", "ln2.b", "out.b", "fc2.b")]
+               for l in self.layout.layers}
+        out["head"] = ["lnf.g", "lnf.b"]
+        return out
+
+    def _sp_index(self, names, dev) -> torch.Tensor:
+        sl = self.flat.slots
+        return torch.cat([torch.arange(sl[n].offset, sl[n].offset + sl[n].numel, dtype=torch.int64)
+                          for n in names]).to(dev)
+
+    def _sp_sum(self, keys):
+        """Sum the partial grads of layers / "head" ``keys`` over the TP group: one gather, one all-reduce
+        (in-graph on the P2P path), one scatter back."""
+        if not self.sp or not keys:
+            return
+        k = tuple(keys)
+        idx = self._sp_idx.get(k)
+        if idx is None:
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"sequence parallel: grad index of group {k} first built during graph capture")
+            idx = torch.cat([self._sp_idx[(kk,)] for kk in k])
+            self._sp_idx[k] = idx
+        g = self.flat.grads
+        buf = g.index_select(0, idx)
+        self.tp.all_reduce_(buf)
+        g.index_copy_(0, idx, buf)
+
     def _ln_site(self, l: int, k: int, backward: bool) -> int:
         """Execution-order index of a fused LayerNorm call: forward k = 0 (out_proj → ln2) / 1 (fc2 →
         the next ln1 or lnf) of layer l; backward k = 0 (ln2) / 1 (ln1), layers in reverse."""
@@ -275,7 +270,12 @@ class GPTStage:
         ``keys``: the backward's sort keys, already computed on the host (``E.embed_sort_keys_host``);
         otherwise (``want_keys``) they are sorted on the device."""
         f = self.flat
-        h = E.embed_fwd(ids, f.p("wte"), f.p("wpe"), self.cfg.dropout, self.seed, step, row0)
+        if self.sp:  # this rank's sequences only (the backward gathers the output grads of all of them)
+            bl = ids.shape[0] // self.tp.size
+            r0 = self.tp.rank * bl
+            h = E.embed_fwd(ids[r0:r0 + bl], f.p("wte"), f.p("wpe"), self.cfg.dropout, self.seed, step, row0 + r0)
+        else:
+            h = E.embed_fwd(ids, f.p("wte"), f.p("wpe"), self.cfg.dropout, self.seed, step, row0)
         if keys is not None:
             ctx["embed"] = (ids, row0, (keys, None))
         else:
@@ -283,18 +283,13 @@ class GPTStage:
         return h
 
     def embed_keys(self, ids: torch.Tensor):
-        """Sort keys for the deterministic embedding backward, computed on the side stream (they
-        depend only on the ids) so the sort is off the critical path."""
+        """Sort keys for the deterministic embedding backward (they depend only on the ids); the engine
+        normally builds them on the host instead (``E.embed_sort_keys_host``)."""
         if not ids.is_cuda or ids.numel() > E.SORT_MAX:
             return None  # CPU path / chunked backward sorts per chunk
-        # allocated on the main stream (its consumer); the side stream only writes it
         keys = torch.empty(ids.numel(), dtype=torch.int32, device=ids.device)
-        self.side.run(lambda: E.embed_sort_keys(ids, self.flat.p("wte").shape[0], out=keys), ids)
-        ev = None
-        if self.side.stream is not None:
-            ev = torch.cuda.Event()
-            ev.record(self.side.stream)
-        return keys, ev
+        E.embed_sort_keys(ids, self.flat.p("wte").shape[0], out=keys)
+        return keys, None
 
     def embed_backward(self, ctx: Dict, dh: torch.Tensor, step: torch.Tensor, beta: float, gathered=None):
         """``gathered`` = (ids, row0, keys) of a DP-gathered batch whose ``dh`` rows were all-gathered
@@ -303,9 +298,9 @@ class GPTStage:
         if gathered is not None:
             ids, row0, keys = gathered
         if keys is not None:
-            keys, ev = keys
-            if ev is not None:  # keys were produced on the side stream
-                torch.cuda.current_stream().wait_event(ev)
+            keys, _ = keys
+        if self.sp and gathered is None:
+            dh = self.tp.all_gather_rows(dh)  # every rank builds the identical wte / wpe grads
         f = self.flat
         E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta, keys=keys)
 
@@ -321,6 +316,8 @@ class GPTStage:
         return torch.bfloat16 if _FWD_BF16 and self.act_dtype == torch.bfloat16 else torch.float32
 
     def block_forward(self, l: int, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
+        if self.sp:
+            return self._block_forward_sp(l, x, batch, ctx)
         self._await_params(l)
         f, p = self.flat, f"h.{l}."
         tp = self.tp
@@ -373,17 +370,18 @@ class GPTStage:
         """dx3 fp32 (and its compute-dtype copy) → (dx, dx_c) wrt the block input.  ``dx_hook(dx)``
         (optional) is called as soon as dx is final, before the layer's remaining weight-gradient
         work (the DP embedding gather starts there, under that work)."""
+        if self.sp:
+            return self._block_backward_sp(l, ctx, dx3, dx3_c, beta, dx_hook)
         f, p = self.flat, f"h.{l}."
-        tp = self.tp
         x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch = ctx.pop(l)
         T = x.shape[0] // batch
-        side, red = self.side, self.red
+        red = self.red
         # fc2.b's gradient = Σ_rows dx3 was already emitted by the LayerNorm backward that produced
         # dx3 (lnf or the next block's ln1) unless dx3 arrived from another pipeline stage
         fc2b_fused = l in self._bias_fused
         self._bias_fused.discard(l)
         self._beta = beta
-        if side.stream is None and self._defer_wg:
+        if self._defer_wg:
             # deferred weight gradients: the dgrad chain alone, (dY, X) pairs queued for the grouped launch
             wt2 = f.wt(p + "fc2.w")
             du = (G.matmul_nt_dgelu(dx3_c, wt2, u) if wt2 is not None
@@ -391,80 +389,132 @@ class GPTStage:
             self._wg(dx3_c, gact, p + "fc2")
             if not fc2b_fused:
                 G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
-        elif side.stream is None:
-            # single stream: each Dense's dgrad and weight gradient share one launch
-            # (G.linear_backward), weight-gradient reductions go to the layer's batched launch
-            # with a transposed fc2 weight the paired dgrad runs NT (+ GELU backward), both operands K-major
+        else:
+            # each Dense's dgrad and weight gradient share one launch (G.linear_backward), weight-gradient
+            # reductions go to the layer's batched launch; with a transposed fc2 weight the paired dgrad
+            # runs NT (+ GELU backward), both operands K-major
             du = G.linear_backward(dx3_c, f.w(p + "fc2.w"), gact, f.g(p + "fc2.w"), beta, red=red, dgelu_u=u,
                                    wt=f.wt(p + "fc2.w"))
-        if side.stream is None:
-            if not fc2b_fused and not self._defer_wg:
+            if not fc2b_fused:
                 G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
-            # paired launches measured per Dense (in-step, us): fc2 44.1 vs 46.8 and qkv 35.6 vs 38.1
-            # separate; fc1 48.7 vs 48.1 and out_proj 22.4 vs 21.7 -> those two stay separate
-            wt1 = f.wt(p + "fc1.w")
-            if self._fuse_bwd and wt1 is not None:
-                # fc1 dgrad with the LN2 backward in its epilogue (+ out_proj.b's gradient), then fc1's
-                # weight gradient
-                dx2, dx2_c = LF.dgrad_ln_bwd(du, wt1, x2, f.p(p + "ln2.g"), mu2, rs2, dx3, f.g(p + "ln2.g"),
-                                             f.g(p + "ln2.b"), beta, dbias=f.g(p + "out.b"), red=red,
-                                             sync=self.ln_sync, site=self._ln_site(l, 0, True))
-                self._wg(du, y2, p + "fc1", bias=True)
-            else:
-                dy2 = self._tp_reduce(self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False))
-                dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
-            wto = f.wt(p + "out.w")
-            if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
-                do = G.linear(dx2_c, wto)
-                self._wg(dx2_c, o, p + "out")
-            elif self._defer_wg:
-                do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
-                self._wg(dx2_c, o, p + "out")
-            else:
-                do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
-                                       out_dtype=self.act_dtype, pair=False)
-            dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
-                              self.heads_local).view(batch * T, -1)
-            wtq = f.wt(p + "qkv.w")
-            if self._fuse_bwd and wtq is not None:
-                bg = self._prev_fc2b(l)
-                out = LF.dgrad_ln_bwd(dqkv, wtq, x, f.p(p + "ln1.g"), mu1, rs1, dx2, f.g(p + "ln1.g"), f.g(p + "ln1.b"),
-                                      beta, dbias=None if bg is None else f.g(bg), red=red, sync=self.ln_sync,
-                                      site=self._ln_site(l, 1, True))
-                if dx_hook is not None:
-                    dx_hook(out[0])
-                self._wg(dqkv, y1, p + "qkv", bias=True)
-                return out
-            dy1 = self._tp_reduce(self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True))
-            out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
-            if dx_hook is not None:
-                dx_hook(out[0])
-            return out
-        # MLP (dgrad chain on the main stream, weight grads on the side stream)
-        if fc2b_fused:
-            side.defer(lambda: G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta, red=red), dx3_c, gact)
+        # paired launches measured per Dense (in-step, us): fc2 44.1 vs 46.8 and qkv 35.6 vs 38.1
+        # separate; fc1 48.7 vs 48.1 and out_proj 22.4 vs 21.7 -> those two stay separate
+        wt1 = f.wt(p + "fc1.w")
+        if self._fuse_bwd and wt1 is not None:
+            # fc1 dgrad with the LN2 backward in its epilogue (+ out_proj.b's gradient), then fc1's
+            # weight gradient
+            dx2, dx2_c = LF.dgrad_ln_bwd(du, wt1, x2, f.p(p + "ln2.g"), mu2, rs2, dx3, f.g(p + "ln2.g"),
+                                         f.g(p + "ln2.b"), beta, dbias=f.g(p + "out.b"), red=red,
+                                         sync=self.ln_sync, site=self._ln_site(l, 0, True))
+            self._wg(du, y2, p + "fc1", bias=True)
         else:
-            side.defer(lambda: (G.wgrad(dx3_c, gact, f.g(p + "fc2.w"), beta, red=red), G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)),
-                     dx3_c, gact, dx3)
-        du = G.matmul_nn_dgelu(dx3_c, f.w(p + "fc2.w"), u)
-        side.flush_one()
-        side.defer(lambda: G.wgrad(du, y2, f.g(p + "fc1.w"), beta, red=red, db=f.g(p + "fc1.b")), du, y2)
-        dy2 = G.matmul_nn(du, f.w(p + "fc1.w"))
-        side.flush_one()
-        tp.all_reduce_(dy2)
-        # LN2 backward also emits out_proj.b's gradient (Σ_rows dx2)
-        dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
-        # attention
-        side.defer(lambda: G.wgrad(dx2_c, o, f.g(p + "out.w"), beta, red=red), dx2_c, o)
-        do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
-        side.flush_one()
+            dy2 = self._tp_reduce(self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False))
+            dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
+        wto = f.wt(p + "out.w")
+        if wto is not None:  # NT dgrad on the transposed weight, then the weight gradient
+            do = G.linear(dx2_c, wto)
+            self._wg(dx2_c, o, p + "out")
+        elif self._defer_wg:
+            do = G.matmul_nn(dx2_c, f.w(p + "out.w"), out_dtype=self.act_dtype)
+            self._wg(dx2_c, o, p + "out")
+        else:
+            do = G.linear_backward(dx2_c, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
+                                   out_dtype=self.act_dtype, pair=False)
         dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
                           self.heads_local).view(batch * T, -1)
-        side.defer(lambda: G.wgrad(dqkv, y1, f.g(p + "qkv.w"), beta, red=red, db=f.g(p + "qkv.b")),
-                 dqkv, y1)
-        dy1 = G.matmul_nn(dqkv, f.w(p + "qkv.w"))
-        side.flush_one()
-        tp.all_reduce_(dy1)
+        wtq = f.wt(p + "qkv.w")
+        if self._fuse_bwd and wtq is not None:
+            bg = self._prev_fc2b(l)
+            out = LF.dgrad_ln_bwd(dqkv, wtq, x, f.p(p + "ln1.g"), mu1, rs1, dx2, f.g(p + "ln1.g"), f.g(p + "ln1.b"),
+                                  beta, dbias=None if bg is None else f.g(bg), red=red, sync=self.ln_sync,
+                                  site=self._ln_site(l, 1, True))
+            if dx_hook is not None:
+                dx_hook(out[0])
+            self._wg(dqkv, y1, p + "qkv", bias=True)
+            return out
+        dy1 = self._tp_reduce(self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True))
+        out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
+        if dx_hook is not None:
+            dx_hook(out[0])
+        return out
+
+    # ------------------------------------------------------------------ sequence-parallel block
+    def _row_parallel_sp(self, a, wname: str, resid, bias):
+        """resid + bias + Σ_tp a·Wᵀ on this rank's rows (reduce-scatter); the partial is bf16 under
+        ``tp_bf16``, else fp32, written by the GEMM straight into the P2P buffer when that path takes it."""
+        w = self.flat.w(wname)
+        rows, cols = a.shape[0], w.shape[0]
+        dt = torch.bfloat16 if self.tp_bf16 else torch.float32
+        dst = self.tp.partial_out_rows(rows, cols, dt, bias) if a.is_cuda else None
+        if dst is not None:
+            G.linear_into(a, w, dst)
+            return self.tp.reduce_scatter_staged(rows, cols, dt, resid=resid, bias=bias, device=a.device)
+        return self.tp.reduce_scatter_rows(G.linear(a, w, None, out_dtype=dt), resid=resid, bias=bias)
+
+    def _tp_rs(self, d):
+        """Reduce-scatter an input-gradient partial (the output of :meth:`_dgrad_wgrad`) to this rank's rows."""
+        if isinstance(d, _Staged):
+            return self.tp.reduce_scatter_staged(d.rows, d.cols, torch.bfloat16, device=d.device)
+        return self.tp.reduce_scatter_rows(d)
+
+    def _block_forward_sp(self, l: int, x: torch.Tensor, batch: int, ctx: Dict) -> torch.Tensor:
+        self._await_params(l)
+        f, p, tp = self.flat, f"h.{l}.", self.tp
+        rows = x.shape[0] * tp.size
+        T = rows // batch
+        y1l, mu1, rs1 = LN.layernorm_fwd(x, f.p(p + "ln1.g"), f.p(p + "ln1.b"), self.eps, self.act_dtype)
+        y1 = tp.all_gather_rows(y1l)
+        qkv = G.linear(y1, f.w(p + "qkv.w"), f.p(p + "qkv.b"))
+        o, lse = A.attn_fwd(qkv.view(batch, T, -1), self.heads_local)
+        o = o.view(rows, -1)
+        x2 = self._row_parallel_sp(o, p + "out.w", resid=x, bias=f.p(p + "out.b"))
+        y2l, mu2, rs2 = LN.layernorm_fwd(x2, f.p(p + "ln2.g"), f.p(p + "ln2.b"), self.eps, self.act_dtype)
+        y2 = tp.all_gather_rows(y2l)
+        u, gact = G.linear_gelu(y2, f.w(p + "fc1.w"), f.p(p + "fc1.b"))
+        x3 = self._row_parallel_sp(gact, p + "fc2.w", resid=x2, bias=f.p(p + "fc2.b"))
+        ctx[l] = (x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch)
+        return x3
+
+    def _block_backward_sp(self, l: int, ctx: Dict, dx3: torch.Tensor, dx3_c: torch.Tensor, beta: float,
+                           dx_hook=None):
+        """dx3 (fp32, own rows) → (dx, dx_c) on the own rows.  The residual gradient is all-gathered in the
+        compute dtype for the GEMMs, their input-gradient partials are reduce-scattered; the LayerNorm and
+        row-parallel-bias grads come out as partials over the own rows (summed by :meth:`_sp_sum`)."""
+        f, p, tp = self.flat, f"h.{l}.", self.tp
+        x, y1, mu1, rs1, qkv, o, lse, x2, y2, mu2, rs2, u, gact, batch = ctx.pop(l)
+        rows = y1.shape[0]
+        T = rows // batch
+        red = self.red
+        fc2b_fused = l in self._bias_fused
+        self._bias_fused.discard(l)
+        self._beta = beta
+        g3 = tp.all_gather_rows(dx3_c)
+        if self._defer_wg:
+            wt2 = f.wt(p + "fc2.w")
+            du = (G.matmul_nt_dgelu(g3, wt2, u) if wt2 is not None
+                  else G.matmul_nn_dgelu(g3, f.w(p + "fc2.w"), u))
+            self._wg(g3, gact, p + "fc2")
+        else:
+            du = G.linear_backward(g3, f.w(p + "fc2.w"), gact, f.g(p + "fc2.w"), beta, red=red, dgelu_u=u,
+                                   wt=f.wt(p + "fc2.w"))
+        if not fc2b_fused:
+            G.colsum(dx3, f.g(p + "fc2.b"), beta, red=red)
+        dy2 = self._tp_rs(self._dgrad_wgrad(du, p + "fc1", y2, beta, red, pair=False))
+        dx2, dx2_c = self._ln_bwd(dy2, x2, p + "ln2", mu2, rs2, dx3, beta, bias_grad=p + "out.b")
+        g2 = tp.all_gather_rows(dx2_c)
+        wto = f.wt(p + "out.w")
+        if wto is not None:
+            do = G.linear(g2, wto)
+            self._wg(g2, o, p + "out")
+        elif self._defer_wg:
+            do = G.matmul_nn(g2, f.w(p + "out.w"), out_dtype=self.act_dtype)
+            self._wg(g2, o, p + "out")
+        else:
+            do = G.linear_backward(g2, f.w(p + "out.w"), o, f.g(p + "out.w"), beta, red=red,
+                                   out_dtype=self.act_dtype, pair=False)
+        dqkv = A.attn_bwd(qkv.view(batch, T, -1), o.view(batch, T, -1), lse, do.view(batch, T, -1),
+                          self.heads_local).view(rows, -1)
+        dy1 = self._tp_rs(self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True))
         out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
         if dx_hook is not None:
             dx_hook(out[0])
@@ -553,6 +603,8 @@ class GPTStage:
         pre = ctx.pop("lnf_pre", None)  # produced by the last layer's fc2 GEMM (fused LayerNorm)
         yf, muf, rsf = pre if pre is not None else LN.layernorm_fwd(x, f.p("lnf.g"), f.p("lnf.b"), self.eps,
                                                                      self.act_dtype)
+        if self.sp:
+            yf = self.tp.all_gather_rows(yf)  # the vocab-parallel lm_head reads every row
         lab = labels.reshape(-1)
         tp1 = self.tp.size == 1
         if _CE_CHUNK > 0 and self.v_local > _CE_CHUNK:
@@ -619,13 +671,20 @@ class GPTStage:
             G.colsum(cp, gb[c0:c0 + vc], beta, red=red)
             self.flush_reductions()  # this chunk's split-K slabs: the reducer arena is reused by the next
             del logits, dl, cp
-        self.tp.all_reduce_(dyf)
+        dyf = self._head_dx(dyf)
         last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None
         out = self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
                            bias_grad=None if last is None else self._prev_fc2b(last))
-        self.side.flush()
         self.flush_reductions()
+        self._sp_sum(["head"])
         return out
+
+    def _head_dx(self, dyf):
+        """The lm_head input gradient summed over the vocab shards: all-reduced, or under sequence
+        parallelism reduce-scattered to the own rows."""
+        if self.sp:
+            return self.tp.reduce_scatter_rows(dyf)
+        return self.tp.all_reduce_(dyf)
 
     def head_backward(self, ctx: Dict, grad_scale: float, beta: float):
         f = self.flat
@@ -646,28 +705,24 @@ class GPTStage:
             # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
             dyf = (G.linear_resid(dlogits, wt, None, None) if wt is not None
                    else G.matmul_nn(dlogits, f.w("lm_head.w")))
-        wg = lambda dl=dlogits, y=yf, cp=colp: (G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red),
-                                                G.colsum(cp, f.g("lm_head.b"), beta, red=red))
-        keep = (dlogits, yf, colp)
-        if self._defer_wg and self.side.stream is None:
-            # the bias gradient from the CE pass's fp32 column partials now; the weight gradient joins
-            # the grouped launch (its 591 tiles at GPT-2 small fill the layers' last round)
-            G.colsum(colp, f.g("lm_head.b"), beta, red=red)
+        # the bias gradient from the CE pass's fp32 column partials
+        G.colsum(colp, f.g("lm_head.b"), beta, red=red)
+        if self._defer_wg:
+            # the weight gradient joins the grouped launch (its 591 tiles at GPT-2 small fill the layers'
+            # last round)
             self.wg_queue.append((dlogits, yf, f.g("lm_head.w"), None))
             wg = None
-        if wg is None:
-            pass
-        elif _LMHEAD_WGRAD_MAIN:
-            wg()
-        else:
-            self.side.defer(wg, *keep)
+        else:  # after the lnf backward (off the input-gradient chain)
+            wg = lambda dl=dlogits, y=yf: G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red)  # noqa: E731
         del logits, dlogits
-        self.tp.all_reduce_(dyf)
+        dyf = self._head_dx(dyf)
         last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None
         out = self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
                            bias_grad=None if last is None else self._prev_fc2b(last))
-        self.side.flush()
+        if wg is not None:
+            wg()
         self.flush_reductions()
+        self._sp_sum(["head"])
         return out
 
     def flush_reductions(self):
@@ -695,12 +750,11 @@ class GPTStage:
         ``keep_wgrads`` (deferred weight gradients only): the input-gradient chain (B) alone -- the weight
         gradients stay queued for :meth:`take_wgrads` (the zero-bubble pipeline's W item)."""
         if keep_wgrads and not self._defer_wg:
-            raise ValueError("keep_wgrads needs deferred weight gradients (wgrad_group >= 0, no side stream)")
+            raise ValueError("keep_wgrads needs deferred weight gradients (wgrad_group >= 0)")
         first = self.layout.layers[0] if len(self.layout.layers) else None
         waiting = []  # layers whose weight gradients are still queued (deferred mode)
         for l in reversed(list(self.layout.layers)):
             dx, dx_c = self.block_backward(l, ctx, dx, dx_c, beta, dx_hook=dx_hook if l == first else None)
-            self.side.flush()
             if self._defer_wg:
                 waiting.append(l)
                 if keep_wgrads:
@@ -710,6 +764,7 @@ class GPTStage:
                 if l == first or (self.wg_group > 0 and len(waiting) >= self.wg_group):
                     self.flush_wgrads(beta)
                     self.flush_reductions()  # the group's grads are final after these launches
+                    self._sp_sum(waiting)
                     if hook is not None:
                         for ll in waiting:
                             hook(ll)
@@ -718,10 +773,9 @@ class GPTStage:
                     self.flush_reductions()  # this layer's LayerNorm / bias partials
                 continue
             self.flush_reductions()  # layer l's grads are final after this launch
+            self._sp_sum([l])
             if hook is not None:
                 hook(l)
-            if not _SIDE_INTERLEAVE:
-                self.side.flush()  # one fork per layer: its wgrads (+ anything the hook queued)
         if self.wg_queue and not keep_wgrads:  # a stage without layers: the lm_head's weight gradient alone
             self.flush_wgrads(beta)
             self.flush_reductions()

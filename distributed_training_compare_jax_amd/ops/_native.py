@@ -116,6 +116,7 @@ def _declare(lib):
         "dtc_gemm_wgrad_split": ([i, i, i, i], i),
         "dtc_gemm_set_n8": ([i], i),
         "dtc_gemm_set_n8_cb": ([i], i),
+        "dtc_gemm_set_r8": ([i], i),
         "dtc_gemm_set_big_cb3": ([i], i),
         "dtc_gemm_set_n8_mink": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
@@ -147,6 +148,8 @@ def _declare(lib):
         "dtc_p2p_allreduce": ([vp, vp, l, vp, i, i, l, vp, vp, i, vp], i),
         "dtc_p2p_allreduce_bf16": ([vp, vp, l, vp, i, i, l, vp, vp, i, vp, vp, i, vp], i),
         "dtc_p2p_barrier_round": ([vp, i, i, vp, vp, vp], i),
+        "dtc_p2p_reduce_scatter": ([vp, i, vp, l, vp, i, i, l, vp, vp, vp, vp, i, vp], i),
+        "dtc_p2p_all_gather": ([vp, vp, l, vp, i, i, l, vp, vp, vp], i),
         "dtc_embed_sort_bits": ([i], i),
         "dtc_embed_sort": ([vp, i, i, vp, vp], i),
         "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),

@@ -130,7 +130,8 @@ class P2PAllReduce:
         the calls per step even so the half of each call site is the same on every graph replay."""
         from ..ops.gemm import RawOut
 
-        if dtype != torch.bfloat16 or numel % 8 or numel * 2 > self.half:
+        esz = 2 if dtype == torch.bfloat16 else (4 if dtype == torch.float32 else 0)
+        if not esz or numel % 8 or numel * esz > self.half:
             return None
         return RawOut(self._own + self._flag_bytes + (self.calls & 1) * self.half, dtype, self.device)
 
@@ -158,6 +159,36 @@ class P2PAllReduce:
                                                self.world, self.half, self.epoch.data_ptr(), self.err.data_ptr(),
                                                int(mode), N.ptr(resid), N.ptr(bias), ncols, N.stream_ptr(out.device)),
                 "dtc_p2p_allreduce_bf16")
+        self.calls += 1
+        return out
+
+    # ---- sequence parallelism: row-sharded residual stream (parallel/tp.py TPComm.*_rows)
+    def supports_rs(self, rows: int, cols: int, dtype) -> bool:
+        esz = 2 if dtype == torch.bfloat16 else (4 if dtype == torch.float32 else 0)
+        loc = rows // self.world * cols
+        return bool(esz) and rows % self.world == 0 and loc % 8 == 0 and rows * cols * esz <= self.half
+
+    def reduce_scatter(self, x, rows: int, cols: int, dtype, out: torch.Tensor, resid=None, bias=None) -> torch.Tensor:
+        """out (fp32 [rows / W, cols], this rank's rows) = resid + bias + Σ_ranks x[own rows]; ``x`` the full
+        [rows, cols] partial (bf16 / fp32) or None when its producer wrote it into :meth:`staged_out`."""
+        n_loc = rows // self.world * cols
+        N.check(N.lib().dtc_p2p_reduce_scatter(N.ptr(x), int(dtype == torch.bfloat16), out.data_ptr(), n_loc,
+                                               self._bases_ptr, self.rank, self.world, self.half,
+                                               self.epoch.data_ptr(), self.err.data_ptr(), N.ptr(resid), N.ptr(bias),
+                                               cols if bias is not None else 0, N.stream_ptr(out.device)),
+                "dtc_p2p_reduce_scatter")
+        self.calls += 1
+        return out
+
+    def supports_ag(self, x: torch.Tensor) -> bool:
+        nb = x.numel() * x.element_size()
+        return x.is_cuda and x.is_contiguous() and nb % 16 == 0 and nb * self.world <= self.half
+
+    def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out [W * rows, ...] (rank-major) = every rank's ``x`` (any dtype, 16-byte multiple)."""
+        N.check(N.lib().dtc_p2p_all_gather(x.data_ptr(), out.data_ptr(), x.numel() * x.element_size(),
+                                           self._bases_ptr, self.rank, self.world, self.half, self.epoch.data_ptr(),
+                                           self.err.data_ptr(), N.stream_ptr(out.device)), "dtc_p2p_all_gather")
         self.calls += 1
         return out
 

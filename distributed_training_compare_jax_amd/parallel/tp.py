@@ -100,3 +100,59 @@ class TPComm:
         g = self.group
         self.program.comm(lambda: dist.all_gather(outs, t, group=g), sig=csig("all_gather", g, t))
         return out
+
+    # ---- sequence parallelism (TrainConfig.tp_sequence_parallel): the residual stream, the LayerNorms and
+    # the embedding output live on rows/size rows per rank; the all-reduce after a row-parallel GEMM becomes
+    # a reduce-scatter and the LayerNorm output feeding a column-parallel GEMM is all-gathered (Megatron-LM
+    # sequence parallelism: the same bytes as the all-reduce, LN / residual work divided by tp)
+    def _rccl(self) -> bool:
+        return dist.get_backend(self.group) == "nccl"
+
+    def reduce_scatter_rows(self, part: torch.Tensor, resid=None, bias=None) -> torch.Tensor:
+        """fp32 [rows/size, cols] = resid + bias + Σ_ranks part[this rank's rows] for a [rows, cols] partial
+        (bf16 or fp32)."""
+        rows, cols = part.shape
+        rl = rows // self.size
+        out = torch.empty(rl, cols, dtype=torch.float32, device=part.device)
+        if self.p2p is not None and part.is_cuda and part.is_contiguous() and \
+                self.p2p.supports_rs(rows, cols, part.dtype) and (bias is None or cols % 8 == 0):
+            return self.p2p.reduce_scatter(part, rows, cols, part.dtype, out, resid, bias)
+        full = part.float() if part.dtype != torch.float32 else part.clone()
+        g = self.group
+        if self._rccl():
+            self.program.comm(lambda: dist.reduce_scatter_tensor(out, full, group=g),
+                              sig=csig("reduce_scatter", g, full))
+        else:  # gloo: no reduce-scatter; all-reduce and keep the own rows (same sum)
+            self.program.comm(lambda: dist.all_reduce(full, group=g), sig=csig("all_reduce", g, full))
+            out.copy_(full[self.rank * rl:(self.rank + 1) * rl])
+        if resid is not None:
+            out.add_(resid)
+        if bias is not None:
+            out.add_(bias)
+        return out
+
+    def partial_out_rows(self, rows: int, cols: int, dtype, bias=None):
+        """Where a row-parallel GEMM writes its [rows, cols] partial for :meth:`reduce_scatter_staged` (the
+        own P2P buffer half), or None."""
+        if self.p2p is None or not self.p2p.supports_rs(rows, cols, dtype) or (bias is not None and cols % 8):
+            return None
+        return self.p2p.staged_out(rows * cols, dtype)
+
+    def reduce_scatter_staged(self, rows: int, cols: int, dtype, resid=None, bias=None, device=None):
+        out = torch.empty(rows // self.size, cols, dtype=torch.float32, device=device or self.p2p.device)
+        return self.p2p.reduce_scatter(None, rows, cols, dtype, out, resid, bias)
+
+    def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """[rows, ...] on every rank → [size * rows, ...] (rank-major)."""
+        out = torch.empty((self.size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        if self.p2p is not None and self.p2p.supports_ag(x):
+            return self.p2p.all_gather(x.contiguous(), out)
+        g = self.group
+        xc = x.contiguous()
+        if self._rccl():
+            self.program.comm(lambda: dist.all_gather_into_tensor(out, xc, group=g), sig=csig("all_gather", g, xc))
+        else:
+            outs = list(out.chunk(self.size, 0))
+            self.program.comm(lambda: dist.all_gather(outs, xc, group=g), sig=csig("all_gather", g, xc))
+        return out
+

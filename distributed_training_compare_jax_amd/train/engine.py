@@ -111,12 +111,19 @@ class Engine:
             self.p2p = P2PAllReduce(m.tp_group, m.tp_idx, tp, self.device, rows * T * model_cfg.d_model * 4)
         self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program, p2p=self.p2p)
         self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
-                              act_dtype=self.act_dtype,
-                              side_stream=on_gpu and os.environ.get("DTC_SIDE_STREAM", "0") == "1")
+                              act_dtype=self.act_dtype)
         if train_cfg.tp_comm_dtype not in ("fp32", "bf16"):
             raise ValueError(f"tp_comm_dtype={train_cfg.tp_comm_dtype!r}: expected 'fp32' or 'bf16'")
         self.stage.tp_bf16 = bool(tp > 1 and train_cfg.tp_comm_dtype == "bf16")
-        self.program.before_comm.append(self.stage.side.join)
+        if train_cfg.tp_sequence_parallel:
+            if tp == 1:
+                if dinfo.rank == 0:
+                    warnings.warn("tp_sequence_parallel ignored: tp == 1")
+            elif pp > 1:
+                raise ValueError("tp_sequence_parallel needs pp == 1 (one stage holds the embedding and the head)")
+            elif not self.stage.enable_sequence_parallel(self.b_local):
+                raise ValueError(f"tp_sequence_parallel: the local batch {self.b_local} must split into whole "
+                                 f"sequences over tp={tp}")
         # deferred grouped weight gradients (models/gpt.py set_wgrad_group): all layers + the lm_head in
         # one launch when no collective waits on per-layer grads (dp == 1), else groups of wgrad_group
         # layers so each group's DP buckets go out under the next group's backward
@@ -143,10 +150,10 @@ class Engine:
         if self.zero and train_cfg.dp_grad_dtype == "bf16" and dinfo.rank == 0:
             warnings.warn("dp_grad_dtype=bf16 ignored under zero_stage=1: ShardedAdamW reduce-scatters the fp32 grads")
         if self.stage.tp_bf16 and self.stage.wg_group < 0 and dinfo.rank == 0:
-            warnings.warn("tp_comm_dtype=bf16 with wgrad_group=-1 (or the backward side stream): the row-parallel "
+            warnings.warn("tp_comm_dtype=bf16 with wgrad_group=-1: the row-parallel "
                           "partials travel as bf16, the input-gradient partials stay fp32")
         self.embed_gather = bool(self.dp_comm and pp == 1 and train_cfg.dp_embed_gather and self.layout.has_embed
-                                 and not self.zero)
+                                 and not self.zero and not self.stage.sp)
         bnd = None
         if pp == 1 and len(self.layout.layers):
             names = list(self.flat.slots)
@@ -167,7 +174,7 @@ class Engine:
             self.opt.tp_comm = self.tp_comm
         if pp == 1 and not self.zero:
             # incremental Σg²: with dp == 1 each layer's grads are final when its backward ends
-            # (norm chunk per layer, reduced on the side stream); with dp > 1 only the locally
+            # (norm chunk per layer, in the layer's batched reduction launch); with dp > 1 only the locally
             # built embedding grads are final before the all-reduces finish
             if not self.dp_comm:
                 bk = self.buckets
@@ -227,16 +234,16 @@ class Engine:
         self.steps_done = 0
         # Deferred optimizer (pp == 1, GPU): the step ends with the global norm and the AdamW of
         # the embedding tables only; the rest of the update runs at the START of the next step
-        # on the side stream, in forward order and in a few layer groups, each group signalling
+        # on a second stream, in forward order and in a few layer groups, each group signalling
         # an event the forward waits on before its first layer.  The HBM-bound AdamW (~2.2 GB of
         # traffic) then overlaps the compute-bound forward instead of idling the MFMAs at the
         # end of the step.  Semantics are unchanged (same norm, same update, before each use);
         # :meth:`flush_optimizer` completes a pending update (checkpoint, end of run, bench).
         self.defer_opt = bool(on_gpu and pp == 1 and not self.zero and train_cfg.defer_optimizer)
         if self.defer_opt:
-            # its own stream (the backward side stream when that is on): the capped-grid AdamW passes
-            # share the CUs with the forward GEMMs instead of queueing ahead of them
-            self.opt_stream = self.stage.side.stream or torch.cuda.Stream(self.device)
+            # its own stream: the capped-grid AdamW passes share the CUs with the forward GEMMs instead of
+            # queueing ahead of them
+            self.opt_stream = torch.cuda.Stream(self.device)
             self._defer_blocks = int(os.environ.get("DTC_DEFER_BLOCKS", "256"))
             self.program.before_comm.append(self._join_opt)
             # device-side "an update is pending" switch: the graph always contains the deferred
@@ -266,7 +273,7 @@ class Engine:
         # dp == 1 too: under DP the bucket all-reduces (RCCL kernels on other CUs) run during the
         # backward, and the in-launch row-statistics exchange needs all of its blocks co-resident.
         if (lnf and on_gpu and self.act_dtype == torch.bfloat16 and tp == 1 and pp == 1 and not self.dp_comm
-                and not self.defer_opt and self.stage.side.stream is None):
+                and not self.defer_opt):
             has_wt = len(self.layout.layers) > 0 and self.flat.wt(f"h.{self.layout.layers[0]}.fc1.w") is not None
             self.stage.enable_ln_fusion(self.b_local * T, self.opt.step_t, fwd=bool(lnf & 1),
                                         bwd=bool(lnf & 2) and has_wt)
@@ -314,8 +321,6 @@ class Engine:
 
         # split-K slabs: the lm_head dgrad (fused CE, split 8 at the reference size) needs 67 MB
         reserve_workspace(self.device, 96 << 20)
-        if self.stage.side.stream is not None:
-            reserve_workspace(self.device, 96 << 20, role="side")
 
     @property
     def tokens_per_step(self) -> int:
@@ -403,7 +408,7 @@ class Engine:
                 from ..ops import _native as N
 
                 L = N.lib()
-                self.prev = (L.dtc_gemm_set_n8(0), L.dtc_gemm_set_wgrad256(0))
+                self.prev = (L.dtc_gemm_set_n8(0), L.dtc_gemm_set_wgrad256(0), L.dtc_gemm_set_r8(0))
 
         def __exit__(self, *a):
             if self.on:
@@ -412,6 +417,7 @@ class Engine:
                 L = N.lib()
                 L.dtc_gemm_set_n8(self.prev[0])
                 L.dtc_gemm_set_wgrad256(self.prev[1])
+                L.dtc_gemm_set_r8(self.prev[2])
 
     def _step_fn_dp_tp(self):
         st, T, b = self.stage, self.T, self.b_local
@@ -439,7 +445,7 @@ class Engine:
         st, T, b = self.stage, self.T, self.b_local
         dx, dx_c = st.head_backward(ctx, grad_scale=1.0 / (b * T * dp), beta=0.0)
         bk, opt = self.buckets, self.opt
-        side = st.red if st.red is not None else st.side.defer  # where grad-norm chunks are queued
+        side = st.red  # grad-norm chunks: into the reducer's batched launches (None: computed right away)
         # deferred weight gradients: the head's grads are final only after the first grouped launch, so
         # what would follow the head backward runs at the first layer hook (which fires after it)
         head_later = [st._defer_wg]
@@ -453,31 +459,22 @@ class Engine:
                     head_later[0] = False
                 opt.ready_upto(bk.layer_end_offset(l), side)
         else:
-            # Single stream: layer l's grads are final once its reduction launch is queued (before
-            # the hook), so its bucket goes out right away; the head's bucket right after the head
-            # backward.  With the backward side stream a bucket's all-reduce cuts the graph, which
-            # joins that stream, so buckets go out with a one-layer lag (the join then finds that
-            # layer's weight-gradient GEMMs already done instead of blocking the dgrad chain).  The
-            # first layer's bucket waits for the embedding gather (that collective feeds compute;
-            # the bucket only the optimizer).
-            layers = list(self.layout.layers)
-            first = layers[0]
-            lag = st.side.stream is not None
-            if not lag and not self.zero and not head_later[0]:  # (ZeRO-1: ShardedAdamW.step reduce-scatters)
+            # layer l's grads are final once its reduction launch is queued (before the hook), so its
+            # bucket goes out right away; the head's bucket right after the head backward.  The first
+            # layer's bucket waits for the embedding gather (that collective feeds compute; the bucket
+            # only the optimizer).
+            first = self.layout.layers[0]
+            if not self.zero and not head_later[0]:  # (ZeRO-1: ShardedAdamW.step reduce-scatters)
                 bk.ready_upto(bk.head_end_offset())
 
             def hook(l):
                 if head_later[0]:
                     head_later[0] = False
-                    if not lag and not self.zero:
+                    if not self.zero:
                         bk.ready_upto(bk.head_end_offset())
                 if self.embed_gather and l == first:
                     return
-                if not lag:
-                    bk.ready_upto(bk.layer_end_offset(l))
-                    return
-                nxt = l + 1
-                bk.ready_upto(bk.layer_end_offset(nxt) if nxt in layers else bk.head_end_offset())
+                bk.ready_upto(bk.layer_end_offset(l))
         if self.zero:
             hook = None  # grads are reduce-scattered in one call by ShardedAdamW.step
         dx_hook = None
@@ -494,7 +491,6 @@ class Engine:
             opt.chunk_ready(len(opt.chunks) - 1, side)  # local wte/wpe grads: overlaps the tail bucket
         else:
             st.embed_backward(ctx, dx, step, 0.0)
-        st.side.join()
         if not self.zero:
             bk.ready_all()
             bk.wait_all()
@@ -536,7 +532,6 @@ class Engine:
 
         with self._CommSafeGemms(self.stage.flat.device.type == "cuda"):  # send/recv overlap compute
             run_pipeline(self)
-        self.stage.side.join()
         self.buckets.ready_all()
         # the loss sum overlaps the bucket all-reduces and the optimizer; joined at the very end
         waits = self._loss_allreduce(name="loss_pp", pp=True)

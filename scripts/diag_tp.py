@@ -25,7 +25,6 @@ def fwd_bwd(eng):
     dx, dxc = st.head_backward(ctx, 1 / (4 * T), 0.0)
     dx, dxc = st.stage_backward(ctx, dx, dxc, 0.0)
     st.embed_backward(ctx, dx, eng.opt.step_t, 0.0)
-    st.side.join()
     torch.cuda.synchronize()
     return loss.item(), {n: eng.flat.g(n).cpu().clone() for n in eng.flat.slots}
 

@@ -24,13 +24,13 @@ def _worker(parallel, kw, out_dir):
 
     kw = dict(kw)
     mc = _model_cfg(kw.pop("model", None))
-    tc = TrainConfig(seed=0, parallel=parallel, batch=4, steps=STEPS, log_every=1000, output_dir="/tmp/unused",
+    tc = TrainConfig(seed=0, parallel=parallel, batch=kw.pop("batch", 4), steps=STEPS, log_every=1000, output_dir="/tmp/unused",
                      device="cuda", warmup_steps=2, **kw)
     oc = OptimConfig(lr=3e-3, weight_decay=0.1, grad_clip=1.0)
     d = init_distributed("cuda")
     r = train(tc, mc, oc, d, quiet=True, write_csv=False)
     eng = r["engine"]
-    torch.save({"losses": r["history"], "graphs": r["n_graphs"], "comms": r["n_comms"],
+    torch.save({"losses": r["history"], "graphs": r["n_graphs"], "comms": r["n_comms"], "sp": eng.stage.sp,
                 "params": eng.flat.params.cpu(),
                 "named": {n: eng.flat.p(n).detach().float().cpu().clone() for n in eng.flat.slots},
                 "tp_idx": eng.mesh.tp_idx, "dp_idx": eng.mesh.dp_idx},
@@ -99,9 +99,12 @@ def single(cuda):
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),  # B/W split, W in the bubbles
     ("dp", 4, {"tp": 2, "tp_comm": "p2p"}),
+    ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True}),  # reduce-scatter / all-gather P2P kernels
+    ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True, "tp_comm_dtype": "bf16"}),
 ])
 def test_two_ranks_match_single_gpu(single, init_params, parallel, world, kw):
     res = _run(parallel, world, **kw)
+    assert all(r["sp"] == bool(kw.get("tp_sequence_parallel")) for r in res)
     ref = single[0]["losses"]
     got = res[0]["losses"]
     assert got == pytest.approx(ref, rel=2e-2, abs=2e-2), (parallel, got, ref)
@@ -136,13 +139,15 @@ HEADS12 = {"d_model": 384, "n_heads": 12, "d_ff": 512, "n_layers": 2}
     (4, {"parallel": "dp", "tp": 2, "tp_comm": "p2p"}),  # dp2 x tp2 at the box's default HW queue count
     (2, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16"}),  # bf16 payload P2P kernels
     (4, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16"}),  # ... two-shot at W = 4 (12 heads: 3 each)
+    # sequence parallel at TP=8: one sequence of the residual stream per rank, bf16 partials
+    (8, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": True, "batch": 8}),
 ])
 def test_uneven_heads_and_hybrid_one_gpu(world, kw):
     """TP=8 with 12 heads and dp2 x tp2, 8 / 4 processes on one GPU through the P2P all-reduce kernels,
     against a single-process GPU run of the same model (losses + parameter updates, bf16 tolerances)."""
     kw = dict(kw)
     parallel = kw.pop("parallel")
-    single = _run("dp", 1, model=HEADS12)
+    single = _run("dp", 1, model=HEADS12, batch=kw.get("batch", 4))
     res = _run(parallel, world, model=HEADS12, **kw)
     assert res[0]["losses"] == pytest.approx(single[0]["losses"], rel=2e-2, abs=2e-2)
     from distributed_training_compare_jax_amd.models.params import all_param_specs, init_full
@@ -235,6 +240,22 @@ def _p2p_worker(out_dir):
         torch.cuda.synchronize()
         outs.append(out.cpu().clone())
     res["staged_graph"] = outs
+    # sequence-parallel primitives: reduce-scatter of a [W * 128, 64] partial (bf16 / fp32) + own residual
+    # rows + bias, and the all-gather of 128 own rows
+    g5 = torch.Generator().manual_seed(5)
+    parts = torch.randn(d.world, d.world * 128, 64, generator=g5)
+    resid = torch.randn(d.world * 128, 64, generator=g5)
+    bias = torch.randn(64, generator=g5)
+    for name, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+        out = torch.empty(128, 64, device=d.device)
+        ar.reduce_scatter(parts[d.rank].to(dt).to(d.device), d.world * 128, 64, dt, out,
+                          resid[d.rank * 128:(d.rank + 1) * 128].to(d.device), bias.to(d.device))
+        res[f"rs_{name}"] = out.cpu()
+    xg = torch.randn(d.world, 128, 64, generator=g5).to(torch.bfloat16)
+    og = torch.empty(d.world * 128, 64, dtype=torch.bfloat16, device=d.device)
+    ar.all_gather(xg[d.rank].to(d.device), og)
+    res["ag"] = og.cpu()
+    ar.end_step()
     ar.check()
     torch.save(res, os.path.join(out_dir, f"p2p{d.rank}.pt"))
     ar.close()
@@ -273,6 +294,17 @@ def test_p2p_allreduce_two_ranks_one_gpu():
         for it in range(3):
             e_it = rs + bs + (xb.float() * float(it + 1)).to(torch.bfloat16).float().sum(0)
             assert torch.allclose(r[i]["staged_graph"][it], e_it, atol=1e-4, rtol=1e-5), (i, it)
+    g5 = torch.Generator().manual_seed(5)
+    parts = torch.randn(world, world * 128, 64, generator=g5)
+    resid = torch.randn(world * 128, 64, generator=g5)
+    bias = torch.randn(64, generator=g5)
+    xg = torch.randn(world, 128, 64, generator=g5).to(torch.bfloat16)
+    for i in range(world):
+        rows = slice(i * 128, (i + 1) * 128)
+        for name, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+            exp = resid[rows] + bias + parts.to(dt).float().sum(0)[rows]
+            assert torch.allclose(r[i][f"rs_{name}"], exp, atol=1e-5, rtol=1e-5), (name, i)
+        assert torch.equal(r[i]["ag"], xg.reshape(world * 128, 64)), i
 
 
 @pytest.mark.parametrize("parallel,world,kw", [
@@ -281,6 +313,7 @@ def test_p2p_allreduce_two_ranks_one_gpu():
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "zb"}),
     ("dp", 4, {"tp": 2, "tp_comm": "p2p"}),
+    ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True}),
 ])
 def test_fp32_layouts_match_single_gpu(parallel, world, kw):
     """The same layouts with the exact-fp32 kernels (dtype fp32: f32-input MFMA GEMMs and attention):

@@ -146,3 +146,41 @@ def test_lmhead_dgrad_cb3(cuda):
         _close(out, ref, 2e-3, f"lm_head dgrad (cb3={on})")
         outs.append(out)
     _close(outs[0], outs[1], 1e-5, "cb3_vs_256")
+
+
+# gemm8r (DTC_GEMM8R): 256-row tiles of two widths in one launch.  (M, N, K): qkv forward (256 x 256 tiles on
+# columns 0..2047 + 256 x 64 on the rest), fc1 forward / fc2 NT dgrad (N 3072), out_proj (N 768: narrow
+# tiles only), GPT-2 medium qkv (N 3072, K 1024)
+R8 = [(8192, 2304, 768), (8192, 3072, 768), (8192, 768, 768), (4096, 3072, 1024)]
+
+
+@pytest.mark.parametrize("M,Nn,K", R8)
+def test_r8_epilogues(cuda, M, Nn, K):
+    """Every epilogue gemm8r takes (bf16 + bias, GELU pair, NT dGELU, fp32 + bias with mask bit 2) against
+    fp32 torch and against the same call with the plan off."""
+    L = N.lib()
+    x, w = _r(M, K, seed=31), _r(Nn, K, scale=0.05, seed=32)
+    b = _r(Nn, seed=33, dtype=torch.float32)
+    ref = x.float() @ w.float().t() + b
+    dy, u = _r(M, K, seed=34), _r(M, Nn, seed=35)
+    # NT dGELU: dU[M, Nn] = (dy[M, K] . w^T) * u, w [Nn, K] the transposed weight operand
+    dref = (dy.float() @ w.float().t()) * u.float()
+    outs = {}
+    for mask in (3, 0):
+        old = L.dtc_gemm_set_r8(mask)
+        try:
+            y = G.linear(x, w, b)
+            gg, g = G.linear_gelu(x, w, b)
+            yf = G.linear(x, w, b, out_dtype=torch.float32)
+            dg = G.matmul_nt_dgelu(dy, w, u)
+            torch.cuda.synchronize()
+        finally:
+            L.dtc_gemm_set_r8(old)
+        _close(y, ref, 1e-2, f"store_bf16 r8={mask}")
+        _close(gg, G.gelu_tanh_grad(ref), 1e-2, f"gelu_grad r8={mask}")
+        _close(g, G.gelu_tanh(ref), 1e-2, f"gelu r8={mask}")
+        _close(yf, ref, 2e-3, f"store_f32 r8={mask}")
+        _close(dg, dref, 1e-2, f"nt_dgelu r8={mask}")
+        outs[mask] = (y, g, yf, dg)
+    for a, c, name in zip(outs[3], outs[0], ("store_bf16", "gelu", "store_f32", "nt_dgelu")):
+        _close(a, c, 1e-2, f"r8_vs_default {name}")

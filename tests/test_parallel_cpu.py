@@ -18,9 +18,9 @@ from distributed_training_compare_jax_amd.parallel.dist import spawn
 STEPS = 4
 
 
-def _cfgs(parallel, model=None, eps=1e-8, **kw):
+def _cfgs(parallel, model=None, eps=1e-8, batch=4, **kw):
     mc = model_config_from_preset("tiny", vocab_size=1000, **dict({"n_layers": 4}, **(model or {})))
-    tc = TrainConfig(seed=0, parallel=parallel, batch=4, steps=STEPS, log_every=1000, output_dir="/tmp/unused",
+    tc = TrainConfig(seed=0, parallel=parallel, batch=batch, steps=STEPS, log_every=1000, output_dir="/tmp/unused",
                      device="cpu", warmup_steps=0, **kw)
     oc = OptimConfig(lr=3e-3, weight_decay=0.1, grad_clip=1.0, eps=eps)
     return mc, tc, oc
@@ -38,7 +38,8 @@ def _worker(parallel, kw, out_dir):
     eng = r["engine"]
     params = {n: eng.flat.p(n).clone() for n in eng.flat.slots}
     torch.save({"losses": r["history"], "params": params, "mesh": (eng.mesh.dp, eng.mesh.tp, eng.mesh.pp),
-                "tp_idx": eng.mesh.tp_idx, "dp_idx": eng.mesh.dp_idx, "pp_idx": eng.mesh.pp_idx},
+                "tp_idx": eng.mesh.tp_idx, "dp_idx": eng.mesh.dp_idx, "pp_idx": eng.mesh.pp_idx,
+                "sp": eng.stage.sp},
                os.path.join(out_dir, f"rank{d.rank}.pt"))
     destroy()
 
@@ -88,9 +89,13 @@ def single():
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "gpipe"}),
     ("pp", 2, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),
+    ("tp", 2, {"tp_sequence_parallel": True}),
+    ("dp", 4, {"tp": 2, "tp_sequence_parallel": True}),
+    ("tp", 2, {"tp_sequence_parallel": True, "wgrad_group": -1}),
 ])
 def test_layout_matches_single_process(single, parallel, world, kw):
     res = _run(parallel, world, **kw)
+    assert all(r["sp"] == bool(kw.get("tp_sequence_parallel")) for r in res)
     ref_losses = single[0]["losses"]
     assert res[0]["losses"] == pytest.approx(ref_losses, rel=1e-4, abs=1e-4)
     full = _full_params(res)
@@ -129,6 +134,7 @@ HEADS12 = {"d_model": 96, "n_heads": 12, "d_ff": 256, "n_layers": 2}
 @pytest.mark.parametrize("parallel,world,kw", [
     ("tp", 8, {}),
     ("dp", 8, {"tp": 4}),  # dp2 x tp4: 3 heads per rank
+    ("tp", 8, {"tp_sequence_parallel": True, "batch": 8}),  # one sequence of the residual stream per rank
 ])
 def test_uneven_heads_match_single_process(parallel, world, kw):
     """BASELINE.json config 3 (GPT-2 small at TP=8) needs 12 heads on 8 ranks: losses and the reassembled
@@ -136,8 +142,9 @@ def test_uneven_heads_match_single_process(parallel, world, kw):
     the update linear in near-zero gradients, so fp32 reduction-order noise is not amplified to +-lr
     and the params can be compared at fp32 rounding level (measured max |diff| ~1.3e-7)."""
     kw = dict(kw, model=HEADS12, eps=1e-4)
-    single = _run("dp", 1, model=HEADS12, eps=1e-4)
+    single = _run("dp", 1, model=HEADS12, eps=1e-4, batch=kw.get("batch", 4))
     res = _run(parallel, world, **kw)
+    assert all(r["sp"] == bool(kw.get("tp_sequence_parallel")) for r in res)
     assert res[0]["losses"] == pytest.approx(single[0]["losses"], rel=1e-5, abs=1e-5)
     full = _full_params(res, model=HEADS12)
     ref = single[0]["params"]
