@@ -2875,10 +2875,11 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
 }
 
 // ---- gemm8r plans (layer GEMMs on 256-row tiles of two widths, one launch) ---------------------------
-// DTC_GEMM8R: 1 = use the plan for NT problems (forwards, dgrads on transposed weights) with a bf16 staged
-// epilogue (plain + bias, GELU pair, dGELU) whose 256^2 grid is not whole rounds; 2 = also fp32 outputs;
-// 0 = off.
-static int g_r8_mask = [] { const char* v = getenv("DTC_GEMM8R"); return v ? atoi(v) : 0; }();
+// DTC_GEMM8R: 1 (default) = use the plan for NT problems (forwards, dgrads on transposed weights) with a bf16
+// staged epilogue (plain + bias, GELU pair, dGELU) whose 256^2 grid is not whole rounds; 2 = also fp32
+// outputs (measured slower: out_proj f32 21 -> 29 us); 0 = off.  HBM-cold, GPT-2 small (profiles/r5_gemm8r.md):
+// qkv fwd 44.5 -> 41.6 us, fc1 fwd + GELU 67.3 -> 54.9, fc2 NT dgrad + dGELU 73.7 -> 61.3; step 10.89 -> 10.74 ms
+static int g_r8_mask = [] { const char* v = getenv("DTC_GEMM8R"); return v ? atoi(v) : 1; }();
 
 struct R8Plan {
   int n_split = -1, cb2 = 0;
