@@ -137,11 +137,13 @@ class TrainConfig:
     pp_split: str = "cost"  # cost | even: PP layer split (parallel/mesh.py split_layers)
     dp_grad_dtype: str = "fp32"  # fp32 | bf16: DP gradient payload (bf16: all-to-all + fp32 shard sums)
     pp_comm_dtype: str = "fp32"  # fp32 | bf16: PP activation / gradient messages
-    tp_comm_dtype: str = "fp32"  # fp32 | bf16: TP row-parallel / input-gradient partials (fp32 sums)
+    # fp32 | bf16 | auto: TP row-parallel / input-gradient partials (fp32 sums either way); auto = bf16 when the
+    # compute dtype is bf16 (5000-step tp2 curve: the same gap to dp1 as fp32, profiles/r5_cross_strategy.md)
+    tp_comm_dtype: str = "auto"
     # Megatron-style sequence parallelism over the TP group (pp == 1, batch % tp == 0): the residual stream,
     # LayerNorms and embedding output on batch/tp sequences per rank; reduce-scatter + all-gather in place of
-    # each TP all-reduce (models/gpt.py enable_sequence_parallel)
-    tp_sequence_parallel: bool = False
+    # each TP all-reduce (models/gpt.py enable_sequence_parallel).  None = auto: on whenever it applies
+    tp_sequence_parallel: Optional[bool] = None
     pp_head_cost: Optional[float] = None  # lm_head + CE in blocks (None: parallel/mesh.py head_cost_blocks)
     warmup_steps: int = 5
     ckpt_every: int = 0

@@ -112,10 +112,17 @@ class Engine:
         self.tp_comm = TPComm(m.tp_group, tp, m.tp_idx, self.program, p2p=self.p2p)
         self.stage = GPTStage(model_cfg, self.flat, self.layout, self.tp_comm, dropout_seed=train_cfg.seed,
                               act_dtype=self.act_dtype)
-        if train_cfg.tp_comm_dtype not in ("fp32", "bf16"):
-            raise ValueError(f"tp_comm_dtype={train_cfg.tp_comm_dtype!r}: expected 'fp32' or 'bf16'")
-        self.stage.tp_bf16 = bool(tp > 1 and train_cfg.tp_comm_dtype == "bf16")
-        if train_cfg.tp_sequence_parallel:
+        tcd = train_cfg.tp_comm_dtype
+        if tcd not in ("fp32", "bf16", "auto"):
+            raise ValueError(f"tp_comm_dtype={tcd!r}: expected 'fp32', 'bf16' or 'auto'")
+        if tcd == "auto":
+            tcd = "bf16" if self.act_dtype == torch.bfloat16 else "fp32"
+        self.tp_comm_dtype = tcd
+        self.stage.tp_bf16 = bool(tp > 1 and tcd == "bf16")
+        sp = train_cfg.tp_sequence_parallel
+        if sp is None:  # auto: wherever it applies
+            sp = tp > 1 and pp == 1 and self.b_local % tp == 0
+        if sp:
             if tp == 1:
                 if dinfo.rank == 0:
                     warnings.warn("tp_sequence_parallel ignored: tp == 1")

@@ -92,19 +92,19 @@ def single(cuda):
     ("dp", 2, {}),
     ("dp", 2, {"dp_embed_gather": False}),
     ("dp", 2, {"zero_stage": 1}),
-    ("tp", 2, {}),
-    ("tp", 2, {"tp_comm": "p2p"}),
+    ("tp", 2, {"tp_sequence_parallel": False, "tp_comm_dtype": "fp32"}),  # the RCCL (here gloo) all-reduce path
+    ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": False}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global"}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),  # B/W split, W in the bubbles
     ("dp", 4, {"tp": 2, "tp_comm": "p2p"}),
-    ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True}),  # reduce-scatter / all-gather P2P kernels
+    ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True, "tp_comm_dtype": "fp32"}),  # RS / AG P2P kernels
     ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True, "tp_comm_dtype": "bf16"}),
 ])
 def test_two_ranks_match_single_gpu(single, init_params, parallel, world, kw):
     res = _run(parallel, world, **kw)
-    assert all(r["sp"] == bool(kw.get("tp_sequence_parallel")) for r in res)
+    assert "tp_sequence_parallel" not in kw or all(r["sp"] == kw["tp_sequence_parallel"] for r in res)
     ref = single[0]["losses"]
     got = res[0]["losses"]
     assert got == pytest.approx(ref, rel=2e-2, abs=2e-2), (parallel, got, ref)
@@ -135,10 +135,10 @@ HEADS12 = {"d_model": 384, "n_heads": 12, "d_ff": 512, "n_layers": 2}
 
 
 @pytest.mark.parametrize("world,kw", [
-    (8, {"parallel": "tp", "tp_comm": "p2p"}),
-    (4, {"parallel": "dp", "tp": 2, "tp_comm": "p2p"}),  # dp2 x tp2 at the box's default HW queue count
-    (2, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16"}),  # bf16 payload P2P kernels
-    (4, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16"}),  # ... two-shot at W = 4 (12 heads: 3 each)
+    (8, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "fp32"}),
+    (4, {"parallel": "dp", "tp": 2, "tp_comm": "p2p"}),  # dp2 x tp2 at the box's default HW queue count (SP auto)
+    (2, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": False}),  # bf16 AR
+    (4, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": False}),  # two-shot, W 4
     # sequence parallel at TP=8: one sequence of the residual stream per rank, bf16 partials
     (8, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": True, "batch": 8}),
 ])
@@ -309,7 +309,7 @@ def test_p2p_allreduce_two_ranks_one_gpu():
 
 @pytest.mark.parametrize("parallel,world,kw", [
     ("dp", 2, {}),
-    ("tp", 2, {"tp_comm": "p2p"}),
+    ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": False}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "zb"}),
     ("dp", 4, {"tp": 2, "tp_comm": "p2p"}),

@@ -80,7 +80,7 @@ def single():
     ("dp", 2, {}),
     ("dp", 2, {"zero_stage": 1}),
     ("dp", 4, {"zero_stage": 1}),
-    ("tp", 2, {}),
+    ("tp", 2, {"tp_sequence_parallel": False}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global"}),
     ("pp", 2, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("dp", 4, {"tp": 2}),
@@ -95,7 +95,7 @@ def single():
 ])
 def test_layout_matches_single_process(single, parallel, world, kw):
     res = _run(parallel, world, **kw)
-    assert all(r["sp"] == bool(kw.get("tp_sequence_parallel")) for r in res)
+    assert "tp_sequence_parallel" not in kw or all(r["sp"] == kw["tp_sequence_parallel"] for r in res)
     ref_losses = single[0]["losses"]
     assert res[0]["losses"] == pytest.approx(ref_losses, rel=1e-4, abs=1e-4)
     full = _full_params(res)
@@ -144,7 +144,7 @@ def test_uneven_heads_match_single_process(parallel, world, kw):
     kw = dict(kw, model=HEADS12, eps=1e-4)
     single = _run("dp", 1, model=HEADS12, eps=1e-4, batch=kw.get("batch", 4))
     res = _run(parallel, world, **kw)
-    assert all(r["sp"] == bool(kw.get("tp_sequence_parallel")) for r in res)
+    assert "tp_sequence_parallel" not in kw or all(r["sp"] == kw["tp_sequence_parallel"] for r in res)
     assert res[0]["losses"] == pytest.approx(single[0]["losses"], rel=1e-5, abs=1e-5)
     full = _full_params(res, model=HEADS12)
     ref = single[0]["params"]
