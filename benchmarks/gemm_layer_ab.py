@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default="")
-    ap.add_argument("--variants", default="", help="comma list of plan variants: n8, n8w3, n8w4, n8k768")
+    ap.add_argument("--variants", default="", help="comma list of plan variants: n8, n8w3, n8w4, n8k768, r8, r8f, r8nn, nor8")
     ap.add_argument("--cold", action="store_true",
                     help="write a 512 MB buffer before every call (operands come from HBM, as in the step)")
     a = ap.parse_args()
@@ -103,6 +103,9 @@ def main():
             u = r(M, k)
             add(f"ntdgrad {tag} [{M}x{k}x{n}] dgelu", fl, lambda dy=dy, wt=wt, u=u: G.matmul_nt_dgelu(dy, wt, u),
                 lambda dy=dy, w=w, u=u: (dy.float() @ w.float()) * u.float(), lambda dy=dy, w=w: dy @ w)
+            # the same on the row-major weight (NN: what the step runs without DTC_DGRAD_NT_FC2)
+            add(f"nndgrad {tag} [{M}x{k}x{n}] dgelu", fl, lambda dy=dy, w=w, u=u: G.matmul_nn_dgelu(dy, w, u),
+                lambda dy=dy, w=w, u=u: (dy.float() @ w.float()) * u.float(), lambda dy=dy, w=w: dy @ w)
         elif tag == "out":
             add(f"ntdgrad {tag} [{M}x{k}x{n}] bf16", fl, lambda dy=dy, wt=wt: G.linear(dy, wt),
                 lambda dy=dy, w=w: dy.float() @ w.float(), lambda dy=dy, w=w: dy @ w)
@@ -120,7 +123,7 @@ def main():
     for v in [x for x in a.variants.split(",") if x]:
         variants[v] = {"n8": (7, 0, 1024, 0), "n8w3": (7, 3, 1024, 0), "n8w4": (7, 4, 1024, 0),
                        "n8k768": (3, 0, 768, 0), "r8": (3, 0, 1024, 1), "r8f": (3, 0, 1024, 3),
-                       "nor8": (3, 0, 1024, 0)}[v]
+                       "r8nn": (3, 0, 1024, 5), "nor8": (3, 0, 1024, 0)}[v]
 
     def use(v):
         L.dtc_gemm_set_n8(v[0])

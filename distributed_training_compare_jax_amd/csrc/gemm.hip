@@ -2877,9 +2877,12 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
 // ---- gemm8r plans (layer GEMMs on 256-row tiles of two widths, one launch) ---------------------------
 // DTC_GEMM8R: 1 (default) = use the plan for NT problems (forwards, dgrads on transposed weights) with a bf16
 // staged epilogue (plain + bias, GELU pair, dGELU) whose 256^2 grid is not whole rounds; 2 = also fp32
-// outputs (measured slower: out_proj f32 21 -> 29 us); 0 = off.  HBM-cold, GPT-2 small (profiles/r5_gemm8r.md):
+// outputs (measured slower: out_proj f32 21 -> 29 us); 4 = also NN problems (dgrads on the row-major weight:
+// the fc2 dgrad + dGELU); 0 = off.  HBM-cold, GPT-2 small (profiles/r5_gemm8r.md):
 // qkv fwd 44.5 -> 41.6 us, fc1 fwd + GELU 67.3 -> 54.9, fc2 NT dgrad + dGELU 73.7 -> 61.3; step 10.89 -> 10.74 ms
-static int g_r8_mask = [] { const char* v = getenv("DTC_GEMM8R"); return v ? atoi(v) : 1; }();
+// NN added (default 5): fc2 dgrad + dGELU on the row-major weight 74.3 -> 62.3 us cold, step 10.84 -> 10.74 ms
+// (profiles/r5_gemm8r.md), level with the NT form on a transposed copy (DTC_DGRAD_NT_FC2=1: 10.76 ms)
+static int g_r8_mask = [] { const char* v = getenv("DTC_GEMM8R"); return v ? atoi(v) : 5; }();
 
 struct R8Plan {
   int n_split = -1, cb2 = 0;
@@ -2887,7 +2890,9 @@ struct R8Plan {
 
 static R8Plan r8_plan(int layout, int M, int N, int K, int epi, bool f32) {
   R8Plan r;
-  if (!g_r8_mask || layout != 0 || M % BIG || N % 64 || K % 64 || K < 256 || K > 4096 || N > 16384) return r;
+  if (!g_r8_mask || !(layout == 0 || (layout == 1 && (g_r8_mask & 4))) || M % BIG || N % 64 || K % 64 || K < 256 ||
+      K > 4096 || N > 16384)
+    return r;
   if (!(epi == EPI_STORE || epi == EPI_GELU || epi == EPI_DGELU)) return r;
   if (f32 && (epi != EPI_STORE || !(g_r8_mask & 2))) return r;
   const int tm = M / BIG, q = N / BIG, cus = cu_count();
@@ -2932,11 +2937,11 @@ int launch_r8_cb(const GemmArgs& a, const R8Plan& pl, hipStream_t st) {
   return 0;
 }
 
-template <int EPI, bool OUTF32>
+template <int EPI, bool OUTF32, bool BKM = true>
 int launch_r8(const GemmArgs& a, const R8Plan& pl, hipStream_t st) {
-  if (pl.cb2 == 4) return launch_r8_cb<true, true, EPI, OUTF32, 4>(a, pl, st);
-  if (pl.cb2 == 2) return launch_r8_cb<true, true, EPI, OUTF32, 2>(a, pl, st);
-  return launch_r8_cb<true, true, EPI, OUTF32, 1>(a, pl, st);
+  if (pl.cb2 == 4) return launch_r8_cb<true, BKM, EPI, OUTF32, 4>(a, pl, st);
+  if (pl.cb2 == 2) return launch_r8_cb<true, BKM, EPI, OUTF32, 2>(a, pl, st);
+  return launch_r8_cb<true, BKM, EPI, OUTF32, 1>(a, pl, st);
 }
 
 // ---- gemm8n_kernel plans (layer GEMMs, 128 x 64*CB tiles) ----------------------------------------
@@ -3363,13 +3368,16 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
-  if (a->layout == 0 && !a->colsum && a->alpha == 1.f && a->beta == 0.f &&
+  if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f &&
       !n8_cb(a->layout, a->M, a->N, a->K, epi)) {
     const R8Plan pl = r8_plan(a->layout, a->M, a->N, a->K, epi, f32);
-    if (pl.cb2) {
+    if (pl.cb2 && a->layout == 0) {
       if (epi == EPI_STORE) return f32 ? launch_r8<EPI_STORE, true>(*a, pl, st) : launch_r8<EPI_STORE, false>(*a, pl, st);
       if (epi == EPI_GELU) return launch_r8<EPI_GELU, false>(*a, pl, st);
       if (epi == EPI_DGELU) return launch_r8<EPI_DGELU, false>(*a, pl, st);
+    } else if (pl.cb2 && !f32) {  // NN (W MN-major): the fc2 dgrad + dGELU, bf16 dgrads
+      if (epi == EPI_DGELU) return launch_r8<EPI_DGELU, false, false>(*a, pl, st);
+      if (epi == EPI_STORE) return launch_r8<EPI_STORE, false, false>(*a, pl, st);
     }
   }
   if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f) {

@@ -165,14 +165,16 @@ def test_r8_epilogues(cuda, M, Nn, K):
     dy, u = _r(M, K, seed=34), _r(M, Nn, seed=35)
     # NT dGELU: dU[M, Nn] = (dy[M, K] . w^T) * u, w [Nn, K] the transposed weight operand
     dref = (dy.float() @ w.float().t()) * u.float()
+    wkn = w.t().contiguous()  # [K, Nn] row-major: the NN dgrad layout (mask bit 4)
     outs = {}
-    for mask in (3, 0):
+    for mask in (7, 0):
         old = L.dtc_gemm_set_r8(mask)
         try:
             y = G.linear(x, w, b)
             gg, g = G.linear_gelu(x, w, b)
             yf = G.linear(x, w, b, out_dtype=torch.float32)
             dg = G.matmul_nt_dgelu(dy, w, u)
+            dn = G.matmul_nn_dgelu(dy, wkn, u)
             torch.cuda.synchronize()
         finally:
             L.dtc_gemm_set_r8(old)
@@ -181,6 +183,7 @@ def test_r8_epilogues(cuda, M, Nn, K):
         _close(g, G.gelu_tanh(ref), 1e-2, f"gelu r8={mask}")
         _close(yf, ref, 2e-3, f"store_f32 r8={mask}")
         _close(dg, dref, 1e-2, f"nt_dgelu r8={mask}")
-        outs[mask] = (y, g, yf, dg)
-    for a, c, name in zip(outs[3], outs[0], ("store_bf16", "gelu", "store_f32", "nt_dgelu")):
+        _close(dn, dref, 1e-2, f"nn_dgelu r8={mask}")
+        outs[mask] = (y, g, yf, dg, dn)
+    for a, c, name in zip(outs[7], outs[0], ("store_bf16", "gelu", "store_f32", "nt_dgelu", "nn_dgelu")):
         _close(a, c, 1e-2, f"r8_vs_default {name}")
