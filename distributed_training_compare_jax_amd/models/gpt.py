@@ -367,7 +367,7 @@ class GPTStage:
         return x3
 
     def block_backward(self, l: int, ctx: Dict, dx3: torch.Tensor, dx3_c: torch.Tensor, beta: float, dx_hook=None):
-        """dx3 fp32 (and its compute-dtype copy) → (dx, dx_c) wrt the block input.  ``dx_hook(dx)``
+        """dx3 fp32 (and its compute-dtype copy) → (dx, dx_c) wrt the block input.  ``dx_hook(dx, dx_c)``
         (optional) is called as soon as dx is final, before the layer's remaining weight-gradient
         work (the DP embedding gather starts there, under that work)."""
         if self.sp:
@@ -429,13 +429,13 @@ class GPTStage:
                                   beta, dbias=None if bg is None else f.g(bg), red=red, sync=self.ln_sync,
                                   site=self._ln_site(l, 1, True))
             if dx_hook is not None:
-                dx_hook(out[0])
+                dx_hook(*out)
             self._wg(dqkv, y1, p + "qkv", bias=True)
             return out
         dy1 = self._tp_reduce(self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True))
         out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
         if dx_hook is not None:
-            dx_hook(out[0])
+            dx_hook(*out)
         return out
 
     # ------------------------------------------------------------------ sequence-parallel block
@@ -517,7 +517,7 @@ class GPTStage:
         dy1 = self._tp_rs(self._dgrad_wgrad(dqkv, p + "qkv", y1, beta, red, pair=True))
         out = self._ln_bwd(dy1, x, p + "ln1", mu1, rs1, dx2, beta, bias_grad=self._prev_fc2b(l))
         if dx_hook is not None:
-            dx_hook(out[0])
+            dx_hook(*out)
         return out
 
     def _row_parallel(self, a, wname: str, resid, bias):
@@ -746,7 +746,7 @@ class GPTStage:
     def stage_backward(self, ctx: Dict, dx: torch.Tensor, dx_c: torch.Tensor, beta: float, hook=None, dx_hook=None,
                        keep_wgrads: bool = False):
         """Backward over this stage's layers (reverse); ``hook(l)`` fires after layer l's grads exist,
-        ``dx_hook(dx)`` as soon as the stage's input gradient is final (inside the first layer).
+        ``dx_hook(dx, dx_c)`` as soon as the stage's input gradient is final (inside the first layer).
         ``keep_wgrads`` (deferred weight gradients only): the input-gradient chain (B) alone -- the weight
         gradients stay queued for :meth:`take_wgrads` (the zero-bubble pipeline's W item)."""
         if keep_wgrads and not self._defer_wg:

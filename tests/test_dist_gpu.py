@@ -92,6 +92,7 @@ def single(cuda):
     ("dp", 2, {}),
     ("dp", 2, {"dp_embed_gather": False}),
     ("dp", 2, {"zero_stage": 1}),
+    ("dp", 2, {"dp_grad_dtype": "bf16"}),  # bf16 bucket payload + bf16 embedding-gradient gather
     ("tp", 2, {"tp_sequence_parallel": False, "tp_comm_dtype": "fp32"}),  # the RCCL (here gloo) all-reduce path
     ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": False}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global"}),
