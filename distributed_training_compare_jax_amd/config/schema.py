@@ -145,6 +145,9 @@ class TrainConfig:
     # each TP all-reduce (models/gpt.py enable_sequence_parallel).  None = auto: on whenever it applies
     tp_sequence_parallel: Optional[bool] = None
     pp_head_cost: Optional[float] = None  # lm_head + CE in blocks (None: parallel/mesh.py head_cost_blocks)
+    # lm_head + CE split by vocab over the last two pipeline stages (1f1b / zb, tp == 1; parallel/pp.py
+    # _head_split).  None = auto: on when the head alone outweighs an even share of the model (pp >= 4)
+    pp_head_split: Optional[bool] = None
     warmup_steps: int = 5
     ckpt_every: int = 0
     resume: bool = False

@@ -21,7 +21,7 @@ on the CPU oracle path); all accumulation fp32; grads fp32.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -101,6 +101,9 @@ class StageLayout:
     layers: range
     has_embed: bool
     has_head: bool
+    # (part, parts): lm_head + CE split by vocab over the last `parts` pipeline stages (pp_head_split);
+    # part 0 also holds the final LayerNorm
+    head_part: Tuple[int, int] = (0, 1)
 
 
 class GPTStage:
@@ -132,8 +135,9 @@ class GPTStage:
         assert D % H == 0
         # whole heads per TP rank, uneven when tp does not divide H (models/params.py head_split)
         self.heads_local = head_split(H, self.tp.size)[self.tp.rank][1]
-        self.v_local = cfg.padded_vocab // self.tp.size
-        self.v_start = self.tp.rank * self.v_local
+        part, parts = layout.head_part
+        self.v_local = cfg.padded_vocab // parts // self.tp.size
+        self.v_start = part * (cfg.padded_vocab // parts) + self.tp.rank * self.v_local
         self.v_valid = max(0, min(self.v_local, cfg.vocab_size - self.v_start))
         self.eps = cfg.layernorm_eps
         # Deferred weight gradients (set_wgrad_group): the dgrad chain runs alone and every (dY, X, dW, db)
@@ -620,6 +624,46 @@ class GPTStage:
         ctx["head"] = (x, yf, muf, rsf, logits, lse, lab)
         return loss
 
+    # ------------------------------------------------------------------ head split over two pipeline stages
+    def head_split_logits(self, x: torch.Tensor, labels: torch.Tensor, ctx: Dict) -> torch.Tensor:
+        """``pp_head_split``: this stage's vocab half of lm_head + CE.  Part 0 normalises its stage output
+        ``x`` (lnf) and sends the result to part 1 (:meth:`head_split_input`); part 1 gets that as ``x``.
+        Computes the half's logits and per-row CE partials; returns them packed ``[M, 3]`` (max, Σexp,
+        label logit) for the exchange with the other half."""
+        self._await_params("head")
+        f = self.flat
+        lab = labels.reshape(-1)
+        if self.layout.head_part[0] == 0:
+            x, yf, muf, rsf = ctx.pop("head_yf")
+        else:
+            yf, muf, rsf = x, None, None
+        logits, rowstat, lab_logit = X.lmhead_logits_partials(yf, f.w("lm_head.w"), f.p("lm_head.b"), lab,
+                                                              self.v_start, self.v_valid, combine=True)
+        stats = torch.cat([rowstat, lab_logit[:, None]], 1).contiguous()
+        ctx["head"] = (x, yf, muf, rsf, logits, None, lab)
+        ctx["head_stats"] = stats
+        return stats
+
+    def head_split_input(self, x: torch.Tensor, ctx: Dict) -> torch.Tensor:
+        """Part 0: the final LayerNorm of the stage output -- the message to part 1 (compute dtype)."""
+        f = self.flat
+        self._await_params("head")
+        yf, muf, rsf = LN.layernorm_fwd(x, f.p("lnf.g"), f.p("lnf.b"), self.eps, self.act_dtype)
+        ctx["head_yf"] = (x, yf, muf, rsf)
+        return yf
+
+    def head_split_finalize(self, ctx: Dict, other: torch.Tensor, loss_scale: float,
+                            loss_out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+        """Combine both halves' row statistics (in part order, so both stages get the identical lse and
+        loss) into the loss and the lse the backward needs."""
+        mine = ctx.pop("head_stats")
+        a, b = (mine, other) if self.layout.head_part[0] == 0 else (other, mine)
+        rowstats = torch.stack([a[:, :2], b[:, :2]]).contiguous()
+        lse, loss = X.ce_finalize(rowstats, (a[:, 2] + b[:, 2]).contiguous(), loss_scale, loss_out, accumulate)
+        x, yf, muf, rsf, logits, _, lab = ctx["head"]
+        ctx["head"] = (x, yf, muf, rsf, logits, lse, lab)
+        return loss
+
     def _chunks(self):
         """(column offset, columns, valid columns) of each lm_head vocab chunk of this rank's shard."""
         out = []
@@ -686,7 +730,10 @@ class GPTStage:
             return self.tp.reduce_scatter_rows(dyf)
         return self.tp.all_reduce_(dyf)
 
-    def head_backward(self, ctx: Dict, grad_scale: float, beta: float):
+    def head_backward(self, ctx: Dict, grad_scale: float, beta: float, extra_dyf: Optional[torch.Tensor] = None):
+        """lm_head + CE backward, then the final LayerNorm's.  ``pp_head_split``: part 1 returns its half's
+        input-gradient partial ``(dyf, None)`` (no LayerNorm: part 0 holds it); part 0 adds the other half's
+        partial ``extra_dyf`` before the LayerNorm backward."""
         f = self.flat
         x, yf, muf, rsf, logits, lse, lab = ctx.pop("head")
         if logits is None:  # vocab-chunked head (DTC_CE_CHUNK)
@@ -715,7 +762,16 @@ class GPTStage:
         else:  # after the lnf backward (off the input-gradient chain)
             wg = lambda dl=dlogits, y=yf: G.wgrad(dl, y, f.g("lm_head.w"), beta, red=red)  # noqa: E731
         del logits, dlogits
-        dyf = self._head_dx(dyf)
+        part, parts = self.layout.head_part
+        if parts > 1:
+            if part == 1:  # the partial goes to part 0's stage
+                if wg is not None:
+                    wg()
+                self.flush_reductions()
+                return dyf, None
+            dyf.add_(extra_dyf)
+        else:
+            dyf = self._head_dx(dyf)
         last = self.layout.layers[-1] + 1 if len(self.layout.layers) else None
         out = self._ln_bwd(dyf, x, "lnf", muf, rsf, None, beta,
                            bias_grad=None if last is None else self._prev_fc2b(last))

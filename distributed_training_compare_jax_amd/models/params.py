@@ -50,6 +50,9 @@ class ParamSpec:
     mirror: bool               # has a bf16 compute copy (GEMM weight / bias / LN)
     valid_rows: int = -1       # for padded lm_head: rows >= valid_rows are zero
     heads: int = 0             # head-sharded (qkv_rows / head_cols): attention heads along the split dim
+    # (part, parts): the lm_head vocab split over the last `parts` PIPELINE stages (pp_head_split), applied
+    # before the TP split: this stage holds rows [part * Vp / parts, (part + 1) * Vp / parts)
+    vpart: Tuple[int, int] = (0, 1)
 
 
 def layer_param_specs(cfg: ModelConfig, l: int) -> List[ParamSpec]:
@@ -72,14 +75,19 @@ def layer_param_specs(cfg: ModelConfig, l: int) -> List[ParamSpec]:
     ]
 
 
-def head_param_specs(cfg: ModelConfig) -> List[ParamSpec]:
+def head_param_specs(cfg: ModelConfig, part: int = 0, parts: int = 1) -> List[ParamSpec]:
+    """lm_head (+ the final LayerNorm on part 0); ``parts`` > 1: this pipeline stage's vocab slice of a head
+    split over the last ``parts`` stages (``pp_head_split``)."""
     D, Vp = cfg.d_model, cfg.padded_vocab
-    return [
-        ParamSpec("lm_head.w", (Vp, D), "dense", D, "rows", -2, True, valid_rows=cfg.vocab_size),
-        ParamSpec("lm_head.b", (Vp,), "zeros", D, "rows", -2, True, valid_rows=cfg.vocab_size),
-        ParamSpec("lnf.g", (D,), "ones", D, "rep", -2, True),
-        ParamSpec("lnf.b", (D,), "zeros", D, "rep", -2, True),
+    vp = (int(part), int(parts))
+    out = [
+        ParamSpec("lm_head.w", (Vp, D), "dense", D, "rows", -2, True, valid_rows=cfg.vocab_size, vpart=vp),
+        ParamSpec("lm_head.b", (Vp,), "zeros", D, "rows", -2, True, valid_rows=cfg.vocab_size, vpart=vp),
     ]
+    if part == 0:
+        out += [ParamSpec("lnf.g", (D,), "ones", D, "rep", -2, True),
+                ParamSpec("lnf.b", (D,), "zeros", D, "rep", -2, True)]
+    return out
 
 
 def embed_param_specs(cfg: ModelConfig) -> List[ParamSpec]:
@@ -97,10 +105,11 @@ def all_param_specs(cfg: ModelConfig) -> List[ParamSpec]:
     return out + embed_param_specs(cfg)
 
 
-def stage_param_specs(cfg: ModelConfig, layers: range, has_embed: bool, has_head: bool) -> List[ParamSpec]:
+def stage_param_specs(cfg: ModelConfig, layers: range, has_embed: bool, has_head: bool,
+                      head_part: Tuple[int, int] = (0, 1)) -> List[ParamSpec]:
     out: List[ParamSpec] = []
     if has_head:
-        out += head_param_specs(cfg)
+        out += head_param_specs(cfg, *head_part)
     for l in reversed(list(layers)):
         out += layer_param_specs(cfg, l)
     if has_embed:
@@ -157,6 +166,9 @@ def _head_range(spec: ParamSpec, width: int, tp_rank: int, tp_size: int) -> Tupl
 
 def local_shape(spec: ParamSpec, tp_size: int, tp_rank: int = 0) -> Tuple[int, ...]:
     s = list(spec.shape)
+    if spec.vpart[1] > 1:
+        assert s[0] % spec.vpart[1] == 0, f"{spec.name}: dim0 {s[0]} not divisible by {spec.vpart[1]} head stages"
+        s[0] //= spec.vpart[1]
     if tp_size == 1 or spec.tp == "rep":
         return tuple(s)
     if spec.tp == "qkv_rows" and spec.heads:
@@ -175,6 +187,8 @@ def local_shape(spec: ParamSpec, tp_size: int, tp_rank: int = 0) -> Tuple[int, .
 
 
 def shard(spec: ParamSpec, full: torch.Tensor, tp_rank: int, tp_size: int) -> torch.Tensor:
+    if spec.vpart[1] > 1:  # this stage's vocab slice first, then the TP split of it
+        full = full.chunk(spec.vpart[1], 0)[spec.vpart[0]].contiguous()
     if tp_size == 1 or spec.tp == "rep":
         return full
     if spec.tp == "rows":

@@ -119,7 +119,7 @@ def head_cost_blocks(cfg, head_speedup: float = 1.7) -> float:
     return 6.0 * D * V / block / head_speedup
 
 
-def split_layers(n_layers: int, pp: int, weights=None):
+def split_layers(n_layers: int, pp: int, weights=None, head_stages: int = 1):
     """Contiguous layer ranges per stage.  Fixes the reference quirk ``layers_per_stage =
     n_layers // N`` (``train/train.py:118``) that silently drops layers when N ∤ L.
 
@@ -127,7 +127,10 @@ def split_layers(n_layers: int, pp: int, weights=None):
     carries lm_head+CE).  ``weights=(first, last)``: extra cost (in blocks) of the first stage
     (embedding) and the last (lm_head + CE, :func:`head_cost_blocks`): the contiguous split that
     minimises the most expensive stage, then the spread (sum of squared stage costs); every stage but
-    the last keeps at least one layer, the last may hold the head alone."""
+    the last keeps at least one layer, the last may hold the head alone.
+
+    ``head_stages=2`` (``pp_head_split``): lm_head + CE split by vocab over the last two stages, each
+    carrying half of ``last``; the last stage holds no layers, the one before may hold the head half alone."""
     if weights is None:
         base, rem = divmod(n_layers, pp)
         out, start = [], 0
@@ -141,7 +144,11 @@ def split_layers(n_layers: int, pp: int, weights=None):
         return split_layers(n_layers, pp)
     extra = [0.0] * pp
     extra[0] += first
-    extra[-1] += last
+    if head_stages == 2 and pp >= 2:
+        extra[-1] += last / 2
+        extra[-2] += last / 2
+    else:
+        extra[-1] += last
     # DP over (stage, layers placed): minimise (max stage cost, sum of squared stage costs); every stage
     # but the last holds >= 1 layer (an empty middle stage would only relay activations)
     INF = (float("inf"), float("inf"))
@@ -149,12 +156,13 @@ def split_layers(n_layers: int, pp: int, weights=None):
     arg = [[0] * (n_layers + 1) for _ in range(pp + 1)]
     best[0][0] = (0.0, 0.0)
     for s_ in range(pp):
-        lo_k = 0 if s_ == pp - 1 else 1
+        lo_k = 0 if s_ == pp - 1 or (head_stages == 2 and s_ == pp - 2) else 1
+        hi_k = 0 if (head_stages == 2 and s_ == pp - 1) else n_layers
         for used in range(n_layers + 1):
             if best[s_][used] == INF:
                 continue
             mx, sq = best[s_][used]
-            for k in range(lo_k, n_layers - used + 1):
+            for k in range(lo_k, min(hi_k, n_layers - used) + 1):
                 c = k + extra[s_]
                 cand = (max(mx, c), sq + c * c)
                 if cand < best[s_ + 1][used + k]:
@@ -173,10 +181,15 @@ def split_layers(n_layers: int, pp: int, weights=None):
     return out
 
 
-def stage_costs(ranges, weights):
-    """Per-stage cost (blocks) of a split under ``weights=(first, last)``."""
+def stage_costs(ranges, weights, head_stages: int = 1):
+    """Per-stage cost (blocks) of a split under ``weights=(first, last)`` (``head_stages=2``: the head
+    halved over the last two stages)."""
     first, last = weights
     c = [float(len(r)) for r in ranges]
     c[0] += first
-    c[-1] += last
+    if head_stages == 2 and len(c) >= 2:
+        c[-1] += last / 2
+        c[-2] += last / 2
+    else:
+        c[-1] += last
     return c

@@ -49,10 +49,13 @@ from .program import psig
 
 # ------------------------------------------------------------------------------ static programs
 # items: ("F", i) / ("B", i) / ("W", i)              compute of microbatch i (W: zb only)
+#        ("H", i) / ("Hf", i)                         head split only: this stage's vocab half of lm_head + CE
+#                                                    (logits + row statistics) / the loss from both halves
 #        ("post", name, peer, sends, recvs)          one (grouped) p2p call with stage s+peer;
-#                                                    sends/recvs: tuples of tags ("f"|"b", i)
+#                                                    sends/recvs: tuples of tags ("f"|"b"|"s", i)
 #        ("wait", names)                              the compute stream waits for these entries
-# tag ("f", i): activation of microbatch i, stage s -> s+1; ("b", i): its gradient, s+1 -> s.
+# tag ("f", i): activation of microbatch i, stage s -> s+1; ("b", i): its gradient, s+1 -> s; ("s", i): the
+# head split's row statistics, exchanged both ways between the last two stages.
 
 
 def _schedule(kind: str, S: int, s: int, M: int) -> List[tuple]:
@@ -75,9 +78,47 @@ def _schedule(kind: str, S: int, s: int, M: int) -> List[tuple]:
     return ops
 
 
-def pp_program(kind: str, S: int, s: int, M: int, costs=None) -> List[tuple]:
+def _head_split(prog: List[tuple], S: int, s: int) -> List[tuple]:
+    """``pp_head_split``: lm_head + CE by vocab halves on the last two stages A = S-2 and B = S-1.  A's F
+    ends with the final LayerNorm, whose output is the f message to B; right after sending it (and after
+    the wait its grouped call carries) A computes its half (H), exchanges the row statistics with B (one
+    grouped send + receive) and finalises the loss (Hf).  B's F is just H, exchange, Hf; B's backward sends
+    its half's input-gradient partial as the usual b message, which A adds before the LayerNorm backward.
+    Both stages post the exchange of microbatch i after the f message of i on their pair queue, so the
+    1F1B pairing and its deadlock freedom carry over (:func:`simulate` checks every S, M)."""
+    def exch(i, peer):
+        return [("H", i), ("post", f"s{i}", peer, (("s", i),), (("s", i),)), ("wait", (f"s{i}",)), ("Hf", i)]
+
+    if s == S - 1:
+        out = []
+        for it in prog:
+            out += exch(it[1], -1) if it[0] == "F" else [it]
+        return out
+    if s != S - 2:
+        return prog
+    out: List[tuple] = []
+    pending = None  # microbatch whose f message was just posted
+    for k, it in enumerate(prog):
+        out.append(it)
+        if it[0] == "post" and any(t[0] == "f" for t in it[3]) and it[2] > 0:
+            pending = [t[1] for t in it[3] if t[0] == "f"][0]
+            nxt = prog[k + 1] if k + 1 < len(prog) else None
+            if not (nxt and nxt[0] == "wait" and it[1] in nxt[1]):
+                out += exch(pending, +1)
+                pending = None
+        elif it[0] == "wait" and pending is not None:
+            out += exch(pending, +1)
+            pending = None
+    return out
+
+
+def pp_program(kind: str, S: int, s: int, M: int, costs=None, head_split: bool = False) -> List[tuple]:
     if kind == "zb":
-        return zb_programs(S, M, costs)[s]
+        return zb_programs(S, M, costs, head_split=head_split)[s]
+    if head_split:
+        if kind != "1f1b" or S < 2:
+            raise ValueError("pp_head_split needs pp >= 2 and the 1f1b or zb schedule")
+        return _head_split(pp_program(kind, S, s, M), S, s)
     first, last = s == 0, s == S - 1
     prog: List[tuple] = []
     sends: List[str] = []
@@ -155,14 +196,20 @@ def pp_program(kind: str, S: int, s: int, M: int, costs=None) -> List[tuple]:
 
 
 # ------------------------------------------------------------------------------ zero bubble (B/W split)
-def stage_item_costs(S: int, stage_cost=None, split=(1.0, 1.0, 1.0)) -> List[Dict[str, float]]:
+def stage_item_costs(S: int, stage_cost=None, split=(1.0, 1.0, 1.0), head_half: float = 0.0) -> List[Dict[str, float]]:
     """Per-stage cost of one microbatch's F, B (input-gradient chain) and W (weight gradients), in any
     unit.  ``stage_cost[s]``: the stage's relative size (``mesh.stage_costs``: its layers + the head's
     block-equivalents on the last stage); ``split``: the F : B : W ratio of a block (a block's backward is
     ~2x its forward, half of it the dgrads, half the weight gradients)."""
     stage_cost = [1.0] * S if stage_cost is None else list(stage_cost)
     tot = float(sum(split))
-    return [{k: c * v / tot for k, v in zip("FBW", split)} for c in stage_cost]
+    out = [dict({k: c * v / tot for k, v in zip("FBW", split)}, H=0.0, Hf=0.0) for c in stage_cost]
+    if head_half > 0 and S >= 2:  # pp_head_split: the head half's forward is the H item of the last two stages
+        for c in out[-2:]:
+            h = head_half * split[0] / tot
+            c["H"] = h
+            c["F"] = max(0.0, c["F"] - h)
+    return out
 
 
 def timeline(progs: List[List[tuple]], costs: List[Dict[str, float]], comm: float = 0.0,
@@ -197,7 +244,7 @@ def timeline(progs: List[List[tuple]], costs: List[Dict[str, float]], comm: floa
                         gaps.append((s, pc[s], clock[s], t))
                     clock[s] = max(clock[s], t)
                 else:
-                    c = costs[s][it[0]]
+                    c = costs[s].get(it[0], 0.0)
                     clock[s] += c
                     busy[s] += c
                 pc[s] += 1
@@ -255,7 +302,7 @@ def _place_w(progs, base, s, costs, comm, M):
     return out + tail
 
 
-def zb_programs(S: int, M: int, costs=None, comm: float = 0.0) -> List[List[tuple]]:
+def zb_programs(S: int, M: int, costs=None, comm: float = 0.0, head_split: bool = False) -> List[List[tuple]]:
     """ZB-H1-style programs: 1F1B's items with every B split into B (input gradients) and W (weight
     gradients), W placed to fill idle time.  Start from 1F1B with a split backward (each W right after
     its B: 1F1B's timing); then stage by stage the W's leave the steady state for the idle gaps of the
@@ -264,7 +311,7 @@ def zb_programs(S: int, M: int, costs=None, comm: float = 0.0) -> List[List[tupl
     pass of each are tried and the programs with the shortest replayed makespan are kept.  Memory stays
     1F1B's: a W never moves before its own B, and its B already holds the activations it reads."""
     costs = stage_item_costs(S) if costs is None else costs
-    base = [pp_program("1f1b", S, s, M) for s in range(S)]
+    base = [pp_program("1f1b", S, s, M, head_split=head_split) for s in range(S)]
     inline = [[x for it in b for x in ((it, ("W", it[1])) if it[0] == "B" else (it,))] for b in base]
     if S == 1:
         return inline
@@ -283,21 +330,21 @@ def zb_programs(S: int, M: int, costs=None, comm: float = 0.0) -> List[List[tupl
     return best
 
 
-def estimate(kind: str, S: int, M: int, costs=None, comm: float = 0.0) -> Dict[str, float]:
+def estimate(kind: str, S: int, M: int, costs=None, comm: float = 0.0, head_split: bool = False) -> Dict[str, float]:
     """Predicted step (makespan) and bubble of a schedule under per-item costs (``stage_item_costs``):
     the 1F1B / GPipe B items cost B + W (their backward runs the weight gradients inline)."""
     costs = stage_item_costs(S) if costs is None else costs
     if kind == "zb":
-        progs = zb_programs(S, M, costs, comm)
+        progs = zb_programs(S, M, costs, comm, head_split=head_split)
         c = costs
     else:
-        progs = [pp_program(kind, S, s, M) for s in range(S)]
-        c = [{"F": x["F"], "B": x["B"] + x["W"], "W": 0.0} for x in costs]
+        progs = [pp_program(kind, S, s, M, head_split=head_split) for s in range(S)]
+        c = [dict(x, B=x["B"] + x["W"], W=0.0) for x in costs]
     tl = timeline(progs, c, comm)
     return {"makespan": tl["makespan"], "bubble": tl["bubble"], "ideal": max(M * sum(x.values()) for x in costs)}
 
 
-def simulate(kind: str, S: int, M: int, model: str = "pair") -> Dict[str, int]:
+def simulate(kind: str, S: int, M: int, model: str = "pair", head_split: bool = False) -> Dict[str, int]:
     """Run every stage's :func:`pp_program` under RCCL p2p semantics and return counters.
 
     Model: each stage executes its items in order on one compute stream; a ``post`` enqueues its
@@ -315,7 +362,8 @@ def simulate(kind: str, S: int, M: int, model: str = "pair") -> Dict[str, int]:
     Raises RuntimeError on a deadlock or on a head pair that does not match (wrong message order)."""
     if model not in ("pair", "rank"):
         raise ValueError(model)
-    progs = zb_programs(S, M) if kind == "zb" else [pp_program(kind, S, s, M) for s in range(S)]
+    hk = {"head_split": True} if head_split else {}
+    progs = zb_programs(S, M, **hk) if kind == "zb" else [pp_program(kind, S, s, M, **hk) for s in range(S)]
     pc = [0] * S
     queues: Dict[Tuple[int, int], List[tuple]] = {}
     done = set()
@@ -405,9 +453,15 @@ def run_pipeline(eng) -> None:
     outs: Dict[int, torch.Tensor] = {}  # forward outputs (sent to the next stage)
 
     bf = getattr(eng, "pp_bf16", False)  # bf16 stage messages (pp_comm_dtype): the bf16 images travel
+    hs = bool(getattr(eng, "pp_head_split", False))
+    head_a, head_b = hs and s == S - 2, hs and s == S - 1  # the two halves of a split head
 
     def tensor_of(tag, sending):
         d, i = tag
+        if d == "s":  # head split: packed row statistics of the half (both directions)
+            return ctxs[i]["head_stats"] if sending else eng.recv_s[i]
+        if d == "f" and (head_a if sending else head_b):  # the final LayerNorm output, compute dtype
+            return outs[i] if sending else eng.recv_yf[i]
         if bf:
             if d == "f":
                 return eng.send_x_bf[i] if sending else eng.recv_x_bf[i]
@@ -481,7 +535,7 @@ def run_pipeline(eng) -> None:
 
     kind = eng.tcfg.pp_schedule
     zb = kind == "zb"
-    items = pp_program(kind, S, s, M, costs=eng.pp_item_costs() if zb else None)
+    items = pp_program(kind, S, s, M, costs=eng.pp_item_costs() if zb else None, head_split=hs)
     wq: Dict[int, list] = {}  # zb: microbatch -> its queued weight gradients (run by its W item)
     n_w_done = 0
     sent_tags = {it[1]: it[3] for it in items if it[0] == "post"}  # post name -> tags it sends
@@ -505,12 +559,23 @@ def run_pipeline(eng) -> None:
         labels = eng.labels[i * rows:(i + 1) * rows]
         row0 = eng.row0 + i * rows
         ctx = ctxs[i]
+        if kind == "H":  # head split: this stage's vocab half (A reads its own LayerNorm output)
+            st.head_split_logits(eng.recv_yf[i] if head_b else None, labels, ctx)
+            k += 1
+            continue
+        if kind == "Hf":
+            st.head_split_finalize(ctx, eng.recv_s[i], loss_scale, loss_out=eng.loss if last else None,
+                                   accumulate=(i > 0))
+            k += 1
+            continue
         if kind == "F":
             if not first and bf:
                 cast_bf16_to_f32(eng.recv_x_bf[i], eng.recv_x[i])
             h = st.embed_forward(ids, step, row0, ctx) if first else eng.recv_x[i]
             h = st.stage_forward(h, rows, ctx)
-            if last:
+            if head_a:
+                outs[i] = st.head_split_input(h, ctx)  # the f message to the other half
+            elif last:
                 st.head_forward(h, labels, loss_scale, ctx, loss_out=eng.loss, accumulate=(i > 0))
             else:
                 outs[i] = h
@@ -519,7 +584,10 @@ def run_pipeline(eng) -> None:
         else:
             beta = 0.0 if n_bwd_done == 0 else 1.0
             n_bwd_done += 1
-            if last:
+            if head_b:  # this half's input-gradient partial is the b message
+                dx, _ = st.head_backward(ctx, grad_scale, beta)
+                dx_c = dx
+            elif last:
                 dx, dx_c = st.head_backward(ctx, grad_scale, beta)
             else:
                 dx = eng.recv_dx[i]
@@ -528,8 +596,10 @@ def run_pipeline(eng) -> None:
                     cast_bf16_to_f32(eng.recv_dx_bf[i], dx)
                     if dx_c is not dx:
                         dx_c = eng.recv_dx_bf[i]
-                elif dx_c is not dx:
+                elif dx_c is not dx and not head_a:
                     cast_to_bf16(dx, dx_c)
+                if head_a:  # the other half's partial joins this half's before the final LayerNorm backward
+                    dx, dx_c = st.head_backward(ctx, grad_scale, beta, extra_dyf=dx)
             dx, dx_c = st.stage_backward(ctx, dx, dx_c, beta, keep_wgrads=zb)
             if zb:
                 wq[i] = st.take_wgrads()

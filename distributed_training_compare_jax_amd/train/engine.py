@@ -41,6 +41,20 @@ class Engine:
         self.dinfo = dinfo
         self.device = dinfo.device
         dp, tp, pp = resolve_degrees(train_cfg.parallel, dinfo.world, train_cfg.dp, train_cfg.tp, train_cfg.pp)
+        # lm_head + CE split by vocab over the last two pipeline stages (models/gpt.py head_split_*): auto when
+        # the head alone outweighs an even share of the model (GPT-2 small at pp >= 5: 2.9 blocks vs 14.9 / pp)
+        hsplit = train_cfg.pp_head_split
+        hc_auto = head_cost_blocks(model_cfg) if train_cfg.pp_head_cost is None else float(train_cfg.pp_head_cost)
+        if hsplit is None:
+            hsplit = (pp >= 4 and tp == 1 and train_cfg.pp_schedule in ("1f1b", "zb")
+                      and hc_auto > (model_cfg.n_layers + hc_auto) / pp)
+        if hsplit and (pp < 2 or train_cfg.pp_schedule not in ("1f1b", "zb") or tp > 1):
+            raise ValueError("pp_head_split needs pp >= 2, tp == 1 and the 1f1b or zb schedule")
+        self.pp_head_split = bool(hsplit)
+        if self.pp_head_split and model_cfg.padded_vocab % 128:
+            # each half a multiple of 64 columns
+            model_cfg = replace(model_cfg, vocab_pad_multiple=math.lcm(max(1, int(model_cfg.vocab_pad_multiple)), 128))
+            self.mcfg = model_cfg
         if tp > 1:
             # every TP rank's vocab shard a multiple of 64 columns (the GEMM K-steps of the lm_head dgrad and
             # the 64-wide CE tiles): pad the vocab to a multiple of 64 * tp (GPT-2 at tp = 8: 50688 instead
@@ -81,10 +95,16 @@ class Engine:
         if pp > 1 and train_cfg.pp_split == "cost":
             hc = train_cfg.pp_head_cost
             weights = (0.05, head_cost_blocks(model_cfg) if hc is None else float(hc))
-        layer_ranges = split_layers(model_cfg.n_layers, pp, weights)
+        hstages = 2 if self.pp_head_split else 1
+        if hstages == 2 and weights is None:
+            weights = (0.0, 0.0)  # even split over the stages before the head halves
+        layer_ranges = split_layers(model_cfg.n_layers, pp, weights, head_stages=hstages)
         self.layer_ranges = layer_ranges
-        self.layout = StageLayout(layer_ranges[m.pp_idx], has_embed=m.pp_idx == 0, has_head=m.pp_idx == pp - 1)
-        specs = stage_param_specs(model_cfg, self.layout.layers, self.layout.has_embed, self.layout.has_head)
+        head_stage = m.pp_idx >= pp - hstages
+        self.layout = StageLayout(layer_ranges[m.pp_idx], has_embed=m.pp_idx == 0, has_head=head_stage,
+                                  head_part=(m.pp_idx - (pp - 2), 2) if hstages == 2 and head_stage else (0, 1))
+        specs = stage_param_specs(model_cfg, self.layout.layers, self.layout.has_embed, self.layout.has_head,
+                                  head_part=self.layout.head_part)
         self.flat = FlatParams(specs, m.tp_idx, tp, self.device, compute_dtype=self.act_dtype)
         if self.act_dtype == torch.bfloat16 and os.environ.get("DTC_DGRAD_NT", "1") == "1":
             # Dense / lm_head dgrads as NT GEMMs on a transposed bf16 weight copy (buffers.enable_transposed)
@@ -238,6 +258,12 @@ class Engine:
             if train_cfg.pp_comm_dtype not in ("fp32", "bf16"):
                 raise ValueError(f"pp_comm_dtype={train_cfg.pp_comm_dtype!r}: expected 'fp32' or 'bf16'")
             self.pp_bf16 = train_cfg.pp_comm_dtype == "bf16"
+            if self.pp_head_split and m.pp_idx >= pp - 2:
+                # the final LayerNorm output (A -> B, compute dtype) and the halves' packed row statistics
+                self.recv_yf = [torch.zeros(self.mb_rows * T, D, dtype=self.act_dtype, device=self.device)
+                                for _ in range(self.n_micro)]
+                self.recv_s = [torch.zeros(self.mb_rows * T, 3, dtype=torch.float32, device=self.device)
+                               for _ in range(self.n_micro)]
             if self.pp_bf16:
                 mk = lambda: [torch.zeros(self.mb_rows * T, D, dtype=torch.bfloat16, device=self.device)
                               for _ in range(self.n_micro)]
@@ -325,7 +351,9 @@ class Engine:
 
         hc = self.tcfg.pp_head_cost
         w = (0.05, head_cost_blocks(self.mcfg) if hc is None else float(hc))
-        return stage_item_costs(self.mesh.pp, stage_costs(self.layer_ranges, w))
+        hs = 2 if self.pp_head_split else 1
+        return stage_item_costs(self.mesh.pp, stage_costs(self.layer_ranges, w, head_stages=hs),
+                                head_half=w[1] / 2 if hs == 2 else 0.0)
 
     def _reserve_workspaces(self):
         from ..ops.gemm import reserve_workspace

@@ -35,7 +35,8 @@ def save(eng, output_dir: str, step: int):
     m = eng.mesh
     torch.save({"params": f.params.cpu(), "exp_avg": f.exp_avg.cpu(), "exp_avg_sq": f.exp_avg_sq.cpu(),
                 "step_t": eng.opt.step_t.cpu(), "step": step}, os.path.join(d, f"rank{m.rank}.pt"))
-    slots = {n: dict(offset=s.offset, shape=list(s.shape), tp=s.spec.tp, full=list(s.spec.shape))
+    slots = {n: dict(offset=s.offset, shape=list(s.shape), tp=s.spec.tp, full=list(s.spec.shape),
+                     vpart=list(s.spec.vpart))
              for n, s in f.slots.items()}
     lr = getattr(eng, "layout", None)
     meta = dict(step=step, dp=m.dp, tp=m.tp, pp=m.pp, rank=m.rank, dp_idx=m.dp_idx, tp_idx=m.tp_idx,
@@ -196,7 +197,7 @@ def consolidate(output_dir: str, step: int, vocab_size: int = None) -> Dict[str,
 
     d = _dir(output_dir, step)
     metas = [json.load(open(os.path.join(d, x))) for x in sorted(os.listdir(d)) if x.startswith("meta_rank")]
-    pieces: Dict[str, Dict[int, torch.Tensor]] = {}
+    pieces: Dict[str, Dict[tuple, torch.Tensor]] = {}
     tp_rule: Dict[str, str] = {}
     full_shape: Dict[str, tuple] = {}
     for meta in metas:
@@ -208,7 +209,8 @@ def consolidate(output_dir: str, step: int, vocab_size: int = None) -> Dict[str,
             for x in s["shape"]:
                 numel *= x
             t = st["params"][s["offset"]: s["offset"] + numel].view(s["shape"]).clone()
-            pieces.setdefault(n, {})[meta["tp_idx"]] = t
+            vp = tuple(s.get("vpart", (0, 1)))  # lm_head vocab slice of a head split over PP stages
+            pieces.setdefault(n, {})[(vp[0], meta["tp_idx"])] = t
             tp_rule[n] = s["tp"]
             full_shape[n] = tuple(s["full"])
     if vocab_size is None:
@@ -216,7 +218,9 @@ def consolidate(output_dir: str, step: int, vocab_size: int = None) -> Dict[str,
     out = {}
     for n, parts in pieces.items():
         spec = ParamSpec(n, full_shape[n], "zeros", 1, tp_rule[n], 0, False)
-        t = unshard(spec, [parts[k] for k in sorted(parts)])
+        vparts = sorted({k[0] for k in parts})
+        t = torch.cat([unshard(spec, [parts[k] for k in sorted(parts) if k[0] == v]) for v in vparts], 0) \
+            if len(vparts) > 1 else unshard(spec, [parts[k] for k in sorted(parts)])
         if vocab_size is not None and n in _VOCAB_ROWS and t.shape[0] > vocab_size:
             t = t[:vocab_size].clone()
         out[n] = t

@@ -29,19 +29,24 @@ def test_resume_reproduces_uninterrupted_run(tmp_path):
     assert part1 + part2 == pytest.approx(full, rel=1e-6, abs=1e-6)
 
 
-def _tp_worker(out):
+def _tp_worker(out, parallel="tp", kw=None):
     from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
 
     d = init_distributed("cpu")
-    train(TrainConfig(seed=0, parallel="tp", batch=4, steps=2, log_every=1000, output_dir=out, device="cpu",
-                      warmup_steps=0, ckpt_every=2), MC, OC, d, quiet=True)
+    train(TrainConfig(seed=0, parallel=parallel, batch=4, steps=2, log_every=1000, output_dir=out, device="cpu",
+                      warmup_steps=0, ckpt_every=2, **(kw or {})), MC, OC, d, quiet=True)
     destroy()
 
 
 @pytest.mark.slow
-def test_consolidate_tp_checkpoint_equals_single_process(tmp_path):
+@pytest.mark.parametrize("parallel,kw", [
+    ("tp", {}),
+    # lm_head vocab-split over the two pipeline stages: consolidate joins the halves
+    ("pp", {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b", "pp_head_split": True}),
+])
+def test_consolidate_tp_checkpoint_equals_single_process(tmp_path, parallel, kw):
     out_tp = str(tmp_path / "tp")
-    spawn(_tp_worker, 2, args=(out_tp,))
+    spawn(_tp_worker, 2, args=(out_tp, parallel, kw))
     full = C.consolidate(out_tp, 2)
     # vocab-indexed tensors come back at the canonical vocab whatever the writer's TP padding
     assert full["lm_head.w"].shape[0] == MC.vocab_size and full["lm_head.b"].shape[0] == MC.vocab_size

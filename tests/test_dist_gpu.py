@@ -30,7 +30,7 @@ def _worker(parallel, kw, out_dir):
     d = init_distributed("cuda")
     r = train(tc, mc, oc, d, quiet=True, write_csv=False)
     eng = r["engine"]
-    torch.save({"losses": r["history"], "graphs": r["n_graphs"], "comms": r["n_comms"], "sp": eng.stage.sp,
+    torch.save({"losses": r["history"], "graphs": r["n_graphs"], "comms": r["n_comms"], "sp": eng.stage.sp, "head_part": eng.stage.layout.head_part,
                 "params": eng.flat.params.cpu(),
                 "named": {n: eng.flat.p(n).detach().float().cpu().clone() for n in eng.flat.slots},
                 "tp_idx": eng.mesh.tp_idx, "dp_idx": eng.mesh.dp_idx},
@@ -54,8 +54,14 @@ def _full_params(results, model=None):
         if r["dp_idx"] != 0:
             continue
         for n, t in r["named"].items():
-            pieces.setdefault(n, {})[r["tp_idx"]] = t
-    return {n: unshard(specs[n], [p[k] for k in sorted(p)]) for n, p in pieces.items()}
+            # lm_head of a head split over two pipeline stages: (vocab part, tp shard)
+            part = r.get("head_part", (0, 1))[0] if n.startswith("lm_head") else 0
+            pieces.setdefault(n, {})[(part, r["tp_idx"])] = t
+    out = {}
+    for n, p in pieces.items():
+        parts = sorted({k[0] for k in p})
+        out[n] = torch.cat([unshard(specs[n], [p[k] for k in sorted(p) if k[0] == v]) for v in parts], 0)
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -99,6 +105,8 @@ def single(cuda):
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),  # B/W split, W in the bubbles
+    # lm_head + CE vocab-split over the last two stages (row-statistics exchange, partial dgrad message)
+    ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb", "pp_head_split": True}),
     ("dp", 4, {"tp": 2, "tp_comm": "p2p"}),
     ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True, "tp_comm_dtype": "fp32"}),  # RS / AG P2P kernels
     ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True, "tp_comm_dtype": "bf16"}),
@@ -313,6 +321,7 @@ def test_p2p_allreduce_two_ranks_one_gpu():
     ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": False}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b"}),
     ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "zb"}),
+    ("pp", 2, {"pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b", "pp_head_split": True}),
     ("dp", 4, {"tp": 2, "tp_comm": "p2p"}),
     ("tp", 2, {"tp_comm": "p2p", "tp_sequence_parallel": True}),
 ])

@@ -39,7 +39,7 @@ def _worker(parallel, kw, out_dir):
     params = {n: eng.flat.p(n).clone() for n in eng.flat.slots}
     torch.save({"losses": r["history"], "params": params, "mesh": (eng.mesh.dp, eng.mesh.tp, eng.mesh.pp),
                 "tp_idx": eng.mesh.tp_idx, "dp_idx": eng.mesh.dp_idx, "pp_idx": eng.mesh.pp_idx,
-                "sp": eng.stage.sp},
+                "sp": eng.stage.sp, "head_part": eng.stage.layout.head_part},
                os.path.join(out_dir, f"rank{d.rank}.pt"))
     destroy()
 
@@ -66,8 +66,14 @@ def _full_params(results, model=None):
         if r["dp_idx"] != 0:
             continue
         for n, t in r["params"].items():
-            pieces.setdefault(n, {})[r["tp_idx"]] = t
-    return {n: unshard(specs[n], [p[k] for k in sorted(p)]) for n, p in pieces.items()}
+            # lm_head of a head split over two pipeline stages: (vocab part, tp shard)
+            part = r.get("head_part", (0, 1))[0] if n.startswith("lm_head") else 0
+            pieces.setdefault(n, {})[(part, r["tp_idx"])] = t
+    out = {}
+    for n, p in pieces.items():
+        parts = sorted({k[0] for k in p})
+        out[n] = torch.cat([unshard(specs[n], [p[k] for k in sorted(p) if k[0] == v]) for v in parts], 0)
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -91,6 +97,10 @@ def single():
     ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb"}),
     ("tp", 2, {"tp_sequence_parallel": True}),
     ("dp", 4, {"tp": 2, "tp_sequence_parallel": True}),
+    # lm_head + CE split by vocab over the last two pipeline stages
+    ("pp", 2, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "1f1b", "pp_head_split": True}),
+    ("pp", 4, {"pp_microbatches": 4, "pp_clip": "global", "pp_schedule": "zb", "pp_head_split": True}),
+    ("pp", 4, {"dp": 2, "pp_microbatches": 2, "pp_clip": "global", "pp_schedule": "1f1b", "pp_head_split": True}),
     ("tp", 2, {"tp_sequence_parallel": True, "wgrad_group": -1}),
 ])
 def test_layout_matches_single_process(single, parallel, world, kw):
