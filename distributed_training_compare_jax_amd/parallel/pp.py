@@ -112,9 +112,9 @@ def _head_split(prog: List[tuple], S: int, s: int) -> List[tuple]:
     return out
 
 
-def pp_program(kind: str, S: int, s: int, M: int, costs=None, head_split: bool = False) -> List[tuple]:
+def pp_program(kind: str, S: int, s: int, M: int, costs=None, head_split: bool = False, comm=0.0) -> List[tuple]:
     if kind == "zb":
-        return zb_programs(S, M, costs, head_split=head_split)[s]
+        return zb_programs(S, M, costs, comm, head_split=head_split)[s]
     if head_split:
         if kind != "1f1b" or S < 2:
             raise ValueError("pp_head_split needs pp >= 2 and the 1f1b or zb schedule")
@@ -212,6 +212,15 @@ def stage_item_costs(S: int, stage_cost=None, split=(1.0, 1.0, 1.0), head_half: 
     return out
 
 
+def _comm_cost(comm, tags) -> float:
+    """Transfer time of one (grouped) entry: ``comm`` a number (every message), or a dict by tag kind
+    ({"f": .., "b": .., "s": ..}: activations / gradients / the head split's row statistics) -- the largest
+    message of the group."""
+    if not isinstance(comm, dict):
+        return float(comm)
+    return max((float(comm.get(t[0], 0.0)) for t in tags), default=0.0)
+
+
 def timeline(progs: List[List[tuple]], costs: List[Dict[str, float]], comm: float = 0.0,
              model: str = "rank") -> Dict[str, object]:
     """Timed replay of the stages' programs: every stage runs its items in order on one clock (compute
@@ -261,7 +270,7 @@ def timeline(progs: List[List[tuple]], costs: List[Dict[str, float]], comm: floa
                     raise RuntimeError(f"timeline: message order mismatch at stages {a}/{b} ({na} vs {nb})")
                 qa.pop(0)
                 qb.pop(0)
-                t = max(ta, tb) + comm
+                t = max(ta, tb) + _comm_cost(comm, sa | ra)
                 done[(a, na)] = t
                 done[(b, nb)] = t
                 progressed = True
@@ -535,7 +544,8 @@ def run_pipeline(eng) -> None:
 
     kind = eng.tcfg.pp_schedule
     zb = kind == "zb"
-    items = pp_program(kind, S, s, M, costs=eng.pp_item_costs() if zb else None, head_split=hs)
+    items = pp_program(kind, S, s, M, costs=eng.pp_item_costs() if zb else None, head_split=hs,
+                       comm=eng.pp_comm_costs() if zb else 0.0)
     wq: Dict[int, list] = {}  # zb: microbatch -> its queued weight gradients (run by its W item)
     n_w_done = 0
     sent_tags = {it[1]: it[3] for it in items if it[0] == "post"}  # post name -> tags it sends

@@ -355,6 +355,18 @@ class Engine:
         return stage_item_costs(self.mesh.pp, stage_costs(self.layer_ranges, w, head_stages=hs),
                                 head_half=w[1] / 2 if hs == 2 else 0.0)
 
+    def pp_comm_costs(self):
+        """Transfer time of the stage messages in the units of :meth:`pp_item_costs` (one block's F + B + W
+        for one microbatch), for the zero-bubble placement: bytes over one xGMI link (assumed 50 GB/s per
+        direction) against the block's FLOPs at an assumed 600 TF/s (GPT-2 small: 63 us vs 80 us per
+        one-sequence microbatch -- the messages are NOT negligible).  Deterministic, identical on every rank."""
+        mc, T, rows = self.mcfg, self.T, self.mb_rows
+        D, F = mc.d_model, mc.d_ff
+        block_s = 6.0 * (4 * D * D + 2 * D * F + T * D) * rows * T / 600e12
+        esz = 2 if getattr(self, "pp_bf16", False) else 4
+        fb = rows * T * D * esz / 50e9 / block_s
+        return {"f": fb, "b": fb, "s": 1e-5 / block_s}
+
     def _reserve_workspaces(self):
         from ..ops.gemm import reserve_workspace
 
