@@ -279,6 +279,20 @@ __global__ void flag_wait_kernel(const uint32_t* __restrict__ flags, int k, cons
   __syncthreads();
 }
 
+// CU-occupancy probe (benchmarks/cu_steal_proxy.py): `blocks` workgroups, each requesting (nearly) a whole CU's
+// LDS so no other LDS-using workgroup fits next to it, idle for `ticks` of the 100 MHz wall clock -- a stand-in
+// for the CUs an RCCL collective holds while the step's kernels run on the rest.  Bounded: every wave exits.
+__global__ void cu_hog_kernel(uint64_t ticks, int* __restrict__ sink) {
+  extern __shared__ int hog_lds[];
+  // sink[1] (host-mapped): workgroups resident so far -- the host starts timing once all are
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(sink + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t t0 = wall_clock();
+  while (wall_clock() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+  hog_lds[threadIdx.x] = (int)threadIdx.x;
+  __syncthreads();
+  if (threadIdx.x == 0 && hog_lds[1] == 12345) sink[0] = 1;  // never true: keeps the LDS allocation live
+}
+
 }  // namespace
 
 extern "C" {
@@ -472,6 +486,16 @@ int dtc_p2p_all_gather(const void* x, void* out, long loc_bytes, void* const* ba
   DTC_CHECK_LAUNCH();
   const int blocks = (int)std::min(1024L, std::max(1L, (n16 * world + 255) / 256));
   hipLaunchKernelGGL(p2p_ag_kernel, dim3(blocks), dim3(256), 0, st, t, world, n16, half_bytes, (u32x4*)out, epoch);
+  DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+int dtc_cu_hog(int blocks, long ticks, int lds_bytes, int* sink, hipStream_t st) {
+  if (blocks <= 0) return 0;
+  if (ticks <= 0 || ticks > 200000000L || lds_bytes < 1024) return 4001;  // at most 2 s
+  hipError_t e = hipFuncSetAttribute((const void*)cu_hog_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(cu_hog_kernel, dim3(blocks), dim3(256), lds_bytes, st, (uint64_t)ticks, sink);
   DTC_CHECK_LAUNCH();
   return 0;
 }

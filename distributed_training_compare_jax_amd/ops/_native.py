@@ -150,6 +150,7 @@ def _declare(lib):
         "dtc_p2p_barrier_round": ([vp, i, i, vp, vp, vp], i),
         "dtc_p2p_reduce_scatter": ([vp, i, vp, l, vp, i, i, l, vp, vp, vp, vp, i, vp], i),
         "dtc_p2p_all_gather": ([vp, vp, l, vp, i, i, l, vp, vp, vp], i),
+        "dtc_cu_hog": ([i, l, i, vp, vp], i),
         "dtc_embed_sort_bits": ([i], i),
         "dtc_embed_sort": ([vp, i, i, vp, vp], i),
         "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),

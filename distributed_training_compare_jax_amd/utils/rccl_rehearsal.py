@@ -71,11 +71,15 @@ def run_case(name: str, dinfo) -> dict:
             "zero": bool(eng.zero), "embed_gather": bool(eng.embed_gather)}
 
 
-def bench_case(name: str, dinfo, model: str = "gpt2-small", steps: int = 20, warmup: int = 4) -> dict:
+def bench_case(name: str, dinfo, model: str = "gpt2-small", steps: int = 20, warmup: int = 4, hog_cus: int = 0) -> dict:
     """ms/step of one case on a real model (bench.py's timing: graph replays back to back, one loss
     read per step one step late): ``plain`` vs the rehearsals measures what the DP code path costs at
     dp1 before any communication (comm-safe GEMM plans, grouped weight gradients of 2 layers, the
-    embedding gather, the graph cuts) and what capturing the collectives saves."""
+    embedding gather, the graph cuts) and what capturing the collectives saves.
+
+    ``hog_cus`` > 0: a probe kernel holds that many CUs for the whole timed loop (``dtc_cu_hog`` on a side
+    stream; the time is taken with events on the step's stream) -- the CU-steal proxy of a DP step whose
+    RCCL kernels occupy CUs while the backward runs: which GEMM plans (one-round / comm-safe) cope better."""
     import time
 
     from ..config.schema import OptimConfig, TrainConfig, model_config_from_preset
@@ -96,6 +100,24 @@ def bench_case(name: str, dinfo, model: str = "gpt2-small", steps: int = 20, war
         eng.loss_value()
     barrier()
     torch.cuda.synchronize()
+    hog = None
+    if hog_cus > 0:
+        from ..ops import _native as N
+
+        hs = torch.cuda.Stream(priority=-1)  # its own hardware queue (a shared one would serialise it)
+        sink = torch.zeros(4, dtype=torch.int32, pin_memory=True)  # host-mapped: polled without a stream op
+        ticks = int(steps * 0.025 * 1e8)  # 25 ms per step of the 100 MHz clock: outlasts the loop
+        with torch.cuda.stream(hs):
+            N.check(N.lib().dtc_cu_hog(hog_cus, ticks, 160 * 1024 - 1024, sink.data_ptr(), N.stream_ptr(dinfo.device)),
+                    "dtc_cu_hog")
+        hog = (hs, sink)
+        t_w = time.perf_counter()
+        while int(sink[1]) < hog_cus and time.perf_counter() - t_w < 0.2:
+            time.sleep(0.0005)
+        if int(sink[1]) < hog_cus:
+            raise RuntimeError(f"CU probe: only {int(sink[1])} of {hog_cus} workgroups resident")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
     t0 = time.perf_counter()
     pending = None
     for _ in range(steps):
@@ -106,9 +128,15 @@ def bench_case(name: str, dinfo, model: str = "gpt2-small", steps: int = 20, war
             eng.read_loss(pending)
         pending = h
     loss = eng.read_loss(pending)
-    torch.cuda.synchronize()
+    ev1.record()
+    ev1.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
-    out = {"ms_per_step": ms, "graphs": eng.program.n_graphs, "comms": eng.program.n_comms, "loss": loss}
+    if hog is not None:
+        ms = ev0.elapsed_time(ev1) / steps
+        hog[0].synchronize()
+    torch.cuda.synchronize()
+    out = {"ms_per_step": ms, "graphs": eng.program.n_graphs, "comms": eng.program.n_comms, "loss": loss,
+           "hog_cus": hog_cus}
     del eng
     torch.cuda.empty_cache()
     return out
@@ -172,6 +200,10 @@ def main(argv):
     bench = argv[0] == "--bench"
     if bench:
         argv = argv[1:]
+    hogs = [0]
+    if argv and argv[0].startswith("--hog="):  # CU-steal proxy: --hog=0,16,32
+        hogs = [int(x) for x in argv[0].split("=", 1)[1].split(",")]
+        argv = argv[1:]
     path = argv[0]
     cases = argv[1:] or list(CASES)
     d = init_distributed("cuda", single_rank_pg=True)
@@ -188,10 +220,14 @@ def main(argv):
         res["bench"] = {}
         for rnd in range(2):  # interleaved rounds (box clock drift)
             for c in cases:
-                r = bench_case(c, d)
-                res["bench"].setdefault(c, []).append(r)
-                print(f"[bench] round {rnd} {c}: {r['ms_per_step']:.3f} ms/step ({r['graphs']} graph segments, "
-                      f"{r['comms']} eager collectives)", flush=True)
+                for hc in hogs:
+                    safe = not c.endswith("_unsafe")
+                    os.environ["DTC_COMM_SAFE_GEMMS"] = "1" if safe else "0"
+                    r = bench_case(c.replace("_unsafe", ""), d, hog_cus=hc)
+                    res["bench"].setdefault(f"{c} hog{hc}", []).append(r)
+                    print(f"[bench] round {rnd} {c} hog {hc} CUs: {r['ms_per_step']:.3f} ms/step ({r['graphs']} graph "
+                          f"segments, {r['comms']} eager collectives)", flush=True)
+            os.environ["DTC_COMM_SAFE_GEMMS"] = "1"
         torch.save(res, path)
         destroy()
         return
