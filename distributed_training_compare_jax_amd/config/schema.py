@@ -136,7 +136,9 @@ class TrainConfig:
     wgrad_group: Optional[int] = None  # deferred grouped weight gradients (models/gpt.py set_wgrad_group)
     pp_split: str = "cost"  # cost | even: PP layer split (parallel/mesh.py split_layers)
     dp_grad_dtype: str = "fp32"  # fp32 | bf16: DP gradient payload (bf16: all-to-all + fp32 shard sums)
-    pp_comm_dtype: str = "fp32"  # fp32 | bf16: PP activation / gradient messages
+    # fp32 | bf16 | auto: PP activation / gradient messages; auto = bf16 when the compute dtype is bf16 (5000-step
+    # pp2 curve: the same gap to dp1 as fp32 messages; half the bytes of the latency-bound pp8 hops)
+    pp_comm_dtype: str = "auto"
     # fp32 | bf16 | auto: TP row-parallel / input-gradient partials (fp32 sums either way); auto = bf16 when the
     # compute dtype is bf16 (5000-step tp2 curve: the same gap to dp1 as fp32, profiles/r5_cross_strategy.md)
     tp_comm_dtype: str = "auto"

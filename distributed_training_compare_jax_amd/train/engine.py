@@ -255,9 +255,10 @@ class Engine:
                               for _ in range(self.n_micro)] if self.act_dtype != torch.float32 else self.recv_dx
             # pp_comm_dtype=bf16: stage messages travel as bf16 (send images cast after the producing compute,
             # received images cast back to the fp32 residual stream before the consuming compute)
-            if train_cfg.pp_comm_dtype not in ("fp32", "bf16"):
-                raise ValueError(f"pp_comm_dtype={train_cfg.pp_comm_dtype!r}: expected 'fp32' or 'bf16'")
-            self.pp_bf16 = train_cfg.pp_comm_dtype == "bf16"
+            pcd = train_cfg.pp_comm_dtype
+            if pcd not in ("fp32", "bf16", "auto"):
+                raise ValueError(f"pp_comm_dtype={pcd!r}: expected 'fp32', 'bf16' or 'auto'")
+            self.pp_bf16 = pcd == "bf16" or (pcd == "auto" and self.act_dtype == torch.bfloat16)
             if self.pp_head_split and m.pp_idx >= pp - 2:
                 # the final LayerNorm output (A -> B, compute dtype) and the halves' packed row statistics
                 self.recv_yf = [torch.zeros(self.mb_rows * T, D, dtype=self.act_dtype, device=self.device)

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--png", default=None)
     ap.add_argument("--window", type=int, default=100)
     a = ap.parse_args()
-    runs = {k: pd.read_csv(os.path.join(a.root, k, "log.csv")) for k in ("dp", "tp", "tp_bf16", "tp_sp", "pp", "pp_zb")
+    runs = {k: pd.read_csv(os.path.join(a.root, k, "log.csv")) for k in ("dp", "tp", "tp_bf16", "tp_sp", "pp", "pp_zb", "pp_bf16")
             if os.path.exists(os.path.join(a.root, k, "log.csv"))}
     n = min(len(d) for d in runs.values())
     L = {k: d.loss.values[:n] for k, d in runs.items()}
@@ -31,7 +31,7 @@ def main():
              f"{n} timed steps each after 5 warmup steps, `main.py` with the reference YAMLs: dp = 1 process; tp = 2 "
              "processes, TP all-reduces on the in-graph P2P kernels (fp32 partials; tp_bf16: bf16 partials, fp32 "
              "sums; tp_sp: bf16 partials + sequence parallelism, reduce-scatter / all-gather); pp = 2 processes, 1F1B with 8 microbatches (`configs/train_config_pp_1f1b.yaml`; pp_zb: the "
-             "zero-bubble B/W split).  The 2-process runs share one GPU over gloo, so their step times "
+             "zero-bubble B/W split; pp_bf16: bf16 stage messages).  The 2-process runs share one GPU over gloo, so their step times "
              "measure nothing about multi-GPU scaling.  Same synthetic data stream and canonical init in every run.", "",
              "| run | step-0 loss | last-50 mean | avg step (ms, shared GPU) |", "|---|---|---|---|"]
     for k in L:
@@ -56,7 +56,7 @@ def main():
         import matplotlib.pyplot as plt
 
         plt.figure(figsize=(8, 4))
-        for k, c in zip(L, ("red", "green", "orange", "brown", "blue", "purple")):
+        for k, c in zip(L, ("red", "green", "orange", "brown", "blue", "purple", "cyan")):
             plt.plot(L[k], label=k, alpha=0.5, color=c)
         plt.xlabel("step")
         plt.ylabel("loss")

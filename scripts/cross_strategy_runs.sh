@@ -15,18 +15,21 @@ $T 400 python main.py --train_config_path configs/train_config_dp.yaml --nproc 1
     --output_dir $OUT/dp > $OUT/dp.log 2>&1 || exit $?
 tail -n 2 $OUT/dp.log
 DTC_DIST_BACKEND=gloo $T 600 python main.py --train_config_path configs/train_config_tp.yaml --nproc 2 --steps $STEPS \
-    --log_every 250 --output_dir $OUT/tp --set tp_comm=p2p > $OUT/tp.log 2>&1 || exit $?
+    --log_every 250 --output_dir $OUT/tp --set tp_comm=p2p --set tp_comm_dtype=fp32 --set tp_sequence_parallel=false > $OUT/tp.log 2>&1 || exit $?
 tail -n 2 $OUT/tp.log
 DTC_DIST_BACKEND=gloo $T 600 python main.py --train_config_path configs/train_config_tp.yaml --nproc 2 --steps $STEPS \
-    --log_every 250 --output_dir $OUT/tp_bf16 --set tp_comm=p2p --set tp_comm_dtype=bf16 > $OUT/tp_bf16.log 2>&1 || exit $?
+    --log_every 250 --output_dir $OUT/tp_bf16 --set tp_comm=p2p --set tp_comm_dtype=bf16 --set tp_sequence_parallel=false > $OUT/tp_bf16.log 2>&1 || exit $?
 tail -n 2 $OUT/tp_bf16.log
 DTC_DIST_BACKEND=gloo $T 600 python main.py --train_config_path configs/train_config_tp.yaml --nproc 2 --steps $STEPS \
     --log_every 250 --output_dir $OUT/tp_sp --set tp_comm=p2p --set tp_comm_dtype=bf16 --set tp_sequence_parallel=true \
     > $OUT/tp_sp.log 2>&1 || exit $?
 tail -n 2 $OUT/tp_sp.log
 DTC_DIST_BACKEND=gloo $T 900 python main.py --train_config_path configs/train_config_pp_1f1b.yaml --nproc 2 --steps $STEPS \
-    --log_every 250 --output_dir $OUT/pp > $OUT/pp.log 2>&1 || exit $?
+    --log_every 250 --output_dir $OUT/pp --set pp_comm_dtype=fp32 > $OUT/pp.log 2>&1 || exit $?
 tail -n 2 $OUT/pp.log
 DTC_DIST_BACKEND=gloo $T 900 python main.py --train_config_path configs/train_config_pp_1f1b.yaml --nproc 2 --steps $STEPS \
-    --log_every 250 --output_dir $OUT/pp_zb --set pp_schedule=zb > $OUT/pp_zb.log 2>&1 || exit $?
+    --log_every 250 --output_dir $OUT/pp_zb --set pp_schedule=zb --set pp_comm_dtype=fp32 > $OUT/pp_zb.log 2>&1 || exit $?
 tail -n 2 $OUT/pp_zb.log
+DTC_DIST_BACKEND=gloo $T 900 python main.py --train_config_path configs/train_config_pp_1f1b.yaml --nproc 2 --steps $STEPS \
+    --log_every 250 --output_dir $OUT/pp_bf16 --set pp_comm_dtype=bf16 > $OUT/pp_bf16.log 2>&1 || exit $?
+tail -n 2 $OUT/pp_bf16.log
