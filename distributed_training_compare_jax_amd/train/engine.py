@@ -116,7 +116,12 @@ class Engine:
         # ---- step program, comms, model, optimizer
         cap = train_cfg.capture_comms
         if cap is None:
-            cap = dinfo.backend == "nccl" and os.environ.get("DTC_CAPTURE_COMMS", "1") == "1"
+            # auto: captured on a one-rank RCCL group (the rehearsal, where it was measured: -0.23 ms) and
+            # wherever DTC_CAPTURE_COMMS=1 asks for it; a multi-rank step cuts its graph at each collective
+            # (the eager path) until capture has run against real peers over xGMI -- an RCCL kernel that
+            # misbehaves inside a capture costs the whole run, an eager one a fraction of a millisecond
+            env = os.environ.get("DTC_CAPTURE_COMMS", "auto")
+            cap = dinfo.backend == "nccl" and (env == "1" or (env == "auto" and dinfo.world == 1))
         self.program = StepProgram(self.device, use_graph=train_cfg.use_graph and on_gpu, capture_comms=cap)
         # gloo on GPU tensors (the one-GPU multi-rank rig): collectives complete where they are issued,
         # so no copy-back from gloo's worker thread can queue behind a later cross-process wait
