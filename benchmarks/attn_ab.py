@@ -60,7 +60,7 @@ def main():
         print(f"fwd 32-row vs 16-row kernel: max |do| {(o.float() - o4.float()).abs().max().item():.3e}", flush=True)
         print(f"fwd round-4 32-row kernel vs round-5 default: max |do| {(o.float() - o5.float()).abs().max().item():.3e} "
               f"max |dlse| {(lse - lse5).abs().max().item():.3e}", flush=True)
-        variants = {"fwd (round 5: 2-deep prefetch)": lambda: A.attn_fwd(qkv, H),
+        variants = {"fwd (round 5 default)": lambda: A.attn_fwd(qkv, H),
                     "fwd (round 4: 32 q/wave)": lambda: A.attn_fwd(qkv, H, flags=16),
                     "fwd (16 q/wave chunk)": lambda: A.attn_fwd(qkv, H, flags=4),
                     "bwd (32 rows/wave)": lambda: A.attn_bwd(qkv, o, lse, do, H),

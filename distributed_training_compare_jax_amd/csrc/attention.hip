@@ -855,15 +855,19 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd32_kernel(const bf16* _
 
 // ---------------------------------------------------------------------------- forward, round 5 pipeline
 // attn_fwd32_kernel's math (transposed score tile, lane-local softmax, deferred max, P straight from the
-// accumulators into PV) with a deeper load pipeline:
+// accumulators into PV) with a deeper load pipeline and one code path per tile:
 //  * TWO register sets alternate (the loop is unrolled by 2, named sets, no runtime-indexed registers), so
 //    tile t+2's K/V loads are issued at the top of tile t and have two compute phases + a barrier to land;
 //    the loads are unconditional (a load in a branch makes hipcc wait vmcnt(0) at the next LDS write);
 //  * all of a tile's V^T fragments (8 x 4 VGPRs) are requested right after the QK^T MFMAs, so they land
 //    under the softmax and the 8 PV MFMAs issue back to back;
-//  * two running row sums instead of one serial chain of 32 dependent adds.
-// Measured (profiles/r5_attention.md): 27.5-28.0 vs 28.2-28.4 us per GPT-2-small layer; the PMC wave-cycle
-// total is unchanged -- the round-4 kernel's stalls were not dominated by these two waits.
+//  * two running row sums instead of one serial chain of 32 dependent adds;
+//  * the diagonal mask under a wave-uniform runtime branch inside ONE tile body: two template
+//    instantiations of the whole tile (masked / unmasked) got different register assignments for the O
+//    accumulators and ended every tile in ~31 v_mov_b64 copies at the join; one body: 180 instead of 248
+//    VGPRs, 12 copies per tile.
+// Measured (profiles/r5_attention.md): 26.6-26.9 us per GPT-2-small layer (two instantiations: 27.9-28.2,
+// round-4 kernel 28.2-28.5).  At 3 waves / SIMD (168 VGPRs, 48 B spilled): 30.7 us.
 template <int HD>
 __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
                                                              float* __restrict__ lse, int B, int T, int H,
@@ -899,7 +903,7 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __
   for (int i = 0; i < HB; ++i) acc[i] = f32x16{};
   const int qlim = min(q, T - 1);
 
-  auto tile = [&](const bf16* sK, const bf16* sV, int kb, auto MASK) {
+  auto tile = [&](const bf16* sK, const bf16* sV, int kb, bool diag) {
     bf16x8 kf[2][HC];
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2)
@@ -920,7 +924,7 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int i = 0; i < HB; ++i) vf[k2][s2][i] = vt_frag32(sV, L::VLD, 32 * k2 + 16 * s2, 32 * i, lane);
-    if constexpr (decltype(MASK)::value) {
+    if (diag) {  // wave-uniform: only the tiles that cross this wave's diagonal pay for the compares
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
         const int lim = qlim - (kb + 32 * k2 + 4 * hh);
@@ -968,10 +972,7 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __
   auto compute = [&](int it) {
     const int kb = it * FW_KEYS;
     const bf16* sK = lds + (it & 1) * L::STAGE;
-    if (kb <= q0 + 31 && q0 < T) {  // wave-uniform
-      if (kb + FW_KEYS - 1 > q0) tile(sK, sK + FW_KEYS * L::KLD, kb, std::true_type{});
-      else tile(sK, sK + FW_KEYS * L::KLD, kb, std::false_type{});
-    }
+    if (kb <= q0 + 31 && q0 < T) tile(sK, sK + FW_KEYS * L::KLD, kb, kb + FW_KEYS - 1 > q0);  // wave-uniform
   };
   auto store = [&](const RS& rs, int buf) {
     bf16* sK = lds + buf * L::STAGE;
@@ -1144,10 +1145,11 @@ __device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv,
   f32x16 acc[HB];
 #pragma unroll
   for (int i = 0; i < HB; ++i) acc[i] = f32x16{};
-  // one 32-key block; MASK only on the diagonal blocks (a separate instantiation, so the full blocks
-  // carry no per-element compares).  Keys >= T only meet queries >= T (key <= q), whose rows are never
-  // written, and load as zeros (buffer range): the causal mask suffices.
-  auto kblock = [&](const bf16* sK, const bf16* sV, int k2, int ks, auto MASK) {
+  // one 32-key block; the causal mask only on the diagonal blocks, under a wave-uniform branch inside ONE
+  // body (two instantiations of the whole block joined with 16 v_mov_b64 copies of the dQ accumulators per
+  // block: 79.4 -> 78.7 us per merged backward, profiles/r5_attention.md).  Keys >= T only meet queries >= T
+  // (key <= q), whose rows are never written, and load as zeros (buffer range): the causal mask suffices.
+  auto kblock = [&](const bf16* sK, const bf16* sV, int k2, int ks, bool diag) {
     f32x16 st = f32x16{}, dp = f32x16{};
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
@@ -1156,11 +1158,13 @@ __device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv,
     }
     const int lim = q - (ks + 4 * hh);  // register i holds key ks + 4h + (i & 3) + 8 (i >> 2)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float pv = fast_exp2(fmaf(st[i], cs, -lq));
-      if constexpr (decltype(MASK)::value) pv = ((i & 3) + 8 * (i >> 2) <= lim) ? pv : 0.f;
-      st[i] = pv * (dp[i] - dlt);
+    for (int i = 0; i < 16; ++i) st[i] = fast_exp2(fmaf(st[i], cs, -lq));
+    if (diag) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] = ((i & 3) + 8 * (i >> 2) <= lim) ? st[i] : 0.f;
     }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) st[i] *= dp[i] - dlt;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 dsb = pack8(st, s2);
@@ -1175,8 +1179,7 @@ __device__ __forceinline__ void dq32_body(int bid, const bf16* __restrict__ qkv,
     for (int k2 = 0; k2 < 2; ++k2) {
       const int ks = kb + 32 * k2;
       if (ks > q0 + 31) break;  // wave-uniform: these 32 keys lie past every query
-      if (ks + 31 > q0) kblock(sK, sV, k2, ks, std::true_type{});
-      else kblock(sK, sV, k2, ks, std::false_type{});
+      kblock(sK, sV, k2, ks, ks + 31 > q0);
     }
   };
   const int nkt = (min(T, qblk * FW_QROWS + FW_QROWS) + 63) / 64;
@@ -2037,8 +2040,9 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
     DTC_CHECK_LAUNCH();
     return 0;
   }
-  // default at head_dim 64: the round-5 forward (2-deep K/V prefetch, V^T fragments ahead of the softmax;
-  // 27.5-28.0 vs 28.2-28.4 us per layer, profiles/r5_attention.md); flags bit 4 = the round-4 kernel (A/B),
+  // default at head_dim 64: the round-5 forward (2-deep K/V prefetch, V^T fragments ahead of the softmax, one
+  // code path per tile; 26.6-26.9 vs 28.2-28.5 us per layer, profiles/r5_attention.md); flags bit 4 = the
+  // round-4 kernel (A/B),
   // bit 2 = the 16-row chunked kernel
   if (HD == 64 && !(flags & 16) && !(flags & 4) && attn_chunk_enabled()) {
     allow_lds(attn_fwd5_kernel<64>, fw_lds_bytes<64>());
