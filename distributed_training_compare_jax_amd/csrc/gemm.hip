@@ -3167,6 +3167,9 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
   if (a2->epi != EPI_STORE || !a2->c_f32 || a2->bias) return 1100;
   if (big_split(a1->layout, a1->M, a1->N, a1->K) || big_split(2, a2->M, a2->N, a2->K)) return 1100;
   if (n8_cb(a1->layout, a1->M, a1->N, a1->K, a1->epi)) return 1100;  // dgrad on gemm8n_kernel: own launch
+  if (a1->alpha == 1.f && a1->beta == 0.f && !a1->colsum &&
+      r8_plan(a1->layout, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0).cb2)
+    return 1100;  // dgrad on gemm8r_kernel: own launch (the same plan dtc_gemm picks for it alone)
   if (dmaw_plan(a1->layout, a1->M, a1->N, a1->K, a1->epi, a1->c_f32 != 0, false).cfg != W_NONE ||
       dmaw_plan(2, a2->M, a2->N, a2->K, a2->epi, a2->c_f32 != 0, a2->colsum != nullptr).cfg != W_NONE)
     return 1100;  // the 8-wave kernels run these as two launches
