@@ -478,6 +478,133 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   } while (STRIDE);
 }
 
+// ---- AdamW with the transposed bf16 mirror written by the update itself (DTC_ADAMW_TR) -------------------
+// The weights that keep a transposed compute copy (fc1 / qkv / out_proj / lm_head: their dgrads run NT on
+// W^T) are updated in 64 x 64 tiles whose bf16 values go through LDS into W^T as well, so the separate
+// transpose pass (re-reading the fresh mirror: 72 us per GPT-2-small step) disappears; every other range of
+// the flat buffer takes the element-wise update in one segmented launch.  Same per-element arithmetic as
+// adamw_kernel (one shared function): p, m, v, the mirror and W^T are bitwise what the two-pass path writes.
+__device__ __forceinline__ void adamw4(f32x4& p, const f32x4& g, f32x4& m, f32x4& v, float clip, float bc1, float bc2,
+                                       float lr, float b1, float b2, float eps, float wd) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float gc = g[r] * clip;
+    m[r] = fmaf(b1, m[r], (1.f - b1) * gc);
+    v[r] = fmaf(b2, v[r], ((1.f - b2) * gc) * gc);
+    const float mh = m[r] / bc1, vh = v[r] / bc2;
+    p[r] = fmaf(-lr, fmaf(wd, p[r], mh / (sqrtf(vh) + eps)), p[r]);
+  }
+}
+
+struct AwHyper {
+  const int64_t* step;
+  const float* sumsq;
+  float lr, b1, b2, eps, wd, max_norm;
+};
+__device__ __forceinline__ void aw_prologue(const AwHyper& h, float& clip, float& bc1, float& bc2) {
+  const float norm = sqrtf(h.sumsq[0]);
+  clip = (h.max_norm > 0.f && !(norm < h.max_norm)) ? h.max_norm / norm : 1.f;
+  const float t = (float)h.step[0];
+  bc1 = 1.f - powf(h.b1, t);
+  bc2 = 1.f - powf(h.b2, t);
+}
+
+constexpr int AW_MAX_SEG = 96;
+struct AwSeg {
+  long lo, n;   // flat range [lo, lo + n), 4-aligned
+  int blk0, pad;
+};
+struct AwSegs {
+  int nseg, nblocks;
+  AwSeg s[AW_MAX_SEG];
+};
+// element-wise update of the segments (the ranges without a transposed copy), 4 x 4 elements per thread
+__global__ void __launch_bounds__(256) adamw_seg_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        bf16* __restrict__ mirror, long n_mirror, AwSegs segs,
+                                                        AwHyper h) {
+  int lo = 0, hi = segs.nseg - 1;  // the segment whose block range holds blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)blockIdx.x >= segs.s[mid].blk0) lo = mid; else hi = mid - 1;
+  }
+  const AwSeg& S = segs.s[lo];
+  float clip, bc1, bc2;
+  aw_prologue(h, clip, bc1, bc2);
+  const long base = S.lo + (long)(blockIdx.x - S.blk0) * 256 * 16;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const long j = base + (long)c * 1024 + threadIdx.x * 4;
+    if (j >= S.lo + S.n) break;
+    DTC_ASSERT(j + 4 <= S.lo + S.n);
+    f32x4 pp = __builtin_nontemporal_load((f32x4*)(p + j)), gg = __builtin_nontemporal_load((const f32x4*)(g + j));
+    f32x4 mm = __builtin_nontemporal_load((f32x4*)(m + j)), vv = __builtin_nontemporal_load((f32x4*)(v + j));
+    adamw4(pp, gg, mm, vv, clip, bc1, bc2, h.lr, h.b1, h.b2, h.eps, h.wd);
+    __builtin_nontemporal_store(pp, (f32x4*)(p + j));
+    __builtin_nontemporal_store(mm, (f32x4*)(m + j));
+    __builtin_nontemporal_store(vv, (f32x4*)(v + j));
+    if (j < n_mirror) *(bf16x4*)(mirror + j) = bf16x4{f2bf(pp[0]), f2bf(pp[1]), f2bf(pp[2]), f2bf(pp[3])};
+  }
+}
+
+constexpr int AWT_MAX = 64;
+struct AwtTask {
+  long off;     // flat offset of the [rows][cols] weight (its mirror sits at the same offset)
+  bf16* dst;    // W^T [cols][rows]
+  int rows, cols, blk0, pad;
+};
+struct AwtBatch {
+  int ntasks, nblocks;
+  AwtTask t[AWT_MAX];
+};
+// 64 x 64 tiles of the transposed-mirror weights: update, mirror, and W^T through an LDS tile
+__global__ void __launch_bounds__(256) adamw_tr_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       bf16* __restrict__ mirror, AwtBatch b, AwHyper h) {
+  int lo = 0, hi = b.ntasks - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)blockIdx.x >= b.t[mid].blk0) lo = mid; else hi = mid - 1;
+  }
+  const AwtTask& T = b.t[lo];
+  const int tcols = (T.cols + 63) / 64, bi = blockIdx.x - T.blk0;
+  DTC_ASSERT(bi >= 0 && bi < ((T.rows + 63) / 64) * tcols && T.cols % 4 == 0 && T.rows % 8 == 0);
+  const int r0 = (bi / tcols) * 64, c0 = (bi % tcols) * 64;
+  __shared__ bf16 tile[64][64 + 1];  // row length 65: the column reads below spread over the banks
+  float clip, bc1, bc2;
+  aw_prologue(h, clip, bc1, bc2);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 64 rows x 16 groups of 4 columns: a row is 16 lanes x 16 B
+    const int c = tid + 256 * i, r = c >> 4, c4 = (c & 15) * 4;
+    bf16x4 o = {};
+    if (r0 + r < T.rows && c0 + c4 + 4 <= T.cols) {
+      const long j = T.off + (long)(r0 + r) * T.cols + c0 + c4;
+      f32x4 pp = __builtin_nontemporal_load((f32x4*)(p + j)), gg = __builtin_nontemporal_load((const f32x4*)(g + j));
+      f32x4 mm = __builtin_nontemporal_load((f32x4*)(m + j)), vv = __builtin_nontemporal_load((f32x4*)(v + j));
+      adamw4(pp, gg, mm, vv, clip, bc1, bc2, h.lr, h.b1, h.b2, h.eps, h.wd);
+      __builtin_nontemporal_store(pp, (f32x4*)(p + j));
+      __builtin_nontemporal_store(mm, (f32x4*)(m + j));
+      __builtin_nontemporal_store(vv, (f32x4*)(v + j));
+      o = bf16x4{f2bf(pp[0]), f2bf(pp[1]), f2bf(pp[2]), f2bf(pp[3])};
+      *(bf16x4*)(mirror + j) = o;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[r][c4 + e] = o[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // W^T rows = W columns, 8 x 16 B per row
+    const int c = tid + i * 256, dr = c >> 3, ch = (c & 7) * 8;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = tile[ch + e][dr];
+    // non-temporal: W^T is read only in the backward (as transpose_batch_kernel's stores)
+    if (c0 + dr < T.cols && r0 + ch + 8 <= T.rows)
+      __builtin_nontemporal_store(o, (bf16x8*)(T.dst + (long)(c0 + dr) * T.rows + r0 + ch));
+  }
+}
+
 __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, long n) {
   long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i + 4 <= n) {
@@ -697,6 +824,31 @@ int dtc_adamw(float* p, const float* g, float* m, float* v, bf16* mirror, long n
   else  // DTC_ADAMW_CH 4-element groups per thread, one grid step
     hipLaunchKernelGGL((adamw_kernel<false, DTC_ADAMW_CH>), dim3(blocks), dim3(256), 0, st, p, g, m, v, mirror, n, n_mirror, step, sumsq, lr, b1, b2, eps, wd, max_norm, enable);
   DTC_CHECK_LAUNCH();
+  return 0;
+}
+
+// fused AdamW + transposed mirror: segments (element-wise) and tiles (with W^T); the host builds both lists
+int dtc_aw_max_seg() { return AW_MAX_SEG; }
+int dtc_aw_max_tasks() { return AWT_MAX; }
+int dtc_aw_seg_bytes() { return (int)sizeof(AwSeg); }
+int dtc_aw_task_bytes() { return (int)sizeof(AwtTask); }
+int dtc_adamw_tr(float* p, const float* g, float* m, float* v, bf16* mirror, long n_mirror, const AwSegs* segs,
+                 const AwtBatch* tasks, const int64_t* step, const float* sumsq, float lr, float b1, float b2, float eps,
+                 float wd, float max_norm, hipStream_t st) {
+  if (segs->nseg > AW_MAX_SEG || tasks->ntasks > AWT_MAX || n_mirror % 4) return 3005;
+  for (int i = 0; i < segs->nseg; ++i)
+    if (segs->s[i].lo % 4 || segs->s[i].n % 4) return 3005;
+  for (int i = 0; i < tasks->ntasks; ++i)
+    if (tasks->t[i].rows % 8 || tasks->t[i].cols % 4 || tasks->t[i].off % 4) return 3011;
+  const AwHyper h{step, sumsq, lr, b1, b2, eps, wd, max_norm};
+  if (segs->nseg > 0 && segs->nblocks > 0) {
+    hipLaunchKernelGGL(adamw_seg_kernel, dim3(segs->nblocks), dim3(256), 0, st, p, g, m, v, mirror, n_mirror, *segs, h);
+    DTC_CHECK_LAUNCH();
+  }
+  if (tasks->ntasks > 0 && tasks->nblocks > 0) {
+    hipLaunchKernelGGL(adamw_tr_kernel, dim3(tasks->nblocks), dim3(256), 0, st, p, g, m, v, mirror, *tasks, h);
+    DTC_CHECK_LAUNCH();
+  }
   return 0;
 }
 

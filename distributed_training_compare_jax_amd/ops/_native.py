@@ -167,6 +167,11 @@ def _declare(lib):
         "dtc_adamw": ([vp, vp, vp, vp, vp, l, l, vp, vp, f, f, f, f, f, f, vp, i, vp], i),
         "dtc_cast_f32_bf16": ([vp, vp, l, vp], i),
         "dtc_transpose_batch": ([vp, vp], i),
+        "dtc_aw_max_seg": ([], i),
+        "dtc_aw_max_tasks": ([], i),
+        "dtc_aw_seg_bytes": ([], i),
+        "dtc_aw_task_bytes": ([], i),
+        "dtc_adamw_tr": ([vp, vp, vp, vp, vp, l, vp, vp, vp, vp, f, f, f, f, f, f, vp], i),
         "dtc_tr_max_tasks": ([], i),
         "dtc_tr_task_bytes": ([], i),
         "dtc_fill_f32": ([vp, f, l, vp], i),

@@ -159,6 +159,81 @@ def transpose_batch(pairs):
         N.check(L.dtc_transpose_batch(ctypes.byref(b), N.stream_ptr(src.device)), "dtc_transpose_batch")
 
 
+class _AwSeg(ctypes.Structure):
+    """Mirror of ``struct AwSeg`` (csrc/elementwise.hip)."""
+
+    _fields_ = [("lo", ctypes.c_long), ("n", ctypes.c_long), ("blk0", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+_AW_SEG_MAX, _AW_TASK_MAX = 96, 64
+
+
+class _AwSegs(ctypes.Structure):
+    _fields_ = [("nseg", ctypes.c_int), ("nblocks", ctypes.c_int), ("s", _AwSeg * _AW_SEG_MAX)]
+
+
+class _AwtTask(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_long), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int), ("cols", ctypes.c_int),
+                ("blk0", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+class _AwtBatch(ctypes.Structure):
+    _fields_ = [("ntasks", ctypes.c_int), ("nblocks", ctypes.c_int), ("t", _AwtTask * _AW_TASK_MAX)]
+
+
+def adamw_tr_plan(lo: int, hi: int, mats):
+    """Launch lists of :func:`adamw_tr` over flat[lo:hi]: ``mats`` = [(offset, rows, cols, W^T tensor)] of the
+    weights that keep a transposed mirror (inside the range).  Returns [(segments, tiles)] chunks (each
+    within the kernels' list capacities), or None when a shape does not fit the tiled kernel."""
+    mats = sorted(mats, key=lambda x: x[0])
+    if any(r % 8 or c % 4 or o % 4 for o, r, c, _ in mats):
+        return None
+    segs, cur = [], lo
+    for o, r, c, _ in mats:
+        if o > cur:
+            segs.append((cur, o - cur))
+        cur = o + r * c
+    if hi > cur:
+        segs.append((cur, hi - cur))
+    if any(a % 4 or n % 4 for a, n in segs):
+        return None
+    chunks = []
+    while segs or mats:
+        sb, tb = _AwSegs(), _AwtBatch()
+        blk = 0
+        take = segs[:_AW_SEG_MAX]
+        segs = segs[_AW_SEG_MAX:]
+        for j, (a, n) in enumerate(take):
+            sb.s[j] = _AwSeg(a, n, blk, 0)
+            blk += (n + 4095) // 4096
+        sb.nseg, sb.nblocks = len(take), blk
+        blk = 0
+        tk = mats[:_AW_TASK_MAX]
+        mats = mats[_AW_TASK_MAX:]
+        for j, (o, r, c, dst) in enumerate(tk):
+            assert tuple(dst.shape) == (c, r) and dst.is_contiguous()
+            tb.t[j] = _AwtTask(o, dst.data_ptr(), r, c, blk, 0)
+            blk += ((r + 63) // 64) * ((c + 63) // 64)
+        tb.ntasks, tb.nblocks = len(tk), blk
+        chunks.append((sb, tb))
+    return chunks
+
+
+def adamw_tr(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, mirror: torch.Tensor, n_mirror: int,
+             plan, step: torch.Tensor, sumsq: torch.Tensor, lr: float, b1: float, b2: float, eps: float, wd: float,
+             max_norm: float):
+    """AdamW over the flat buffers (absolute offsets in ``plan``, :func:`adamw_tr_plan`) with the transposed
+    bf16 mirror of the tiled weights written by the update itself (no separate transpose pass).  GPU only;
+    bitwise equal to :func:`adamw_flat` + :func:`transpose_batch`."""
+    L = N.lib()
+    assert L.dtc_aw_seg_bytes() == ctypes.sizeof(_AwSeg) and L.dtc_aw_task_bytes() == ctypes.sizeof(_AwtTask)
+    assert L.dtc_aw_max_seg() == _AW_SEG_MAX and L.dtc_aw_max_tasks() == _AW_TASK_MAX
+    for sb, tb in plan:
+        N.check(L.dtc_adamw_tr(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), mirror.data_ptr(), n_mirror,
+                               ctypes.byref(sb), ctypes.byref(tb), step.data_ptr(), sumsq.data_ptr(), lr, b1, b2, eps,
+                               wd, max_norm, N.stream_ptr(p.device)), "dtc_adamw_tr")
+
+
 def fill_(t: torch.Tensor, value: float):
     """t[:] = value (fp32; graph-capturable on GPU)."""
     if not t.is_cuda:

@@ -121,6 +121,11 @@ class FlatParams:
         transpose_batch([(self._view(self.mirror, n), t) for n, (sl, t) in self.mirror_t.items()
                          if sl.offset >= lo and sl.offset + sl.numel <= hi])
 
+    def transposed_in(self, lo: int, hi: int):
+        """[(flat offset, rows, cols, W^T)] of the transposed-mirror weights inside flat[lo:hi]."""
+        return [(sl.offset, sl.shape[0], sl.shape[1], t) for sl, t in self.mirror_t.values()
+                if sl.offset >= lo and sl.offset + sl.numel <= hi]
+
     def wt(self, name: str):
         """Transposed bf16 view ``[in, out]`` of a weight, or None when not kept."""
         e = self.mirror_t.get(name)

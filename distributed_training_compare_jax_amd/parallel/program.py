@@ -288,6 +288,13 @@ class StepProgram:
         cur = torch.cuda.current_stream(self.device)
         self._stream.wait_stream(cur)
         self.recording = True
+        # no cyclic garbage collection during the capture: a collected object of an earlier engine (its
+        # graphs, its pool) must not be destroyed while this stream is capturing -- HIP aborts the process
+        import gc
+
+        gc.collect()
+        gc_was = gc.isenabled()
+        gc.disable()
         try:
             with torch.cuda.stream(self._stream):
                 self._begin()
@@ -317,6 +324,8 @@ class StepProgram:
             raise
         finally:
             self.recording = False
+            if gc_was:
+                gc.enable()
         cur.wait_stream(self._stream)
         torch.cuda.synchronize(self.device)
         self.recorded = True

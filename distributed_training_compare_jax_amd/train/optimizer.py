@@ -13,6 +13,8 @@ over exactly the reference's set of gradients:
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -21,6 +23,10 @@ from ..ops import optim as O
 from ..ops.reduce import GradReducer
 from ..parallel.buffers import FlatParams
 from ..parallel.program import csig
+
+# DTC_ADAMW_TR: the transposed bf16 weight mirror written by the AdamW update itself (one segmented
+# element-wise launch + one tiled launch) instead of a transpose pass re-reading the fresh mirror
+_ADAMW_TR = os.environ.get("DTC_ADAMW_TR", "1") == "1"
 
 
 def merge_segments(segs, total: int):
@@ -65,6 +71,7 @@ class FusedAdamW:
         self.flat = flat
         self.cfg = cfg
         self.program = program
+        self._aw_plans = {}  # (lo, hi) -> fused AdamW + transpose launch lists
         self.tp_size, self.tp_group = tp_size, tp_group
         self.pp_group = pp_group if pp_global_clip else None
         dev = flat.device
@@ -191,6 +198,16 @@ class FusedAdamW:
         if hi <= lo:
             return
         nm = (min(max(f.n_mirror - lo, 0), hi - lo) if f.use_mirror else 0)
+        if nm > 0 and enable is None and max_blocks == 0 and f.params.is_cuda and f.mirror_t and _ADAMW_TR:
+            # the transposed mirror written by the update itself (ops/optim.py adamw_tr)
+            key = (lo, hi)
+            if key not in self._aw_plans:
+                self._aw_plans[key] = O.adamw_tr_plan(lo, hi, f.transposed_in(lo, hi))
+            plan = self._aw_plans[key]
+            if plan is not None:
+                O.adamw_tr(f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.mirror, f.n_mirror, plan, self.step_t,
+                           self.sumsq, c.lr, c.b1, c.b2, c.eps, c.weight_decay, c.grad_clip)
+                return
         O.adamw_flat(f.params[lo:hi], f.grads[lo:hi], f.exp_avg[lo:hi], f.exp_avg_sq[lo:hi],
                      f.mirror[lo:lo + max(nm, 4)] if nm > 0 else None, nm, self.step_t, self.sumsq, c.lr, c.b1, c.b2,
                      c.eps, c.weight_decay, c.grad_clip, enable=enable, max_blocks=max_blocks)
