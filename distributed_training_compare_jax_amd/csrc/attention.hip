@@ -55,6 +55,16 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 // raw v_exp_f32 (softmax arguments are <= 0: no overflow range handling needed; the libm exp2f
 // wraps every call in ldexp/compare/select denormal scaffolding)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// max / sum of x over the lane pair (l, l ^ 32): one v_permlane32_swap (a VALU op) instead of the
+// ds_bpermute round trip + address arithmetic __shfl_xor(x, 32) compiles to
+__device__ __forceinline__ float pair_max32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 // stage a [rows][HD] tile (rows starting at token t0) of slot `which` (0 q, 1 k, 2 v) into LDS [rows][ld]
 template <int HD, int ROWS>
@@ -939,7 +949,7 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __
       mt1 = fmaxf(mt1, sc[1][i]);
     }
     float mt = fmaxf(mt0, mt1);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * cs;
+    mt = pair_max32(mt) * cs;
     if (__builtin_amdgcn_ballot_w64(mt > m + FW_THR) != 0) {
       const float mn = mt > m + FW_THR ? mt : m;
       const float alpha = fast_exp2(m - mn);
@@ -1001,8 +1011,7 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __
     if (it + 2 < nkt) store(ra, 0);
     __syncthreads();
   }
-  float l = l0 + l1;
-  l += __shfl_xor(l, 32, 64);
+  const float l = pair_sum32(l0 + l1);
   if (q < T) {
     const float inv = 1.f / l;
     bf16* orow = o + ((long)b * T + q) * H * HD + h * HD;
@@ -1056,11 +1065,12 @@ struct SwStage {
       x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((long)(t0 + r) * sx + 8 * ch) * 2), 0, 0));
       y[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, (int)(((long)(t0 + r) * sy + 8 * ch) * 2), 0, 0));
     }
-    if (VEC && tid < 32) {
+    if (VEC && tid < 32) {  // va (lse) in log2 units: the consumer's exponent is one fma
       const float* src = tid < 16 ? va : vb;
       const int r = 4 * (tid & 15), t = t0 + r;
       if (t + 4 <= T) v = *(const f32x4*)(src + t);
       else for (int e = 0; e < 4; ++e) v[e] = t + e < T ? src[t + e] : 0.f;
+      if (tid < 16) v *= LOG2E;
     }
   }
   __device__ __forceinline__ void store(bf16* lx, bf16* ly, float* lv, int tid) const {
@@ -1241,10 +1251,11 @@ __device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qk
 #pragma unroll
   for (int i = 0; i < HB; ++i) dk[i] = dv[i] = f32x16{};
   const int qt0 = kblk * FW_QROWS / 64;  // first 64-query tile (queries >= the block's keys)
-  // one 32-query block; MASK (causal, key <= query) only where the block straddles the wave's keys.
+  // one 32-query block; the causal mask (key <= query) only where the block straddles the wave's keys,
+  // under a wave-uniform branch inside ONE body (as the forward / dQ: no second register assignment).
   // Queries >= T need no mask: their Q / dO rows load as zeros (buffer range) and lse / delta as 0, so
   // they add nothing to dK / dV; keys >= T are never written.
-  auto qblock = [&](const bf16* sQ, const bf16* sD, const float* sv, int k2, int qs, auto MASK) {
+  auto qblock = [&](const bf16* sQ, const bf16* sD, const float* sv, int k2, int qs, bool diag) {
     f32x16 sc = f32x16{}, dp = f32x16{};
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
@@ -1260,12 +1271,16 @@ __device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qk
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int i = 4 * g4 + e;
-        float pv = fast_exp2(fmaf(sc[i], cs, -l4[e] * LOG2E));
-        if constexpr (decltype(MASK)::value) pv = (8 * g4 + e >= lim) ? pv : 0.f;
-        sc[i] = pv;
-        ds[i] = pv * (dp[i] - d4[e]);
+        sc[i] = fast_exp2(fmaf(sc[i], cs, -l4[e]));
+        ds[i] = dp[i] - d4[e];
       }
     }
+    if (diag) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[i] = ((i & 3) + 8 * (i >> 2) >= lim) ? sc[i] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ds[i] *= sc[i];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb = pack8(sc, s2), dsb = pack8(ds, s2);
@@ -1283,10 +1298,7 @@ __device__ __forceinline__ void dkdv32_body(int bid, const bf16* __restrict__ qk
     for (int k2 = 0; k2 < 2; ++k2) {
       const int qs = qb + 32 * k2;
       if (qs + 31 < k0w || qs >= T) continue;  // wave-uniform
-      // one (masked) instantiation: a second, unmasked one pushes the kernel past 256 VGPRs at 2 waves /
-      // SIMD (59 spilled; measured 101 vs 85 us at 1 wave / SIMD, profiles/r4_attn32_ab.log).  Off the
-      // diagonal lim <= 0, so the compare keeps every element.
-      qblock(sQ, sD, sv, k2, qs, std::true_type{});
+      qblock(sQ, sD, sv, k2, qs, qs < k0w + 31);  // wave-uniform: some query of the block precedes a key
     }
   };
   const int nqt = (T - qt0 * 64 + 63) / 64;

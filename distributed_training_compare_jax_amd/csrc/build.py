@@ -35,6 +35,7 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-munsafe-fp-at
 DEBUG_FLAGS = ["-O1", "-g", "-DDTC_DEBUG", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
                "-Wno-unused-result"]
 DEBUG_OUT = os.path.join(PKG, "_dtc_kernels_debug.so")
+FILE_FLAGS = {}  # per-file extra hipcc options (basename -> list)
 STATUS = {"kernels": None, "host": None}  # "compiled" | "reused" after build()
 
 
@@ -89,7 +90,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool
     bdir = os.path.join(BUILD, "debug") if debug else BUILD
     os.makedirs(bdir, exist_ok=True)
     stamp = os.path.join(bdir, "stamp" + tag)
-    dig = _digest(srcs + hdrs, flags)
+    dig = _digest(srcs + hdrs, flags + [f"{k}:{' '.join(v)}" for k, v in sorted(FILE_FLAGS.items())])
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == dig:
         STATUS["kernels"] = "reused"
         return out
@@ -97,7 +98,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool
 
     def comp(src):
         obj = os.path.join(bdir, os.path.basename(src).replace(".hip", ".o"))
-        cmd = [cc, *flags, "-I", HERE, "-c", src, "-o", obj]
+        cmd = [cc, *flags, *FILE_FLAGS.get(os.path.basename(src), []), "-I", HERE, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
