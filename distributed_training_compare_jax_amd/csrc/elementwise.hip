@@ -27,28 +27,45 @@ __device__ __forceinline__ uint32_t drop_threshold(float p) {
 }
 
 // h[tok, d..d+3] = dropout(wte[id] + wpe[t])  — one thread per 4 channels (one Philox call)
-__global__ void embed_fwd_kernel(const int* __restrict__ ids, const float* __restrict__ wte, const float* __restrict__ wpe,
-                                 float* __restrict__ h, int B, int T, int D, float p, uint32_t seed,
-                                 const int64_t* __restrict__ step, long row0) {
+// One wave per token row (a block = 4 rows): the id is one wave-uniform load, and each lane keeps all of
+// its row's wte / wpe vectors in flight before the dropout and the stores (one thread per 4 channels
+// waited on the id load, then on the row load: 17 us for 8192 x 768).  Same Philox element mapping.
+__global__ void __launch_bounds__(256) embed_fwd_kernel(const int* __restrict__ ids, const float* __restrict__ wte,
+                                                        const float* __restrict__ wpe, float* __restrict__ h, int B,
+                                                        int T, int D, float p, uint32_t seed,
+                                                        const int64_t* __restrict__ step, long row0) {
+  constexpr int VPL = 4;  // f32x4 per lane per pass: rows up to 64 * 4 * 4 = 1024 channels in one pass
+  const long tok = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (tok >= (long)B * T) return;
+  const int t = (int)(tok % T);
+  const int id = __builtin_amdgcn_readfirstlane(ids[tok]);
   const int D4 = D / 4;
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)B * T * D4) return;
-  long tok = i / D4;
-  int d = (int)(i % D4) * 4;
-  int t = (int)(tok % T);
-  int id = ids[tok];
-  DTC_ASSERT(id >= 0 && t < T && d + 4 <= D);
-  f32x4 v = *(const f32x4*)(wte + (long)id * D + d) + *(const f32x4*)(wpe + (long)t * D + d);
-  if (p > 0.f) {
-    long gtok = (row0 + tok / T) * T + t;
-    uint64_t grp = ((uint64_t)gtok * D + d) >> 2;
-    u32x4 u = philox(grp, seed, (uint32_t)step[0]);
-    uint32_t thr = drop_threshold(p);
-    float sc = 1.f / (1.f - p);
+  DTC_ASSERT(id >= 0 && t < T);
+  const uint32_t thr = drop_threshold(p);
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t st = p > 0.f ? (uint32_t)step[0] : 0u;
+  const long gtok = (row0 + tok / T) * T + t;
+  for (int c0 = 0; c0 < D4; c0 += 64 * VPL) {
+    f32x4 v[VPL];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = u[r] >= thr ? v[r] * sc : 0.f;
+    for (int k = 0; k < VPL; ++k) {
+      const int c = c0 + k * 64 + lane;
+      if (c < D4) v[k] = *(const f32x4*)(wte + (long)id * D + 4 * c) + *(const f32x4*)(wpe + (long)t * D + 4 * c);
+    }
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      const int c = c0 + k * 64 + lane;
+      if (c >= D4) continue;
+      if (p > 0.f) {
+        const uint64_t grp = ((uint64_t)gtok * D + 4 * c) >> 2;
+        const u32x4 u = philox(grp, seed, st);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[k][r] = u[r] >= thr ? v[k][r] * sc : 0.f;
+      }
+      *(f32x4*)(h + tok * D + 4 * c) = v[k];
+    }
   }
-  *(f32x4*)(h + tok * D + d) = v;
 }
 
 // ---------------------------------------------------------------- embedding backward
@@ -711,9 +728,8 @@ int dtc_version() { return 1; }
 int dtc_embed_fwd(const int* ids, const float* wte, const float* wpe, float* h, int B, int T, int D, int V, float p,
                   long seed, const int64_t* step, long row0, hipStream_t st) {
   if (D % 4) return 3001;
-  long n = (long)B * T * (D / 4);
-  hipLaunchKernelGGL(embed_fwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ids, wte, wpe, h, B, T, D, p,
-                     (uint32_t)seed, step, row0);
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(blocks_for((long)B * T, 4)), dim3(256), 0, st, ids, wte, wpe, h, B, T, D,
+                     p, (uint32_t)seed, step, row0);
   DTC_CHECK_LAUNCH();
   return 0;
 }

@@ -173,8 +173,9 @@ def test_add_layernorm(cuda, D):
     assert torch.equal(y, y0) and torch.equal(mu, mu0) and torch.equal(rs, rs0)
 
 
-def test_embedding_dropout_bits(cuda):
-    B, T, D, V = 4, 64, 128, 1000
+@pytest.mark.parametrize("D", [128, 768, 1280])
+def test_embedding_dropout_bits(cuda, D):
+    B, T, V = 4, 64, 1000
     ids = torch.randint(0, V, (B, T), dtype=torch.int32)
     wte = _r(V, D, dtype=torch.float32, seed=17)
     wpe = _r(T, D, dtype=torch.float32, seed=18)
