@@ -54,7 +54,7 @@ struct WgEntry {
   float* cs;
   int M, N;
   int tile0;  // first logical tile (filled by the host entry point)
-  int pad;
+  int nfast;  // tile order (host-set): 0 = M-tiles fastest, 1 = N-tiles fastest (see dtc_wgrad_group)
 };
 constexpr int WG_MAX = 64;
 struct WgBatch {

@@ -1664,9 +1664,9 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
   DTC_ASSERT(lid < b.ntiles);
   const WgEntry& w = wg_entry(b, lid);
   const int t = lid - w.tile0;
-  const int tiles_m = (w.M + BIG - 1) / BIG;
-  const int tm_idx = t % tiles_m, tn_idx = t / tiles_m;
-  DTC_ASSERT(tn_idx * BIG < w.N);
+  const int tiles_m = (w.M + BIG - 1) / BIG, tiles_n = (w.N + BIG - 1) / BIG;
+  const int tm_idx = w.nfast ? t / tiles_n : t % tiles_m, tn_idx = w.nfast ? t % tiles_n : t / tiles_m;
+  DTC_ASSERT(tn_idx * BIG < w.N && tm_idx * BIG < w.M);
   Epi e{};
   e.M = w.M; e.N = w.N; e.C = w.C; e.ldc = w.N; e.alpha = 1.f; e.beta = b.beta;
   if (lid >= nmain) {  // K-piece z of a tail tile (no bias column sums there: host-checked)
@@ -1692,8 +1692,8 @@ __global__ void __launch_bounds__(1024) wg_tail_reduce(WgBatch b) {
   const int lid = nmain + tt;
   const WgEntry& w = wg_entry(b, lid);
   const int t = lid - w.tile0;
-  const int tiles_m = (w.M + BIG - 1) / BIG;
-  const int m0 = (t % tiles_m) * BIG, n0 = (t / tiles_m) * BIG;
+  const int tiles_m = (w.M + BIG - 1) / BIG, tiles_n = (w.N + BIG - 1) / BIG;
+  const int m0 = (w.nfast ? t / tiles_n : t % tiles_m) * BIG, n0 = (w.nfast ? t % tiles_n : t / tiles_m) * BIG;
   const float* slab = b.tail_slab + (long)tt * b.tail_split * BIG * BIG;
   float ss = 0.f;
   constexpr int IT = 32 * 64 / 1024;  // float4 per thread, all loads of a slab issued before any add
@@ -3328,6 +3328,13 @@ int dtc_wgrad_group(const WgBatch* in, hipStream_t st) {
     DTC_HOST_CHECK(((unsigned long)w.A % 16) == 0 && ((unsigned long)w.B % 16) == 0 && ((unsigned long)w.C % 16) == 0);
     w.tile0 = t;
     t += ((w.M + BIG - 1) / BIG) * ((w.N + BIG - 1) / BIG);
+    // tile order.  M-tiles fastest (default): the blocks an XCD runs together share one N-panel of X and
+    // each streams its own dY panel, so a problem's dY is read once per N-tile.  A dY far larger than the
+    // Infinity Cache with few N-tiles (the lm_head: 824 MB, 3 N-tiles) is then fetched from HBM 3 times;
+    // N-tiles fastest co-schedules a vocab block's N-tiles on one XCD so its dY panel is read once (the
+    // small X panels stay cache-resident).  DTC_WG_NFAST=0 keeps M-fastest everywhere.
+    static const bool nfast_on = [] { const char* v = getenv("DTC_WG_NFAST"); return !v || atoi(v) != 0; }();
+    w.nfast = nfast_on && w.M > 4 * w.N && (long)b.K * w.M * 2 > (128L << 20);
   }
   b.ntiles = t;
   // tail split: the last (t mod CUs) tiles as K-pieces when every one of them belongs to a problem without

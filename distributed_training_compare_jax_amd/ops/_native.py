@@ -81,7 +81,7 @@ class WgEntry(ctypes.Structure):
     """Mirror of ``struct WgEntry`` in csrc/common.h: one problem of a grouped weight-gradient launch."""
 
     _fields_ = [("A", c_vp), ("B", c_vp), ("C", c_vp), ("cs", c_vp), ("M", c_int), ("N", c_int),
-                ("tile0", c_int), ("pad", c_int)]
+                ("tile0", c_int), ("nfast", c_int)]
 
 
 WG_MAX = 64  # csrc/common.h WG_MAX
