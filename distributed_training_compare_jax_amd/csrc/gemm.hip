@@ -3328,13 +3328,14 @@ int dtc_wgrad_group(const WgBatch* in, hipStream_t st) {
     DTC_HOST_CHECK(((unsigned long)w.A % 16) == 0 && ((unsigned long)w.B % 16) == 0 && ((unsigned long)w.C % 16) == 0);
     w.tile0 = t;
     t += ((w.M + BIG - 1) / BIG) * ((w.N + BIG - 1) / BIG);
-    // tile order.  M-tiles fastest (default): the blocks an XCD runs together share one N-panel of X and
-    // each streams its own dY panel, so a problem's dY is read once per N-tile.  A dY far larger than the
-    // Infinity Cache with few N-tiles (the lm_head: 824 MB, 3 N-tiles) is then fetched from HBM 3 times;
-    // N-tiles fastest co-schedules a vocab block's N-tiles on one XCD so its dY panel is read once (the
-    // small X panels stay cache-resident).  DTC_WG_NFAST=0 keeps M-fastest everywhere.
+    // tile order.  M-tiles fastest: the blocks an XCD runs together share one N-panel of X and each
+    // streams its own dY panel, so a problem's dY is read once per N-tile -- for the lm_head (dY 824 MB,
+    // 3 N-tiles) 3 times from HBM.  N-tiles fastest co-schedules an M-block's N-tiles on one XCD, so the
+    // larger operand dY is read once and the smaller X panels are the re-read ones: used when M >= 2N
+    // (the lm_head: -60 us/step, profiles/r5_wg_nfast_ab.log; also qkv / fc1: a further -15 us,
+    // r5_wg_nfast2_ab.log).  DTC_WG_NFAST=0 keeps M-fastest everywhere.
     static const bool nfast_on = [] { const char* v = getenv("DTC_WG_NFAST"); return !v || atoi(v) != 0; }();
-    w.nfast = nfast_on && w.M > 4 * w.N && (long)b.K * w.M * 2 > (128L << 20);
+    w.nfast = nfast_on && w.M >= 2 * w.N;
   }
   b.ntiles = t;
   // tail split: the last (t mod CUs) tiles as K-pieces when every one of them belongs to a problem without
