@@ -12,7 +12,7 @@ Derived columns (gfx950, 256 CUs x 4 SIMDs, 2.4 GHz):
   dispatches, so they are slightly longer than in the free-running step).
 * Last column: the raw ratio of the two SQ counters (extra conflict cycles over LDS-instruction
   issue cycles; different units, so a relative indicator between kernels, not a percentage).
-One step = the dispatches after the second-to-last ``adamw_kernel`` up to the last one.
+One step = the dispatches after the second-to-last ``adamw_kernel`` / ``adamw_seg_kernel`` up to the last one.
 """
 
 import argparse
@@ -35,7 +35,7 @@ def load(d):
 
 def last_step(x):
     disp = x.drop_duplicates("Dispatch_Id").sort_values("Dispatch_Id")
-    ad = disp[disp.Kernel_Name.str.contains("adamw_kernel")].Dispatch_Id.tolist()
+    ad = disp[disp.Kernel_Name.str.contains("adamw_seg_kernel|adamw_kernel", regex=True)].Dispatch_Id.tolist()
     lo, hi = ad[-2], ad[-1]
     return x[(x.Dispatch_Id > lo) & (x.Dispatch_Id <= hi)]
 
