@@ -14,11 +14,17 @@ GPT-2 small that comparator is conservative: GPT-2 small costs ~2.8x the FLOPs p
 reference model (854 M vs 302 M FLOP/token, fwd+bwd), so its tokens/s would be lower on the
 reference's own hardware.  The JSON names the comparator (``baseline_comparator``).
 
-Each timed step does exactly what the reference's timed loop does (``train/train.py:75-85``):
-next host batch → H2D → full forward + backward + gradient all-reduce + clip + AdamW →
-blocking loss read.  W untimed warmup steps first (the first one eager, then hipGraph
-capture), then K steps bracketed by barrier + device sync on both sides; the MAX over
-ranks is reported.  ``value`` is whole-job tokens/s.
+Timed span.  W untimed warmup steps first (the first one eager, then hipGraph capture), then TWO
+timed loops of K steps, each bracketed by barrier + device sync on both sides, MAX over ranks:
+
+* **blocking** -- ``value`` / ``ms_per_step``: the reference's timed loop (``train/train.py:75-85``)
+  step for step: next host batch -> H2D -> full forward + backward + gradient collectives + clip +
+  AdamW -> blocking read of THIS step's loss before the next step is issued;
+* **pipelined** -- ``ms_per_step_pipelined``: the same steps, but step i's loss is read after step
+  i+1 is enqueued (the host never leaves the GPU idle between steps; every loss is still read).
+
+``value`` is whole-job tokens/s of the blocking loop.  ``tflops_per_gpu`` counts the causal
+attention's useful FLOPs (``ModelConfig.flops_per_token``).
 
 Scaling: ``dp`` keeps 8 sequences per GPU (weak scaling, global batch 8·N); ``tp`` and
 ``pp`` keep the reference global batch of 8 (strong scaling; pp uses 2·N microbatches).
@@ -75,7 +81,9 @@ def main():
     ap.add_argument("--model", default=DEFAULT_MODEL)
     ap.add_argument("--batch_per_gpu", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
-    ap.add_argument("--pp_schedule", default="1f1b")
+    # zb + the auto head split: the schedule the pp8 estimate ranks best (profiles/r5_pp8_estimate.md:
+    # 2.42 ms vs 3.09-3.58 for 1F1B); the JSON reports which schedule and split ran
+    ap.add_argument("--pp_schedule", default="zb", choices=["gpipe", "1f1b", "zb"])
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra TrainConfig overrides for A/B runs, e.g. --set defer_optimizer=false")
     args = ap.parse_args()
@@ -120,27 +128,33 @@ def main():
         eng.run_step()
         eng.loss_value()
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    batch = next(data)
-    loss = float("nan")
-    pending = None
-    for i in range(args.steps):
-        # enqueue step i (H2D batch copy + graph replay), then read step i-1's loss: the host never
-        # leaves the GPU idle between steps, and every step's loss is still read
-        eng.set_batch(batch)
-        eng.run_step()
-        handle = eng.loss_handle()
+    def timed(pipelined: bool):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         batch = next(data)
+        loss = float("nan")
+        pending = None
+        for i in range(args.steps):
+            eng.set_batch(batch)
+            eng.run_step()
+            handle = eng.loss_handle()
+            batch = next(data)
+            if not pipelined:  # the reference: block on this step's loss before the next step
+                loss = eng.read_loss(handle)
+                continue
+            if pending is not None:  # step i-1's loss, read with step i already enqueued
+                loss = eng.read_loss(pending)
+            pending = handle
         if pending is not None:
             loss = eng.read_loss(pending)
-        pending = handle
-    loss = eng.read_loss(pending)
-    eng.flush_optimizer()  # the last step's deferred AdamW lands inside the timed region
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
+        eng.flush_optimizer()  # a deferred last AdamW lands inside the timed region
+        torch.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0, loss
+
+    dt_pipe, _ = timed(True)
+    dt, loss = timed(False)
     healthy = 1.0
     try:  # device-side wait timeouts (P2P flags, fused LayerNorm statistics): the timed steps computed NaN
         eng.check_health()
@@ -148,9 +162,9 @@ def main():
         healthy = 0.0
         print(f"[rank {dinfo.rank}] ERROR: {exc}", file=sys.stderr, flush=True)
     if world > 1:
-        t = torch.tensor([dt, -healthy], device=dinfo.device, dtype=torch.float64)
+        t = torch.tensor([dt, dt_pipe, -healthy], device=dinfo.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, healthy = float(t[0].item()), -float(t[1].item())
+        dt, dt_pipe, healthy = float(t[0].item()), float(t[1].item()), -float(t[2].item())
     if not (loss == loss):
         healthy = 0.0
     ms = 1e3 * dt / args.steps
@@ -172,6 +186,7 @@ def main():
         out = {
             "metric": metric, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": scaling,
+            "ms_per_step_pipelined": round(1e3 * dt_pipe / args.steps, 4), "timed_span": "blocking per-step loss read",
             "vs_baseline": round(value / base, 3) if base else None, "dtype": tc.dtype,
             "data": "synthetic (FineWeb-shaped token stream, random-init weights)",
             "healthy": bool(healthy),
@@ -179,8 +194,12 @@ def main():
                                 f"T{mc.max_seq_len} V{mc.vocab_size})",
                        "global_batch": global_batch, "seq_len": mc.max_seq_len, "parallelism": par,
                        "pp_microbatches": micro if args.parallel == "pp" else None,
+                       "pp_schedule": args.pp_schedule if args.parallel == "pp" else None,
+                       "pp_head_split": eng.pp_head_split if args.parallel == "pp" else None,
+                       "capture_comms": eng.program.capture_comms,
                        "hipgraph": eng.program.use_graph, "final_loss": round(loss, 4),
                        "tflops_per_gpu": round(mc.flops_per_token() * tokens / (ms / 1e3) / world / 1e12, 1),
+                       "flops_count": "causal attention (useful work)",
                        "backend": dinfo.backend, "world_size": dist.get_world_size() if dist.is_initialized() else 1,
                        "tp_comm": tp_path, "rccl_version": rccl,
                        "graph_segments": eng.program.n_graphs, "eager_collectives": eng.program.n_comms,

@@ -83,11 +83,14 @@ class ModelConfig:
         per_layer = 4 * D * D + 4 * D + D * F + F + F * D + D + 4 * D
         return V * D + T * D + L * per_layer + 2 * D + D * V + V
 
-    def flops_per_token(self) -> float:
-        """Matmul FLOPs per token, fwd+bwd (6*N_matmul + attention), as SURVEY §2.4."""
+    def flops_per_token(self, causal: bool = True) -> float:
+        """Matmul FLOPs per token, fwd+bwd: 6 * N_matmul + attention.  ``causal`` (default): the useful
+        work of the causal attention, (T + 1) / 2 keys per query on average; ``causal=False``: the full
+        T x T count SURVEY §2.4 / BASELINE.md's 1.715 TFLOP/step estimate use."""
         D, F, V, T, L = self.d_model, self.d_ff, self.vocab_size, self.max_seq_len, self.n_layers
         mm = L * (4 * D * D + 2 * D * F) + D * V
-        attn = L * 2 * T * D  # QK^T + PV per token (full, non-causal count as the survey)
+        keys = (T + 1) / 2.0 if causal else float(T)
+        attn = L * 2 * keys * D  # QK^T + PV multiply-adds per token
         return 6.0 * mm + 3.0 * 2.0 * attn
 
 
@@ -160,9 +163,10 @@ class TrainConfig:
     # The one-GPU box uses it to execute the exact RCCL call sequence of a DP step (tests/test_rccl_gpu.py)
     dp_comm_rehearsal: bool = False
     # capture the step's collectives INTO its hipGraph (one graph per step) instead of cutting the graph at
-    # each collective and issuing it eagerly between segments (parallel/program.py).  None = auto: on for an
-    # RCCL process group (DTC_CAPTURE_COMMS=0 turns it off), off for gloo.  GPT-2 small, one-rank RCCL
-    # rehearsal of the DP path: 11.39-11.41 ms/step captured vs 11.62-11.64 cut (profiles/r5_rccl_rehearsal.md)
+    # each collective and issuing it eagerly between segments (parallel/program.py).  None = auto: on for a
+    # ONE-rank RCCL process group (the rehearsal, where it was measured: 11.39-11.41 ms/step captured vs
+    # 11.62-11.64 cut, profiles/r5_rccl_rehearsal.md), off at world > 1 until capture has run against real
+    # peers (docs/CAPTURE.md), off for gloo; DTC_CAPTURE_COMMS=1 / 0 force it
     capture_comms: Optional[bool] = None
     device: str = "auto"  # auto | cuda | cpu
     batch_is_global: bool = True  # reference: `batch` is the global batch

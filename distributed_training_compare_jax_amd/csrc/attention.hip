@@ -2095,7 +2095,7 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
 long dtc_attn_bwd_workspace_bytes(int B, int T, int H, int HD) { return (long)B * H * T * 4; }
 
 int dtc_attn_bwd(const bf16* qkv, const bf16* o, const float* lse, const bf16* dout, bf16* dqkv, int flags, int B,
-                 int T, int H, int HD, long unused, float scale, float* ws, long ws_bytes, hipStream_t st) {
+                 int T, int H, int HD, float scale, float* ws, long ws_bytes, hipStream_t st) {
   if (ws_bytes < dtc_attn_bwd_workspace_bytes(B, T, H, HD)) return 4002;
   int nb = (T + 63) / 64;
   dim3 grid(B * H * nb);

@@ -155,7 +155,7 @@ def _declare(lib):
         "dtc_embed_sort": ([vp, i, i, vp, vp], i),
         "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp], i),
         "dtc_attn_fwd": ([vp, vp, vp, i, i, i, i, l, f, vp], i),
-        "dtc_attn_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, i, l, f, vp, l, vp], i),
+        "dtc_attn_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, i, f, vp, l, vp], i),
         "dtc_attn_bwd_workspace_bytes": ([i, i, i, i], l),
         "dtc_ce_combine": ([vp, i, i, l, l, vp, vp, vp, f, vp, i, vp], i),
         "dtc_ce_bwd": ([vp, l, vp, vp, i, i, i, i, f, vp, vp], i),

@@ -15,7 +15,6 @@ in place with strides and writes ``o[B, T, H, hd]`` which is directly the out_pr
 
 from __future__ import annotations
 
-import math
 
 import torch
 
@@ -85,7 +84,7 @@ def attn_bwd(qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, do: torch.Te
         return dqkv
     ws = _workspace(qkv.device, int(L.dtc_attn_bwd_workspace_bytes(B, T, n_heads, hd)))
     N.check(L.dtc_attn_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), int(flags),
-                           B, T, n_heads, hd, int(flags), scale, ws.data_ptr(), ws.numel() * ws.element_size(),
+                           B, T, n_heads, hd, scale, ws.data_ptr(), ws.numel() * ws.element_size(),
                            N.stream_ptr(qkv.device)),
             "dtc_attn_bwd")
     return dqkv
@@ -95,5 +94,3 @@ def attn_flops(B: int, T: int, H: int, hd: int, causal: bool = True) -> float:
     f = 4.0 * B * H * T * T * hd
     return f / 2 if causal else f
 
-
-_ = math

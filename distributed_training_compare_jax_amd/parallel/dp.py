@@ -8,9 +8,10 @@ all-reduce is issued (async, on RCCL's stream) and the next backward segment run
 it; the step waits on all buckets only before the optimizer.
 
 Bucket size is chosen for xGMI, not NVSwitch: a ring all-reduce on the 8×MI355X mesh is
-per-link bound (~150 GB/s/link), so buckets are kept large (default 64 MB, a few per
-step: enough to saturate RCCL's multi-channel rings, few enough that per-call latency
-is noise).  Loss scaling makes the SUM equal the global-mean gradient (no extra pass).
+per-link bound (~150 GB/s/link), so buckets are kept large (``dp_bucket_mb``, default 40 MB,
+cut at layer boundaries, with a 16 MB ``dp_tail_mb`` last bucket because its all-reduce is
+exposed: enough to saturate RCCL's multi-channel rings, few enough that per-call latency is
+noise).  Loss scaling makes the SUM equal the global-mean gradient (no extra pass).
 """
 
 from __future__ import annotations
@@ -47,7 +48,7 @@ class GradBuckets:
     ``boundaries``: offsets where grads become final together (the head's and each layer's end,
     in backward order).  Buckets then end only there, so each is issued the moment its last layer
     is done; cut at arbitrary param boundaries, a bucket straddling two layers waits for the later
-    one (for the reference model the second-to-last 64 MB bucket used to wait for the END of
+    one (for the reference model the second-to-last large bucket used to wait for the END of
     backward, its all-reduce fully exposed)."""
 
     def __init__(self, flat: FlatParams, group, dp: int, program, bucket_mb: float = 64.0, tail_mb: float = 16.0,
@@ -180,9 +181,12 @@ class GradBuckets:
             ev.record(self._cs)
             return _StreamJoin(ev)
 
-        # not captured under capture_comms: the bf16 chain (side-stream fork + all_to_all_single) crashed the
-        # one-rank RCCL rehearsal inside a hipGraph capture (segfault, tests/test_rccl_gpu.py); it stays an
-        # eager item between segments
+        # NEVER captured (capture_comms or not): the chain issues its collectives from a side stream forked into
+        # the capture, and an RCCL collective issued from a forked stream segfaults inside hipStreamEndCapture
+        # (torch 2.10 / ROCm 7.0 / RCCL 2.26.6; minimal repro benchmarks/capture_side_stream_probe.py: the same
+        # all_to_all_single from the capture's origin stream records and replays fine, from a stream joined by
+        # wait_stream it crashes at capture_end; in the engine the PG watchdog then also trips over the event
+        # recorded in the capturing stream).  It stays an eager item between graph segments.
         self.program.comm(fn, name=f"dp_bucket{i}", sig=csig("all_to_all", g, send) + csig("all_gather", g, red),
                           capturable=False)
 

@@ -282,10 +282,32 @@ def timeline(progs: List[List[tuple]], costs: List[Dict[str, float]], comm: floa
             raise RuntimeError("timeline: deadlock")
 
 
+def w_cap(S: int, s: int) -> int:
+    """Most W's stage s may hold pending (each keeps its microbatch's weight-gradient operands, dY and X,
+    alive): S, the number of microbatches 1F1B keeps in flight on its first stage -- ZB-H1's bound, which
+    keeps every stage's peak within 1F1B's peak stage (a pending W holds less than an in-flight
+    microbatch's activations).  A tighter per-stage S - s costs the 8 x 8 replay 19 % (10.3 -> 12.3)."""
+    return max(1, S)
+
+
+def max_pending_w(prog: List[tuple]) -> int:
+    """Largest number of microbatches whose B has run and whose W has not, over a stage program."""
+    pend = peak = 0
+    for it in prog:
+        if it[0] == "B":
+            pend += 1
+            peak = max(peak, pend)
+        elif it[0] == "W":
+            pend -= 1
+    return peak
+
+
 def _place_w(progs, base, s, costs, comm, M):
     """Stage s's program with its W's moved out of the steady state into the idle gaps the timed replay
-    shows (the other stages as in ``progs``), the ones that fit nowhere at the end."""
+    shows (the other stages as in ``progs``), the ones that fit nowhere at the end -- but never more than
+    :func:`w_cap` pending: a B that would exceed it runs the oldest pending W right after itself."""
     prog = base[s]
+    cap = w_cap(len(progs), s)
     trial = list(progs)
     trial[s] = prog + [("W", i) for i in range(M)]
     tl = timeline(trial, costs, comm)
@@ -295,6 +317,10 @@ def _place_w(progs, base, s, costs, comm, M):
     out: List[tuple] = []
     delay = 0.0  # how far the W's placed so far pushed this stage's clock past the replay's
     for idx, it in enumerate(prog):
+        if it[0] != "post":  # over the cap: the oldest W's run now, after the B's own message posts
+            while len(ws) >= cap:
+                out.append(("W", ws.pop(0)))
+                delay += wcost
         if it[0] == "wait" and idx in gap_at:
             t0, t1 = gap_at[idx]
             room = (t1 - t0) - delay
@@ -318,7 +344,9 @@ def zb_programs(S: int, M: int, costs=None, comm: float = 0.0, head_split: bool 
     timed replay (:func:`_place_w`).  The placement depends on the order the stages are visited in (a
     placed W changes when its stage posts later messages): first-to-last, last-to-first and a second
     pass of each are tried and the programs with the shortest replayed makespan are kept.  Memory stays
-    1F1B's: a W never moves before its own B, and its B already holds the activations it reads."""
+    within 1F1B's peak: a W never moves before its own B, and at most ``w_cap(S, s)`` = S W's (their dY / X
+    operands) are pending on any stage at any time -- the number of microbatches 1F1B keeps in flight on
+    its first stage (``tests/test_pp_schedule_cpu.py`` checks it for S up to 8 and M up to 32)."""
     costs = stage_item_costs(S) if costs is None else costs
     base = [pp_program("1f1b", S, s, M, head_split=head_split) for s in range(S)]
     inline = [[x for it in b for x in ((it, ("W", it[1])) if it[0] == "B" else (it,))] for b in base]

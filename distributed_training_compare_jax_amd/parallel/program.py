@@ -2,13 +2,14 @@
 
 The reference jit-compiles the whole step into one XLA program
 (``train/create_train_step.py:28-50``) so the host issues one call per step.  The MI355X
-analog is to capture the step's kernel stream into hipGraphs.  Collectives are kept OUT
-of the graphs on purpose: RCCL calls are issued eagerly between graph segments on the
-same stream order, which
+analog is to capture the step's kernel stream into hipGraphs.  Collectives have two modes
+(``TrainConfig.capture_comms``, decision and evidence in ``docs/CAPTURE.md``):
 
-* lets a DP gradient bucket's all-reduce run on RCCL's own stream while the NEXT backward
-  segment replays (overlap without capturing RCCL),
-* keeps PP send/recv and TP all-reduces on the well-trodden eager RCCL path.
+* **cut** (the default at world > 1): each collective cuts the graph and is issued eagerly
+  between segments in stream order -- a DP bucket's all-reduce runs on RCCL's own stream while
+  the NEXT backward segment replays, PP send/recv and TP RCCL calls stay on the eager path;
+* **captured** (the default on a one-rank RCCL group, ``DTC_CAPTURE_COMMS=1`` anywhere): RCCL's
+  kernels become nodes of the one step graph (below).
 
 ``record(step_fn)`` runs ``step_fn`` once with capture on; every ``comm(fn)`` call the
 step makes cuts the current graph, stores ``fn`` WITHOUT running it (the recording pass

@@ -164,6 +164,11 @@ class Engine:
             wg = 0 if not self.dp_comm else 2
             if wg == 0:
                 wg = self._wgrad_group_for_memory(model_cfg, len(self.layout.layers))
+        if pp > 1 and train_cfg.pp_schedule == "zb" and wg < 0:
+            # the zero-bubble schedule runs each microbatch's weight gradients (W) apart from its
+            # input-gradient chain (B): that needs the deferred grouped path.  Refused here, before any
+            # collective, instead of inside the first backward (where only some ranks would raise)
+            raise ValueError("pp_schedule='zb' needs deferred weight gradients: wgrad_group >= 0 (or unset)")
         self.stage.set_wgrad_group(wg)
         # DP embedding-grad gather (pp == 1): instead of all-reducing the dense wte/wpe grads
         # (103 MB fp32 for the reference vocab, issued last -> fully exposed), all-gather the

@@ -152,8 +152,8 @@ def load_into(eng, output_dir: str, step: int):
         for k, have in (("params", f.params), ("exp_avg", f.exp_avg), ("exp_avg_sq", f.exp_avg_sq)):
             if st[k].shape != have.shape:
                 raise ValueError(f"checkpoint {k} has {st[k].numel()} elements, this rank holds {have.numel()}")
-    except (ValueError, FileNotFoundError, KeyError) as e:
-        err = e
+    except Exception as e:  # noqa: BLE001 -- any failure (corrupt / truncated zip, unpickling refused,
+        err = e             # permission) must still reach the agreement collective on this rank
     _agree(err is None, err, f.device)
     f.params.copy_(st["params"].to(f.device))
     f.exp_avg.copy_(st["exp_avg"].to(f.device))

@@ -152,3 +152,47 @@ def test_replicated_checkpoint_resumes_at_larger_dp(tmp_path):
     spawn(_dp_resume_worker, 2, args=(out, str(tmp_path)))
     part2 = torch.load(str(tmp_path / "hist_dp2.pt"))
     assert part2 == pytest.approx(full[3:], rel=1e-4, abs=1e-4)
+
+
+def _corrupt_worker(out, res_dir):
+    from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
+
+    torch.set_num_threads(1)
+    d = init_distributed("cpu")
+    eng = train(TrainConfig(seed=0, parallel="dp", batch=4, steps=0, log_every=1000, output_dir=out + "_fresh",
+                            device="cpu", warmup_steps=0, zero_stage=1), MC, OC, d, quiet=True)["engine"]
+    try:
+        C.load_into(eng, out, 2)
+        msg = "loaded"
+    except Exception as e:  # noqa: BLE001
+        msg = f"{type(e).__name__}: {e}"
+    with open(os.path.join(res_dir, f"r{d.rank}.txt"), "w") as fh:
+        fh.write(msg)
+    destroy()
+
+
+def _ckpt_worker(out):
+    from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
+
+    torch.set_num_threads(1)
+    d = init_distributed("cpu")
+    train(TrainConfig(seed=0, parallel="dp", batch=4, steps=2, log_every=1000, output_dir=out, device="cpu",
+                      warmup_steps=0, ckpt_every=2, zero_stage=1), MC, OC, d, quiet=True)
+    destroy()
+
+
+@pytest.mark.slow
+def test_truncated_rank_file_fails_on_every_rank(tmp_path):
+    """One rank's file is a truncated zip (torch.load raises a RuntimeError, not a ValueError): that rank must
+    still reach the failure agreement, so both ranks raise instead of one blocking in the all-reduce."""
+    out = str(tmp_path / "z")
+    spawn(_ckpt_worker, 2, args=(out,))
+    p = os.path.join(out, "ckpt", "step_2", "rank1.pt")
+    data = open(p, "rb").read()
+    with open(p, "wb") as fh:
+        fh.write(data[: len(data) // 3])
+    spawn(_corrupt_worker, 2, args=(out, str(tmp_path)))
+    r0 = open(tmp_path / "r0.txt").read()
+    r1 = open(tmp_path / "r1.txt").read()
+    assert "another rank" in r0, r0
+    assert r1 != "loaded" and "another rank" not in r1, r1

@@ -56,3 +56,25 @@ def test_param_cut_buckets_unchanged_without_boundaries():
     b = GradBuckets(f, None, 8, _Prog(), 64.0, 16.0, local_names=("wte", "wpe"))
     assert b.buckets[0][0] == 0 and b.buckets[-1][1] == b.reduce_end
     assert sum(c - a for a, c in b.buckets) == b.reduce_end
+
+
+def test_bf16_payload_chain_is_never_captured():
+    """The bf16 payload chain issues its collectives from a side stream forked into the step; an RCCL
+    collective issued from a stream forked into a hipGraph capture segfaults at capture end (root cause:
+    benchmarks/capture_side_stream_probe.py, docs/CAPTURE.md), so the chain must always be registered as
+    a non-capturable (eager, graph-cutting) item -- and the fp32 all-reduce buckets as capturable."""
+    class Prog:
+        def __init__(self):
+            self.cap = {}
+
+        def comm(self, fn, name=None, sig=None, capturable=True):
+            self.cap[name] = capturable
+
+    f = _ref_flat()
+    ends, head = _bounds(f, range(12))
+    for payload, want in (("bf16", False), ("fp32", True)):
+        prog = Prog()
+        b = GradBuckets(f, None, 8, prog, 40.0, 16.0, local_names=("wte", "wpe"), boundaries=ends + [head],
+                        payload=payload)
+        b.ready_all()
+        assert len(prog.cap) == len(b.buckets) and all(v is want for v in prog.cap.values()), (payload, prog.cap)

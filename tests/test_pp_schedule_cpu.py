@@ -45,6 +45,19 @@ def test_zero_bubble_programs(S, M):
         assert z["bubble"] <= 0.25, z
 
 
+@pytest.mark.parametrize("head_split", [False, True])
+@pytest.mark.parametrize("S", [2, 3, 4, 8])
+def test_zero_bubble_pending_w_bounded(S, head_split):
+    """Each pending W keeps its microbatch's dY and X alive: no stage ever holds more than 1F1B's peak
+    in-flight count (S, its first stage) of them, also with many microbatches and with a heavy last stage
+    (costs that push a stage's W's into the final drain without the cap)."""
+    for M in (S, 2 * S, 4 * S, 32):
+        costs = PP.stage_item_costs(S, [1.0] * (S - 1) + [3.0])
+        for s, prog in enumerate(PP.zb_programs(S, M, costs, head_split=head_split)):
+            assert PP.max_pending_w(prog) <= PP.w_cap(S, s), (S, M, s, PP.max_pending_w(prog))
+        PP.simulate("zb", S, M, head_split=head_split)  # still deadlock-free under the cap
+
+
 def test_simulator_catches_the_ungrouped_1f1b_order(monkeypatch):
     """The round-2 executor's order (send, then an ungrouped receive from the same peer) deadlocks
     under blocking semantics as soon as S >= 2 and M >= 2: the simulator must see it."""
