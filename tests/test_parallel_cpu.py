@@ -226,3 +226,43 @@ def test_dp_comm_rehearsal_on_one_rank_group(single, kw):
         assert r["gather"] == kw.get("dp_embed_gather", True)
     tol = 2e-2 if kw.get("dp_grad_dtype") == "bf16" else 1e-5
     assert r["losses"] == pytest.approx(single[0]["losses"], rel=tol, abs=tol)
+
+
+# BASELINE.json's three 8-GPU layouts at world 8 (gloo), on a 12-layer / 12-head model so the layer split,
+# the head split and the uneven TP head split are the ones GPT-2 small gets on the node
+BASE8 = {"d_model": 96, "n_heads": 12, "d_ff": 256, "n_layers": 12}
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("parallel,world,kw,fp32", [
+    ("dp", 8, {}, True),  # config 2: pure dp8, embedding-output gather (one sequence per rank)
+    ("dp", 8, {"dp_grad_dtype": "bf16"}, False),  # config 2 with the bf16 payload chain
+    # config 4: pp8, zero-bubble schedule + lm_head/CE split over the last two stages, M = 8
+    ("pp", 8, {"pp_microbatches": 8, "pp_clip": "global", "pp_schedule": "zb", "pp_head_split": True}, True),
+    ("dp", 8, {"tp": 2, "tp_sequence_parallel": True}, True),  # config 5's mesh: dp4 x tp2 with SP
+])
+def test_baseline_8gpu_layouts_match_single_process(parallel, world, kw, fp32):
+    kw = dict(kw, model=BASE8, eps=1e-4, batch=8)
+    single = _run("dp", 1, model=BASE8, eps=1e-4, batch=8)
+    res = _run(parallel, world, **kw)
+    if parallel == "dp" and "tp" not in kw:
+        assert res[0]["mesh"] == (8, 1, 1)
+    if parallel == "pp":
+        assert res[0]["mesh"] == (1, 1, 8) and res[-1]["head_part"] == (1, 2) and res[-2]["head_part"] == (0, 2)
+    if "tp_sequence_parallel" in kw:
+        assert res[0]["mesh"] == (4, 2, 1) and all(r["sp"] for r in res)
+    tol = 1e-4 if fp32 else 1e-3
+    assert res[0]["losses"] == pytest.approx(single[0]["losses"], rel=tol, abs=tol)
+    full = _full_params(res, model=BASE8)
+    ref = single[0]["params"]
+    assert set(full) == set(ref)
+    for n in ref:
+        a, b = full[n], ref[n]
+        if fp32:
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), (n, (a - b).abs().max().item())
+        else:
+            assert ((a - b).norm() / b.norm()).item() < 2e-3, n
+    if parallel == "dp" and "tp" not in kw:  # every replica ends with the same params
+        for r in res[1:]:
+            for n in ref:
+                assert torch.equal(r["params"][n], res[0]["params"][n]), n
