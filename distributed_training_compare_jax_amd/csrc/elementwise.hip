@@ -708,14 +708,10 @@ __global__ void __launch_bounds__(256) transpose_batch_kernel(TrBatch batch) {
     bf16x8 v;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = tile[ch + e][dr];
-    // non-temporal: the transposed mirror is read only in the backward (DTC_TR_CACHED: cached stores)
-    if (c0 + dr < T.cols && r0 + ch + 8 <= T.rows) {
-#ifdef DTC_TR_CACHED
-      *(bf16x8*)(T.dst + (long)(c0 + dr) * T.rows + r0 + ch) = v;
-#else
+    // non-temporal: the transposed mirror is read only in the backward (cached stores measured slower,
+    // profiles/r2_ab_nt_transpose.log)
+    if (c0 + dr < T.cols && r0 + ch + 8 <= T.rows)
       __builtin_nontemporal_store(v, (bf16x8*)(T.dst + (long)(c0 + dr) * T.rows + r0 + ch));
-#endif
-    }
   }
 }
 

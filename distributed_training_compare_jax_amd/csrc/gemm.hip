@@ -164,14 +164,9 @@ struct Epi {
   LnEpi ln;
 };
 
-// Output stores of the GEMM epilogues.  DTC_NT_STORES: non-temporal (streamed past L2), so a
-// kernel's outputs drain to memory while other blocks still compute instead of being written back
-// from L2 at the kernel boundary.
-#ifdef DTC_NT_STORES
-#define DTC_OUT_STORE(ptr, val) __builtin_nontemporal_store((val), (ptr))
-#else
+// Output stores of the GEMM epilogues: cached (every layer-GEMM output non-temporal measured slower for
+// the outputs the next kernel reads, profiles/r2_ab_nt_stores.log; the few streamed outputs say so)
 #define DTC_OUT_STORE(ptr, val) (*(ptr) = (val))
-#endif
 
 template <int EPI, bool OUTF32>
 __device__ __forceinline__ float epilogue_store(const Epi& e, int m, int n, f32x4 v) {  // returns sum o^2 of fp32 stores
@@ -909,53 +904,30 @@ __device__ __forceinline__ void gemm_body(bf16* smem, int bid, const bf16* __res
     TA::store(ra, s0, tid);
     TB::store(rb, s0 + TA::ELEMS, tid);
     if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra);
-#ifndef DTC_WRITE_AFTER_BARRIER
-#define DTC_WRITE_AFTER_BARRIER 1
-#endif
-    if constexpr (DTC_WRITE_AFTER_BARRIER) {
-      // write-after-barrier (guide T14 as G15 writes it): tile kt+1, loaded one iteration ago, is
-      // written at the top of iteration kt (its buffer was last read before the previous barrier)
-      // and tile kt+2's loads go out right behind it, so each load has a whole compute phase AND a
-      // barrier to land instead of the compute phase alone
-      if (nk > 1) {
-        TA::load(ra, rsA, lda, m0, kbeg + BK, tid);
-        TB::load(rb, rsB, ldb, n0, kbeg + BK, tid);
-      }
-      __syncthreads();
-      for (int kt = 0; kt < nk; ++kt) {
-        bf16* cur = (kt & 1) ? s1 : s0;
-        bf16* nxt = (kt & 1) ? s0 : s1;
-        if (kt + 1 < nk) {
-          TA::store(ra, nxt, tid);
-          TB::store(rb, nxt + TA::ELEMS, tid);
-          if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra);
-          if (kt + 2 < nk) {
-            TA::load(ra, rsA, lda, m0, kbeg + (kt + 2) * BK, tid);
-            TB::load(rb, rsB, ldb, n0, kbeg + (kt + 2) * BK, tid);
-          }
-        }
-        compute(cur);
-        __syncthreads();
-      }
-    } else {
+    // write-after-barrier (guide T14 as G15 writes it): tile kt+1, loaded one iteration ago, is
+    // written at the top of iteration kt (its buffer was last read before the previous barrier)
+    // and tile kt+2's loads go out right behind it, so each load has a whole compute phase AND a
+    // barrier to land instead of the compute phase alone
+    if (nk > 1) {
+      TA::load(ra, rsA, lda, m0, kbeg + BK, tid);
+      TB::load(rb, rsB, ldb, n0, kbeg + BK, tid);
+    }
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-      const bool more = kt + 1 < nk;
       bf16* cur = (kt & 1) ? s1 : s0;
       bf16* nxt = (kt & 1) ? s0 : s1;
-      if (more) {
-        TA::load(ra, rsA, lda, m0, kbeg + (kt + 1) * BK, tid);
-        TB::load(rb, rsB, ldb, n0, kbeg + (kt + 1) * BK, tid);
-      }
-      compute(cur);
-      if (more) {
+      if (kt + 1 < nk) {
         TA::store(ra, nxt, tid);
         TB::store(rb, nxt + TA::ELEMS, tid);
         if (do_cs) colsum_acc<BM, TA::PER_THREAD>(cs, ra);
+        if (kt + 2 < nk) {
+          TA::load(ra, rsA, lda, m0, kbeg + (kt + 2) * BK, tid);
+          TB::load(rb, rsB, ldb, n0, kbeg + (kt + 2) * BK, tid);
+        }
       }
+      compute(cur);
       __syncthreads();
     }
-    }  // DTC_WRITE_AFTER_BARRIER == 0: write-before-barrier
   }
   if constexpr (!AK) {
     // do_cs is block-uniform, so the combine's barrier is reached by every thread of the block;
@@ -2803,8 +2775,6 @@ int big_split(int layout, int M, int N, int K) {
   static const int tail_ok = [] { const char* v = getenv("DTC_BIG_TAIL"); return v ? atoi(v) : 64; }();
   if (K < 16384) return (t >= min_tiles || (layout == 0 && t >= 256 && t % 256 <= tail_ok)) ? 1 : 0;
   if (t > 256) return 0;                           // dgrad through the vocab (NN, or NT on W^T): split-K
-  static const int vsplit = [] { const char* v = getenv("DTC_VOCAB_SPLIT"); return v ? atoi(v) : 0; }();
-  if (vsplit > 0) return vsplit;                   // A/B override
   int split = (int)std::max(1L, 256 / t);
   while (split > 1 && (K / 64) / split < 8) --split;
   return split;
@@ -2983,9 +2953,7 @@ int launch_n8(const GemmArgs& a, hipStream_t st) {
   e.aux_out = a.aux_out; e.alpha = a.alpha; e.beta = a.beta;
   const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / (64 * CB);
   // an XCD's ~32 concurrent tiles = 8 M-tiles x 4 N-tiles (A panel and B panel both shared)
-  static const int n8gm = [] { const char* v = getenv("DTC_N8_GM"); return v ? atoi(v) : 0; }();  // A/B override
-  const int gm = n8gm > 0 ? std::min(tiles_m, n8gm)
-                          : (tiles_n <= 4 ? std::max(1, std::min(tiles_m, 32 / tiles_n)) : std::min(tiles_m, 8));
+  const int gm = tiles_n <= 4 ? std::max(1, std::min(tiles_m, 32 / tiles_n)) : std::min(tiles_m, 8);
   constexpr int NS = CB == 3 ? 4 : 3;
   const int grid = std::min(tiles_m * tiles_n, cu_count());  // persistent: one block per CU
   hipLaunchKernelGGL((gemm8n_kernel<CB, NS, AK, BKM, EPI, OUTF32>), dim3(grid), dim3(NT2), 0, st,
@@ -3185,12 +3153,8 @@ int dtc_gemm_pair(const GemmArgs* a1, const GemmArgs* a2, hipStream_t st) {
 
 // Fused lm_head backward (ce_dgrad256_kernel): dX [M][N] fp32 (= sum of the split-K slabs, written
 // by splitk_reduce), dlogits [M][K] bf16, colpart [2*ceil(M/256)][K] fp32.  K % 64 == 0, N % 8 == 0.
-// split-K of the fused lm_head dgrad: the big_split plan, or DTC_CE_SPLIT when set (A/B)
-static int ce_split(int M, int N, int K) {
-  static const int forced = [] { const char* v = getenv("DTC_CE_SPLIT"); return v ? atoi(v) : 0; }();
-  if (forced > 0) return forced;
-  return std::max(1, big_split(1, M, N, K));
-}
+// split-K of the fused lm_head dgrad: the big_split plan (forced 4 / 5 / 8 measured within noise)
+static int ce_split(int M, int N, int K) { return std::max(1, big_split(1, M, N, K)); }
 
 long dtc_ce_dgrad_workspace_bytes(int M, int N, int K) {
   const int split = ce_split(M, N, K);

@@ -371,17 +371,10 @@ int dtc_add_layernorm_fwd(const float* x, const float* resid, float* x_out, cons
                           float* mean, float* rstd, int M, int D, float eps, int out_f32, hipStream_t st) {
   if (D % 4) return 2002;
   int nv = (D / 4 + 63) / 64;
-  // DTC_LN_FWD_RPW: rows per wave (1 or 2)
-  static const int rpw = [] { const char* v = getenv("DTC_LN_FWD_RPW"); return v ? atoi(v) : 1; }();
-  if (rpw == 2) {
-    dim3 grid((M + 7) / 8);
-    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 2>), grid, dim3(256), 0, st, x, resid, x_out, g, b, y, mean,
-                                         rstd, M, D, eps, out_f32));
-  } else {
-    dim3 grid((M + 3) / 4);
-    DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 1>), grid, dim3(256), 0, st, x, resid, x_out, g, b, y, mean,
-                                         rstd, M, D, eps, out_f32));
-  }
+  // one row per wave (two rows per wave measured neutral on GPT-2 small, round 3: removed)
+  dim3 grid((M + 3) / 4);
+  DTC_NV_SWITCH(nv, hipLaunchKernelGGL((ln_fwd_kernel<NVC, 1>), grid, dim3(256), 0, st, x, resid, x_out, g, b, y, mean,
+                                       rstd, M, D, eps, out_f32));
   DTC_CHECK_LAUNCH();
   return 0;
 }

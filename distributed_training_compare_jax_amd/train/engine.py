@@ -108,7 +108,9 @@ class Engine:
         self.flat = FlatParams(specs, m.tp_idx, tp, self.device, compute_dtype=self.act_dtype)
         if self.act_dtype == torch.bfloat16 and os.environ.get("DTC_DGRAD_NT", "1") == "1":
             # Dense / lm_head dgrads as NT GEMMs on a transposed bf16 weight copy (buffers.enable_transposed)
-            dense = ["fc1", "qkv", "out"] + (["fc2"] if os.environ.get("DTC_DGRAD_NT_FC2", "0") == "1" else [])
+            # (fc2's dgrad + dGELU runs NN on the row-major weight: level with the NT form on a mirror,
+            # profiles/r5_gemm8r.md, so fc2 needs no transposed copy)
+            dense = ["fc1", "qkv", "out"]
             head = ["lm_head.w"] if os.environ.get("DTC_DGRAD_NT_HEAD", "1") == "1" else []
             self.flat.enable_transposed([f"h.{l}.{n}.w" for l in self.layout.layers for n in dense] + head)
         self.flat.init_canonical(train_cfg.seed)
