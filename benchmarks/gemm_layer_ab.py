@@ -103,7 +103,7 @@ def main():
             u = r(M, k)
             add(f"ntdgrad {tag} [{M}x{k}x{n}] dgelu", fl, lambda dy=dy, wt=wt, u=u: G.matmul_nt_dgelu(dy, wt, u),
                 lambda dy=dy, w=w, u=u: (dy.float() @ w.float()) * u.float(), lambda dy=dy, w=w: dy @ w)
-            # the same on the row-major weight (NN: what the step runs without DTC_DGRAD_NT_FC2)
+            # the same on the row-major weight (NN: what the step runs)
             add(f"nndgrad {tag} [{M}x{k}x{n}] dgelu", fl, lambda dy=dy, w=w, u=u: G.matmul_nn_dgelu(dy, w, u),
                 lambda dy=dy, w=w, u=u: (dy.float() @ w.float()) * u.float(), lambda dy=dy, w=w: dy @ w)
         elif tag == "out":

@@ -268,7 +268,6 @@ def test_dgrad_nt_matches_nn(cuda, monkeypatch):
     """The fc1 / qkv dgrads on the transposed weight mirror (NT GEMMs, the 8-wave kernels at the
     reference shapes) give the same gradients as the NN dgrads (summation order only)."""
     grads = {}
-    monkeypatch.setenv("DTC_DGRAD_NT_FC2", "1")  # every Dense's dgrad on its transposed weight
     for nt in ("1", "0"):
         monkeypatch.setenv("DTC_DGRAD_NT", nt)
         eng, mc = _engine(cuda, use_graph=False, preset="ref", vocab=50258, batch=8, dropout=0.1)
@@ -278,7 +277,7 @@ def test_dgrad_nt_matches_nn(cuda, monkeypatch):
         torch.cuda.synchronize()
         grads[nt] = {n: eng.flat.g(n).float().cpu() for n in eng.flat.slots}
         if nt == "1":
-            for n in ("h.3.fc1.w", "h.7.qkv.w", "h.5.out.w", "h.1.fc2.w", "lm_head.w"):  # the copies track the updated mirror
+            for n in ("h.3.fc1.w", "h.7.qkv.w", "h.5.out.w", "lm_head.w"):  # the copies track the updated mirror
                 assert torch.equal(eng.flat.wt(n).cpu(), eng.flat.w(n).cpu().t())
         del eng
     for n, g in grads["1"].items():
