@@ -33,6 +33,7 @@ Scaling: ``dp`` keeps 8 sequences per GPU (weak scaling, global batch 8·N); ``t
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -70,6 +71,46 @@ def _overrides(items):
     return out
 
 
+def _ref_fp32_point(dinfo, steps: int = 20, warmup: int = 3):
+    """ms/step and tokens/s of the reference's model (configs/model_config.yaml: d512 L12 H16 F2048 T512,
+    batch 8 = 4096 tokens) trained at the reference's precision (exact fp32 MFMA kernels), same timed span
+    as the headline's blocking loop, against the published DP number (146.88 ms, 27,887 tok/s)."""
+    import torch
+
+    from distributed_training_compare_jax_amd.config.schema import (OptimConfig, TrainConfig,
+                                                                     model_config_from_preset)
+    from distributed_training_compare_jax_amd.data.synthetic import get_batch_iterator
+    from distributed_training_compare_jax_amd.parallel.dist import barrier
+    from distributed_training_compare_jax_amd.train.engine import Engine
+
+    mc = model_config_from_preset("ref")
+    tc = TrainConfig(seed=0, parallel="dp", batch=8 * dinfo.world, steps=steps, log_every=10 ** 9,
+                     output_dir="/tmp/bench", dtype="fp32")
+    e = Engine(mc, tc, OptimConfig(lr=3e-4, weight_decay=0.1, grad_clip=1.0), dinfo)
+    data = get_batch_iterator(tc.batch, mc.max_seq_len + 1, seed=0, row0=e.feed_row0, nrows=e.feed_rows)
+    for _ in range(max(warmup, 2)):
+        e.set_batch(next(data))
+        e.run_step()
+        e.loss_value()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e.set_batch(next(data))
+        e.run_step()
+        loss = e.read_loss(e.loss_handle())
+    e.flush_optimizer()
+    torch.cuda.synchronize()
+    barrier()
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    tok = 8 * mc.max_seq_len / (ms / 1e3)  # per GPU
+    del e
+    torch.cuda.empty_cache()
+    return {"model": "gpt-ref-89M (d512 L12 H16 F2048 T512 V50258)", "dtype": "fp32", "steps": steps,
+            "ms_per_step": round(ms, 3), "tokens_per_s_per_gpu": round(tok, 1), "final_loss": round(loss, 4),
+            "reference_ms_per_step": 146.88, "vs_reference": round(tok / BASELINE_TOKENS_PER_S["dp"], 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -84,6 +125,9 @@ def main():
     # zb + the auto head split: the schedule the pp8 estimate ranks best (profiles/r5_pp8_estimate.md:
     # 2.42 ms vs 3.09-3.58 for 1F1B); the JSON reports which schedule and split ran
     ap.add_argument("--pp_schedule", default="zb", choices=["gpipe", "1f1b", "zb"])
+    ap.add_argument("--ref32", default="auto", choices=["auto", "on", "off"],
+                    help="also time the reference's own model (d512 L12 T512) at the reference's precision (exact "
+                         "fp32) and report it as ref_fp32 next to the headline (auto: on for a 1-GPU run)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra TrainConfig overrides for A/B runs, e.g. --set defer_optimizer=false")
     args = ap.parse_args()
@@ -170,6 +214,7 @@ def main():
     ms = 1e3 * dt / args.steps
     tokens = global_batch * mc.max_seq_len
     value = tokens / (ms / 1e3)
+    out = None
     if dinfo.rank == 0:
         base = BASELINE_TOKENS_PER_S.get(args.parallel)
         par = {"dp": f"dp{world}", "tp": f"tp{world}", "pp": f"pp{world}"}[args.parallel]
@@ -206,6 +251,17 @@ def main():
                        "baseline_comparator": (f"reference 89.6M model, fp32, {args.parallel.upper()} "
                                                f"{BASELINE_TOKENS_PER_S.get(args.parallel):,.0f} tok/s (BASELINE.md)")},
         }
+    # the like-for-like point: the reference's own model and precision (fp32) on this GPU, timed after the
+    # headline engine is released
+    del eng, data
+    gc.collect()
+    torch.cuda.empty_cache()
+    if args.ref32 == "on" or (args.ref32 == "auto" and world == 1 and args.model != "ref"):
+        ref32 = _ref_fp32_point(dinfo)
+    else:
+        ref32 = None
+    if dinfo.rank == 0:
+        out["ref_fp32"] = ref32
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

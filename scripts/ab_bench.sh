@@ -17,7 +17,7 @@ for r in $(seq 1 "$ROUNDS"); do
     [[ "$v" == *"|"* ]] && args=${v#*|}
     log=gpurun_out/ab/r${r}_v${i}.log
     # shellcheck disable=SC2086
-    env $envs timeout -k 10 120 python bench.py --steps "$STEPS" --warmup 5 $args > "$log" 2>&1 || { echo "FAIL variant [$v] rc=$?"; tail -5 "$log"; exit 1; }
+    env $envs timeout -k 10 120 python bench.py --steps "$STEPS" --warmup 5 --ref32 off $args > "$log" 2>&1 || { echo "FAIL variant [$v] rc=$?"; tail -5 "$log"; exit 1; }
     ms=$(grep -o '"ms_per_step": [0-9.]*' "$log" | awk '{print $2}')
     echo "round $r variant [$v] ms_per_step $ms" | tee -a gpurun_out/ab/summary.log
   done

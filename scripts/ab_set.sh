@@ -5,7 +5,7 @@ declare -A res
 for rep in $(seq $REPS); do
   for v in $VALS; do
     if [ "$v" = "-" ]; then a=""; else a="--set $v"; fi
-    r=$(timeout -k 10 300 python bench.py --steps 60 --warmup 5 $a 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['ms_per_step'])") || exit 1
+    r=$(timeout -k 10 300 python bench.py --steps 60 --warmup 5 --ref32 off $a 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['ms_per_step'])") || exit 1
     res[$v]="${res[$v]} $r"
   done
 done
