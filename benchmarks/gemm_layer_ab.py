@@ -123,9 +123,15 @@ def main():
     for v in [x for x in a.variants.split(",") if x]:
         variants[v] = {"n8": (7, 0, 1024, 0), "n8w3": (7, 3, 1024, 0), "n8w4": (7, 4, 1024, 0),
                        "n8k768": (3, 0, 768, 0), "r8": (3, 0, 1024, 1), "r8f": (3, 0, 1024, 3),
-                       "r8nn": (3, 0, 1024, 5), "nor8": (3, 0, 1024, 0)}[v]
+                       "r8nn": (3, 0, 1024, 5), "nor8": (3, 0, 1024, 0), "r8ilv": None}[v]
+
+    ilv_default = L.dtc_gemm_set_r8_ilv(0)
+    L.dtc_gemm_set_r8_ilv(ilv_default)
+    if "r8ilv" in variants:
+        variants["r8ilv"] = variants["ours"] + (1,)
 
     def use(v):
+        L.dtc_gemm_set_r8_ilv(v[4] if len(v) > 4 else ilv_default)
         L.dtc_gemm_set_n8(v[0])
         L.dtc_gemm_set_n8_cb(v[1])
         L.dtc_gemm_set_n8_mink(v[2])

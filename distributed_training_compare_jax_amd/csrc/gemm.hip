@@ -1570,7 +1570,30 @@ struct R8Args {
   int M, N, K, n_split;
   int tm, tn1, gm1, nb1;  // part 1: tiles_m x tn1 tiles of 256 x 256 (nb1 blocks)
   int tn2, gm2;           // part 2: tiles_m x tn2 tiles of 256 x 64*CB2
+  int ilv;                // 1: interleaved block order (below)
 };
+
+// Block -> (part, logical tile).  ilv = 0: all 256^2 tiles, then the narrow ones.  ilv = 1 (DTC_R8_ILV):
+// [first half of the 256^2 tiles | first half of the narrow ones | second half of each]: the first
+// dispatch round then holds both widths, the CUs that drew a narrow tile go on to a 256^2 one and the
+// others to a narrow one, so the CUs end their tiles at staggered times and each epilogue's store burst
+// overlaps other CUs' main loops instead of the whole chip storing at once.
+__device__ __forceinline__ void r8_block(const R8Args& a, int b, int nb2, bool& big, int& lid) {
+  if (!a.ilv) {
+    big = b < a.nb1;
+    lid = big ? xcd_remap(b, a.nb1) : xcd_remap(b - a.nb1, nb2);
+    return;
+  }
+  const int h1 = a.nb1 / 2, h2 = nb2 / 2;
+  if (b < h1) { big = true; lid = xcd_remap(b, h1); return; }
+  b -= h1;
+  if (b < h2) { big = false; lid = xcd_remap(b, h2); return; }
+  b -= h2;
+  if (b < a.nb1 - h1) { big = true; lid = h1 + xcd_remap(b, a.nb1 - h1); return; }
+  b -= a.nb1 - h1;
+  big = false;
+  lid = h2 + xcd_remap(b, nb2 - h2);
+}
 
 template <bool AK, bool BKM, int EPI, bool OUTF32, int CB2>
 __global__ void __launch_bounds__(NT2, 1) gemm8r_kernel(R8Args a, Epi e) {
@@ -1583,16 +1606,19 @@ __global__ void __launch_bounds__(NT2, 1) gemm8r_kernel(R8Args a, Epi e) {
     tn_idx = in_g / gm_eff;
   };
   int tm_idx, tn_idx;
-  if (b < a.nb1) {
-    order(xcd_remap(b, a.nb1), a.tm, a.tn1, a.gm1, tm_idx, tn_idx);
+  const int nb2 = a.tm * a.tn2;
+  bool big;
+  int lid;
+  r8_block(a, b, nb2, big, lid);
+  if (big) {
+    order(lid, a.tm, a.tn1, a.gm1, tm_idx, tn_idx);
     Epi e1 = e;
     e1.N = a.n_split;
     gemm8p_tile_s<AK, BKM, EPI, OUTF32, 4, false>(smem, a.A, a.lda, a.B, a.ldb, a.M, a.n_split, a.K, tm_idx, tn_idx,
                                                    0, 1, a.K, nullptr, e1);
     return;
   }
-  const int nb2 = a.tm * a.tn2;
-  order(xcd_remap(b - a.nb1, nb2), a.tm, a.tn2, a.gm2, tm_idx, tn_idx);
+  order(lid, a.tm, a.tn2, a.gm2, tm_idx, tn_idx);
   // part 2 as its own problem: columns n_split.. of B / C / bias / aux
   const int ns = a.n_split;
   Epi e2 = e;
@@ -2853,6 +2879,8 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
 // NN added (default 5): fc2 dgrad + dGELU on the row-major weight 74.3 -> 62.3 us cold, step 10.84 -> 10.74 ms
 // (profiles/r5_gemm8r.md), level with the NT form on a transposed copy (DTC_DGRAD_NT_FC2=1: 10.76 ms)
 static int g_r8_mask = [] { const char* v = getenv("DTC_GEMM8R"); return v ? atoi(v) : 5; }();
+// DTC_R8_ILV: interleaved gemm8r block order (r8_block); A/B switch, set at run time by dtc_gemm_set_r8_ilv
+static int g_r8_ilv = [] { const char* v = getenv("DTC_R8_ILV"); return v ? atoi(v) : 1; }();
 
 struct R8Plan {
   int n_split = -1, cb2 = 0;
@@ -2901,6 +2929,7 @@ int launch_r8_cb(const GemmArgs& a, const R8Plan& pl, hipStream_t st) {
   r.gm1 = r.tn1 > 0 ? std::max(1, std::min(r.tm, 32 / r.tn1)) : 1;
   r.tn2 = (a.N - pl.n_split) / (64 * CB2);
   r.gm2 = std::max(1, std::min(r.tm, 32 / std::max(1, r.tn2)));
+  r.ilv = g_r8_ilv && r.nb1 >= 2 && r.tm * r.tn2 >= 2;
   const int grid = r.nb1 + r.tm * r.tn2;
   hipLaunchKernelGGL((gemm8r_kernel<AK, BKM, EPI, OUTF32, CB2>), dim3(grid), dim3(NT2), 0, st, r, e);
   DTC_CHECK_LAUNCH();
@@ -3334,6 +3363,12 @@ int dtc_wgrad_group(const WgBatch* in, hipStream_t st) {
 int dtc_gemm_set_r8(int mask) {
   const int old = g_r8_mask;
   g_r8_mask = mask;
+  return old;
+}
+
+int dtc_gemm_set_r8_ilv(int on) {
+  const int old = g_r8_ilv;
+  g_r8_ilv = on;
   return old;
 }
 

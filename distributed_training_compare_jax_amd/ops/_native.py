@@ -117,6 +117,7 @@ def _declare(lib):
         "dtc_gemm_set_n8": ([i], i),
         "dtc_gemm_set_n8_cb": ([i], i),
         "dtc_gemm_set_r8": ([i], i),
+        "dtc_gemm_set_r8_ilv": ([i], i),
         "dtc_gemm_set_big_cb3": ([i], i),
         "dtc_gemm_set_n8_mink": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),

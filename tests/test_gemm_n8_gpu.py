@@ -187,3 +187,24 @@ def test_r8_epilogues(cuda, M, Nn, K):
         outs[mask] = (y, g, yf, dg, dn)
     for a, c, name in zip(outs[7], outs[0], ("store_bf16", "gelu", "store_f32", "nt_dgelu", "nn_dgelu")):
         _close(a, c, 1e-2, f"r8_vs_default {name}")
+
+
+@pytest.mark.parametrize("M,Nn,K", R8[:2])
+def test_r8_interleaved_order_bitwise(cuda, M, Nn, K):
+    """DTC_R8_ILV only changes which block computes which tile: every output bit is unchanged."""
+    L = N.lib()
+    x, w = _r(M, K, seed=51), _r(Nn, K, scale=0.05, seed=52)
+    b = _r(Nn, seed=53, dtype=torch.float32)
+    dy, u = _r(M, K, seed=54), _r(M, Nn, seed=55)
+    wkn = w.t().contiguous()
+    outs = {}
+    for ilv in (1, 0):
+        old = L.dtc_gemm_set_r8_ilv(ilv)
+        try:
+            outs[ilv] = (G.linear(x, w, b), *G.linear_gelu(x, w, b), G.matmul_nt_dgelu(dy, w, u),
+                         G.matmul_nn_dgelu(dy, wkn, u))
+            torch.cuda.synchronize()
+        finally:
+            L.dtc_gemm_set_r8_ilv(old)
+    for a, c in zip(outs[1], outs[0]):
+        assert torch.equal(a, c)
