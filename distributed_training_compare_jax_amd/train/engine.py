@@ -461,7 +461,8 @@ class Engine:
         a GEMM built as exactly one round of one-block-per-CU tiles with all 160 KB of LDS (gemm8n) or
         one ~256-block round of 128 KB-LDS blocks (split-K 256^2 weight gradients) cannot place its last
         blocks until the collective's CUs free up, and would run about twice as long.  Inside this
-        context those problems take the many-block 128^2 / 256^2 plans that rebalance over the CUs left.
+        context those problems take the many-block 128^2 / 256^2 plans that rebalance over the CUs left (the
+        gemm8r plans already have more blocks than CUs and stay).
         No-op on CPU, with a single rank, or with DTC_COMM_SAFE_GEMMS=0."""
 
         def __init__(self, on: bool):
@@ -472,7 +473,15 @@ class Engine:
                 from ..ops import _native as N
 
                 L = N.lib()
-                self.prev = (L.dtc_gemm_set_n8(0), L.dtc_gemm_set_wgrad256(0), L.dtc_gemm_set_r8(0))
+                # gemm8r stays (DTC_COMM_SAFE_R8, default 1): 1.5 rounds of two interleaved tile widths, more
+                # blocks than CUs, so a CU held by RCCL only delays the blocks it would have run.  One-rank
+                # rehearsal with 32 CUs held by a probe kernel: 12.61-12.67 ms/step kept vs 12.77 (and one 20.7
+                # outlier) off; with none held 10.97-11.02 vs 11.15-11.20 (profiles/r6_comm_safe_r8.md)
+                keep_r8 = os.environ.get("DTC_COMM_SAFE_R8", "1") == "1"
+                r8 = L.dtc_gemm_set_r8(0)
+                if keep_r8:
+                    L.dtc_gemm_set_r8(r8)
+                self.prev = (L.dtc_gemm_set_n8(0), L.dtc_gemm_set_wgrad256(0), r8)
 
         def __exit__(self, *a):
             if self.on:

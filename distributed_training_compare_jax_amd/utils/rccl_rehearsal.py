@@ -221,13 +221,16 @@ def main(argv):
         for rnd in range(2):  # interleaved rounds (box clock drift)
             for c in cases:
                 for hc in hogs:
+                    # suffixes: _unsafe = comm-safe plans off; _r8 = comm-safe plans but gemm8r kept (DTC_COMM_SAFE_R8)
                     safe = not c.endswith("_unsafe")
                     os.environ["DTC_COMM_SAFE_GEMMS"] = "1" if safe else "0"
-                    r = bench_case(c.replace("_unsafe", ""), d, hog_cus=hc)
+                    os.environ["DTC_COMM_SAFE_R8"] = "1" if c.endswith("_r8") else "0"
+                    r = bench_case(c.replace("_unsafe", "").replace("_r8", ""), d, hog_cus=hc)
                     res["bench"].setdefault(f"{c} hog{hc}", []).append(r)
                     print(f"[bench] round {rnd} {c} hog {hc} CUs: {r['ms_per_step']:.3f} ms/step ({r['graphs']} graph "
                           f"segments, {r['comms']} eager collectives)", flush=True)
             os.environ["DTC_COMM_SAFE_GEMMS"] = "1"
+            os.environ["DTC_COMM_SAFE_R8"] = "0"
         torch.save(res, path)
         destroy()
         return
