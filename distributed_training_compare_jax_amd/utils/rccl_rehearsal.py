@@ -43,6 +43,9 @@ CASES = {
     "bf16_captured": dict(dp_grad_dtype="bf16", capture_comms=True),
     "zero1": dict(zero_stage=1, capture_comms=False),
     "zero1_captured": dict(zero_stage=1, capture_comms=True),
+    # bench-only variants of the captured fp32 DP path: weight gradients in groups of 4 / 6 layers (default 2)
+    "fp32_captured_wg4": dict(capture_comms=True, wgrad_group=4),
+    "fp32_captured_wg6": dict(capture_comms=True, wgrad_group=6),
 }
 STEPS = 5
 
@@ -221,16 +224,20 @@ def main(argv):
         for rnd in range(2):  # interleaved rounds (box clock drift)
             for c in cases:
                 for hc in hogs:
-                    # suffixes: _unsafe = comm-safe plans off; _r8 = comm-safe plans but gemm8r kept (DTC_COMM_SAFE_R8)
+                    # suffixes: _unsafe = comm-safe plans off; _nor8 = comm-safe plans with gemm8r off too (the
+                    # round-5 scope, DTC_COMM_SAFE_R8=0); none = the engine's defaults
                     safe = not c.endswith("_unsafe")
                     os.environ["DTC_COMM_SAFE_GEMMS"] = "1" if safe else "0"
-                    os.environ["DTC_COMM_SAFE_R8"] = "1" if c.endswith("_r8") else "0"
-                    r = bench_case(c.replace("_unsafe", "").replace("_r8", ""), d, hog_cus=hc)
+                    if c.endswith("_nor8"):
+                        os.environ["DTC_COMM_SAFE_R8"] = "0"
+                    else:
+                        os.environ.pop("DTC_COMM_SAFE_R8", None)
+                    r = bench_case(c.replace("_unsafe", "").replace("_nor8", ""), d, hog_cus=hc)
                     res["bench"].setdefault(f"{c} hog{hc}", []).append(r)
                     print(f"[bench] round {rnd} {c} hog {hc} CUs: {r['ms_per_step']:.3f} ms/step ({r['graphs']} graph "
                           f"segments, {r['comms']} eager collectives)", flush=True)
             os.environ["DTC_COMM_SAFE_GEMMS"] = "1"
-            os.environ["DTC_COMM_SAFE_R8"] = "0"
+            os.environ.pop("DTC_COMM_SAFE_R8", None)
         torch.save(res, path)
         destroy()
         return
