@@ -22,10 +22,10 @@ for s in $STEPS; do
     gpu)     run gpu 900 python -m pytest tests -q -m gpu -rf ;;
     dist)    run dist 900 python -m pytest tests/test_dist_gpu.py -q -m gpu -rf ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench)   run bench 600 python bench.py --steps 30 --warmup 5 ;;
+    bench)   run bench 600 python bench.py --steps 30 --warmup 5 ;;  # (+ the ref_fp32 point)
     benchng) run benchng 600 python bench.py --steps 20 --warmup 3 --no_graph ;;
     gemmb)   run gemmb 600 python benchmarks/gemm_bench.py --json gpurun_out/gemm_bench.json ;;
-    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o prof --output-format csv -- python bench.py --steps 10 --warmup 3 ;;
+    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o prof --output-format csv -- python bench.py --steps 10 --warmup 3 --ref32 off ;;
   esac
 done
 echo ALLDONE | tee -a gpurun_out/summary.log

@@ -15,5 +15,5 @@ i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i + 1))
   timeout -s KILL 150 rocprofv3 --pmc $P -d gpurun_out/pmc_$TAG$i -o pmc --output-format csv -- \
-    python bench.py --steps 2 --warmup 1 ${BENCH_ARGS:-} > gpurun_out/pmc_$TAG$i.log 2>&1 || exit $?
+    python bench.py --steps 2 --warmup 1 --ref32 off ${BENCH_ARGS:-} > gpurun_out/pmc_$TAG$i.log 2>&1 || exit $?
 done

@@ -6,4 +6,4 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 name=$1; shift
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/$name" -o prof --output-format csv -- \
-  python bench.py --steps 10 --warmup 3 "$@" > "gpurun_out/$name.log" 2>&1
+  python bench.py --steps 10 --warmup 3 --ref32 off "$@" > "gpurun_out/$name.log" 2>&1
