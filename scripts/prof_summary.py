@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--step-marker", default="adamw_kernel")
     ap.add_argument("--title", default="rocprofv3 kernel trace")
     a = ap.parse_args()
-    t = pd.read_csv(a.trace)
+    t = pd.read_csv(a.trace).sort_values("Start_Timestamp").reset_index(drop=True)  # rows are not in time order
     t["dur_us"] = (t.End_Timestamp - t.Start_Timestamp) / 1e3
     t["kernel"] = t.Kernel_Name.map(lambda s: re.sub(r"\(anonymous namespace\)::", "", s))
     t["kernel"] = t.kernel.map(lambda s: re.sub(r"\(.*", "", s)[:70])
