@@ -75,6 +75,10 @@ if _CE_CHUNK < 0 or _CE_CHUNK % 256:
 
 
 
+# lm_head input-gradient partial as bf16 into the P2P buffer below this shard width (GPTStage._head_dgrad)
+_HEAD_BF16_MAXK = 16384
+
+
 class _Staged:
     """A TP input-gradient partial a dgrad GEMM wrote into the P2P buffer (``TPComm.partial_out``)."""
 
@@ -132,6 +136,7 @@ class GPTStage:
         # tp_comm_dtype: bf16 -> row-parallel partials and input-gradient partials travel as bf16
         # (TPComm.reduce_to; residual + bias added after the fp32 sum), set by the engine
         self.tp_bf16 = False
+        self.head_dgrad_staged = 0  # lm_head input-gradient partials sent as bf16 (_head_dgrad)
         assert D % H == 0
         # whole heads per TP rank, uneven when tp does not divide H (models/params.py head_split)
         self.heads_local = head_split(H, self.tp.size)[self.tp.rank][1]
@@ -725,10 +730,31 @@ class GPTStage:
 
     def _head_dx(self, dyf):
         """The lm_head input gradient summed over the vocab shards: all-reduced, or under sequence
-        parallelism reduce-scattered to the own rows."""
+        parallelism reduce-scattered to the own rows (``dyf`` a tensor or a :class:`_Staged` bf16 partial)."""
         if self.sp:
-            return self.tp.reduce_scatter_rows(dyf)
-        return self.tp.all_reduce_(dyf)
+            return self._tp_rs(dyf)
+        return self._tp_reduce(dyf)
+
+    def _head_dgrad(self, dlogits, wt):
+        """dlogits·W, the lm_head input gradient of this rank's vocab shard.  Under ``tp_bf16`` (tp > 1, no
+        head split) the partial is written as bf16 straight into the P2P buffer -- the shard sum then moves
+        half the bytes (GPT-2 small at tp 8: 12.6 instead of 25.2 MB per step) -- when the shard's K is short
+        enough that the fp32 output would not have taken the split-K 256^2 plan anyway (K < 16384: tp >= 4
+        at GPT-2 small's vocab; at tp 2 the bf16-output plan would cost more GEMM time than the bytes save)."""
+        f = self.flat
+        w = f.w("lm_head.w")
+        rows, cols = dlogits.shape[0], (wt.shape[0] if wt is not None else w.shape[1])
+        if (self.tp_bf16 and self.tp.size > 1 and dlogits.is_cuda and self.layout.head_part[1] == 1
+                and dlogits.shape[1] < _HEAD_BF16_MAXK):
+            dst = self.tp.partial_out(rows, cols)
+            if dst is not None:
+                if wt is not None:
+                    G.linear_into(dlogits, wt, dst)
+                else:
+                    G.matmul_nn_into(dlogits, w, dst)
+                self.head_dgrad_staged += 1  # (tests: the bf16 path ran)
+                return _Staged(rows, cols, dlogits.device)
+        return G.linear_resid(dlogits, wt, None, None) if wt is not None else G.matmul_nn(dlogits, w)
 
     def head_backward(self, ctx: Dict, grad_scale: float, beta: float, extra_dyf: Optional[torch.Tensor] = None):
         """lm_head + CE backward, then the final LayerNorm's.  ``pp_head_split``: part 1 returns its half's
@@ -750,8 +776,7 @@ class GPTStage:
                                                   colpart=True)
             # dgrad first (critical path), then the weight gradient: both lm_head GEMMs run the 256^2
             # kernel at one block per CU, so issuing them concurrently only time-slices the CUs
-            dyf = (G.linear_resid(dlogits, wt, None, None) if wt is not None
-                   else G.matmul_nn(dlogits, f.w("lm_head.w")))
+            dyf = self._head_dgrad(dlogits, wt)
         # the bias gradient from the CE pass's fp32 column partials
         G.colsum(colp, f.g("lm_head.b"), beta, red=red)
         if self._defer_wg:

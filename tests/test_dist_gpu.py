@@ -18,6 +18,9 @@ STEPS = 6
 
 def _worker(parallel, kw, out_dir):
     os.environ["DTC_DIST_BACKEND"] = "gloo"
+    kw = dict(kw)
+    if "ce_fused" in kw:  # read when models.gpt is first imported (a fresh spawned rank)
+        os.environ["DTC_CE_FUSED"] = kw.pop("ce_fused")
     from distributed_training_compare_jax_amd.config.schema import OptimConfig, TrainConfig, model_config_from_preset
     from distributed_training_compare_jax_amd.parallel.dist import destroy, init_distributed
     from distributed_training_compare_jax_amd.train.loop import train
@@ -31,6 +34,7 @@ def _worker(parallel, kw, out_dir):
     r = train(tc, mc, oc, d, quiet=True, write_csv=False)
     eng = r["engine"]
     torch.save({"losses": r["history"], "graphs": r["n_graphs"], "comms": r["n_comms"], "sp": eng.stage.sp, "head_part": eng.stage.layout.head_part,
+                "head_staged": eng.stage.head_dgrad_staged,
                 "params": eng.flat.params.cpu(),
                 "named": {n: eng.flat.p(n).detach().float().cpu().clone() for n in eng.flat.slots},
                 "tp_idx": eng.mesh.tp_idx, "dp_idx": eng.mesh.dp_idx},
@@ -149,7 +153,9 @@ HEADS12 = {"d_model": 384, "n_heads": 12, "d_ff": 512, "n_layers": 2}
     (2, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": False}),  # bf16 AR
     (4, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": False}),  # two-shot, W 4
     # sequence parallel at TP=8: one sequence of the residual stream per rank, bf16 partials
-    (8, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": True, "batch": 8}),
+    # (unfused CE backward: the lm_head input-gradient partial goes out as bf16, as at GPT-2 small size)
+    (8, {"parallel": "tp", "tp_comm": "p2p", "tp_comm_dtype": "bf16", "tp_sequence_parallel": True, "batch": 8,
+         "ce_fused": "0"}),
 ])
 def test_uneven_heads_and_hybrid_one_gpu(world, kw):
     """TP=8 with 12 heads and dp2 x tp2, 8 / 4 processes on one GPU through the P2P all-reduce kernels,
@@ -159,6 +165,10 @@ def test_uneven_heads_and_hybrid_one_gpu(world, kw):
     single = _run("dp", 1, model=HEADS12, batch=kw.get("batch", 4))
     res = _run(parallel, world, model=HEADS12, **kw)
     assert res[0]["losses"] == pytest.approx(single[0]["losses"], rel=2e-2, abs=2e-2)
+    if kw.get("tp_comm_dtype") == "bf16" and kw.get("tp_sequence_parallel"):
+        # the lm_head input-gradient shard sum travelled as a bf16 partial (GPTStage._head_dgrad; the
+        # non-SP layouts here are small enough for the fused CE + dgrad kernel, whose fp32 output is summed)
+        assert all(r["head_staged"] > 0 for r in res), [r["head_staged"] for r in res]
     from distributed_training_compare_jax_amd.models.params import all_param_specs, init_full
 
     p0 = {sp.name: init_full(sp, 0) for sp in all_param_specs(_model_cfg(HEADS12))}  # canonical init (seed 0)
