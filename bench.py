@@ -19,7 +19,9 @@ timed loops of K steps, each bracketed by barrier + device sync on both sides, M
 
 * **blocking** -- ``value`` / ``ms_per_step``: the reference's timed loop (``train/train.py:75-85``)
   step for step: next host batch -> H2D -> full forward + backward + gradient collectives + clip +
-  AdamW -> blocking read of THIS step's loss before the next step is issued;
+  AdamW -> blocking read of THIS step's loss before the next step is issued.  The next batch's host
+  work (pinned-buffer fill, embedding sort keys: ``Engine.stage_batch``) runs while the step is on the
+  GPU, as a host data loader's would; its H2D copies and the next launch come after the loss read;
 * **pipelined** -- ``ms_per_step_pipelined``: the same steps, but step i's loss is read after step
   i+1 is enqueued (the host never leaves the GPU idle between steps; every loss is still read).
 
@@ -176,20 +178,24 @@ def main():
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        batch = next(data)
         loss = float("nan")
         pending = None
+        eng.stage_batch(next(data))
         for i in range(args.steps):
-            eng.set_batch(batch)
+            eng.upload_batch()
             eng.run_step()
             handle = eng.loss_handle()
-            batch = next(data)
             if not pipelined:  # the reference: block on this step's loss before the next step
+                # the next batch's host work (ids / labels into pinned memory, embedding sort keys) while this
+                # step runs; its H2D copies are enqueued only after the loss read.  The pinned slot it fills was
+                # last copied from before step i-1, whose loss was read.
+                eng.stage_batch(next(data))
                 loss = eng.read_loss(handle)
                 continue
             if pending is not None:  # step i-1's loss, read with step i already enqueued
                 loss = eng.read_loss(pending)
             pending = handle
+            eng.stage_batch(next(data))  # after step i-1's read: its pinned slot's copy has landed
         if pending is not None:
             loss = eng.read_loss(pending)
         eng.flush_optimizer()  # a deferred last AdamW lands inside the timed region

@@ -244,6 +244,7 @@ class Engine:
         pin = on_gpu
         self._host = [torch.zeros(2, self.feed_rows, T, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self._host_i = 0
+        self._staged_slot = None  # pinned slot holding the batch stage_batch prepared, until upload_batch
         # the embedding backward's sort keys of the fed ids, sorted on the host while the GPU runs the
         # previous step (a one-block device sort would sit serially in the step: ~48 us)
         self.host_keys = bool(on_gpu and pp == 1 and self.feed_rows * T <= E.SORT_MAX)
@@ -393,22 +394,41 @@ class Engine:
     def set_batch(self, batch_np: np.ndarray):
         """batch_np int32 [feed_rows, T+1] (global rows [feed_row0, feed_row0+feed_rows): this rank's
         rows, or the whole global batch under the DP embedding gather) → static device ids/labels."""
+        self.stage_batch(batch_np)
+        self.upload_batch()
+
+    def stage_batch(self, batch_np: np.ndarray):
+        """The host half of :meth:`set_batch`: the token ids / labels into the next pinned host slot and the
+        embedding backward's sort keys computed on the host.  A caller that blocks on every step's loss (the
+        reference's timed loop, ``bench.py``) stages step t+1's batch while step t still runs on the GPU, so
+        only :meth:`upload_batch` (the H2D enqueue) sits between the loss read and the next launch."""
         assert batch_np.shape[0] == self.feed_rows, (batch_np.shape, self.feed_rows)
-        h = self._host[self._host_i]
+        i = self._host_i
+        h = self._host[i]
         if self._packed_in:
             h[0].copy_(torch.from_numpy(batch_np[:, :-1]))
             h[1].copy_(torch.from_numpy(batch_np[:, 1:]))
             E.embed_sort_keys_host(batch_np[:, :-1], out=h[2].view(-1).numpy())
-            self._host_i ^= 1
+        else:
+            if self.host_keys:
+                E.embed_sort_keys_host(batch_np[:, :-1], out=self._host_keys[i].numpy())
+            h[0].copy_(torch.from_numpy(batch_np[:, :-1]))
+            h[1].copy_(torch.from_numpy(batch_np[:, 1:]))
+        self._staged_slot = i
+        self._host_i ^= 1
+
+    def upload_batch(self):
+        """Enqueue the H2D copies of the batch :meth:`stage_batch` prepared (a two-slot pinned ring: the slot
+        is rewritten two batches later, after a loss read has ordered its copy)."""
+        i = self._staged_slot
+        assert i is not None, "upload_batch without stage_batch"
+        self._staged_slot = None
+        h = self._host[i]
+        if self._packed_in:
             self._dev_in.copy_(h, non_blocking=True)
             return
         if self.host_keys:
-            hk = self._host_keys[self._host_i]
-            E.embed_sort_keys_host(batch_np[:, :-1], out=hk.numpy())
-            self.keys.copy_(hk, non_blocking=True)
-        self._host_i ^= 1
-        h[0].copy_(torch.from_numpy(batch_np[:, :-1]))
-        h[1].copy_(torch.from_numpy(batch_np[:, 1:]))
+            self.keys.copy_(self._host_keys[i], non_blocking=True)
         if self.embed_gather:
             lo = self.row0 - self.feed_row0
             self.ids_all.copy_(h[0], non_blocking=True)
