@@ -60,7 +60,12 @@ def main():
         print(f"fwd 32-row vs 16-row kernel: max |do| {(o.float() - o4.float()).abs().max().item():.3e}", flush=True)
         print(f"fwd round-4 32-row kernel vs round-5 default: max |do| {(o.float() - o5.float()).abs().max().item():.3e} "
               f"max |dlse| {(lse - lse5).abs().max().item():.3e}", flush=True)
-        variants = {"fwd (round 5 default)": lambda: A.attn_fwd(qkv, H),
+        o6, lse6 = A.attn_fwd(qkv, H, flags=32)
+        torch.cuda.synchronize()
+        print(f"fwd 2 waves/SIMD vs default (3): max |do| {(o.float() - o6.float()).abs().max().item():.3e} "
+              f"max |dlse| {(lse - lse6).abs().max().item():.3e}", flush=True)
+        variants = {"fwd (default, 3 waves/SIMD)": lambda: A.attn_fwd(qkv, H),
+                    "fwd (2 waves/SIMD, round 5)": lambda: A.attn_fwd(qkv, H, flags=32),
                     "fwd (round 4: 32 q/wave)": lambda: A.attn_fwd(qkv, H, flags=16),
                     "fwd (16 q/wave chunk)": lambda: A.attn_fwd(qkv, H, flags=4),
                     "bwd (32 rows/wave)": lambda: A.attn_bwd(qkv, o, lse, do, H),

@@ -878,10 +878,15 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd32_kernel(const bf16* _
 //    VGPRs, 12 copies per tile.
 // Measured (profiles/r5_attention.md): 26.6-26.9 us per GPT-2-small layer (two instantiations: 27.9-28.2,
 // round-4 kernel 28.2-28.5).  At 3 waves / SIMD (168 VGPRs, 48 B spilled): 30.7 us.
-template <int HD>
-__global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
-                                                             float* __restrict__ lse, int B, int T, int H,
-                                                             float scale) {
+// WPS = waves per SIMD (blocks per CU).  3 (default): the V^T fragments of each 32-key half requested just
+// before its PV MFMAs instead of all at once after QK^T -- 154 instead of 178 VGPRs, so three 4-wave blocks
+// share a CU (768 blocks = one round at GPT-2 small) and the extra wave per SIMD covers the tile's serial
+// QK^T -> softmax -> PV chain: 27.21 -> 26.54 us per layer, bitwise identical (profiles/r6_attn_fwd_wps3.log;
+// 4 waves/SIMD spills 38 VGPRs).  flags bit 5 = the 2-wave form (A/B).
+template <int HD, int WPS = 3>
+__global__ void __launch_bounds__(FW_THREADS, WPS) attn_fwd5_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+                                                               float* __restrict__ lse, int B, int T, int H,
+                                                               float scale) {
   static_assert(HD == 64, "round-5 forward: head_dim 64");
   constexpr int HC = HD / 16, HB = HD / 32;
   using L = FwLds<HD>;
@@ -928,12 +933,14 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __
     }
     // every V^T fragment of the tile in flight now: they land under the softmax
     bf16x8 vf[2][2][HB];
+    if constexpr (WPS == 2) {
 #pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2)
+      for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int i = 0; i < HB; ++i) vf[k2][s2][i] = vt_frag32(sV, L::VLD, 32 * k2 + 16 * s2, 32 * i, lane);
+          for (int i = 0; i < HB; ++i) vf[k2][s2][i] = vt_frag32(sV, L::VLD, 32 * k2 + 16 * s2, 32 * i, lane);
+    }
     if (diag) {  // wave-uniform: only the tiles that cross this wave's diagonal pay for the compares
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
@@ -971,13 +978,20 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd5_kernel(const bf16* __
       l1 += p1;
     }
 #pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2)
+    for (int k2 = 0; k2 < 2; ++k2) {
+      if constexpr (WPS != 2) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int i = 0; i < HB; ++i) vf[k2][s2][i] = vt_frag32(sV, L::VLD, 32 * k2 + 16 * s2, 32 * i, lane);
+      }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const bf16x8 pf = pack8(sc[k2], s2);
 #pragma unroll
         for (int i = 0; i < HB; ++i) acc[i] = mfma32(vf[k2][s2][i], pf, acc[i]);
       }
+    }
   };
   auto compute = [&](int it) {
     const int kb = it * FW_KEYS;
@@ -2056,9 +2070,16 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
   // code path per tile; 26.6-26.9 vs 28.2-28.5 us per layer, profiles/r5_attention.md); flags bit 4 = the
   // round-4 kernel (A/B),
   // bit 2 = the 16-row chunked kernel
+  if (HD == 64 && (flags & 32) && !(flags & 16) && !(flags & 4) && attn_chunk_enabled()) {
+    allow_lds(attn_fwd5_kernel<64, 2>, fw_lds_bytes<64>());
+    hipLaunchKernelGGL((attn_fwd5_kernel<64, 2>), dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
+                       fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale);
+    DTC_CHECK_LAUNCH();
+    return 0;
+  }
   if (HD == 64 && !(flags & 16) && !(flags & 4) && attn_chunk_enabled()) {
-    allow_lds(attn_fwd5_kernel<64>, fw_lds_bytes<64>());
-    hipLaunchKernelGGL(attn_fwd5_kernel<64>, dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
+    allow_lds(attn_fwd5_kernel<64, 3>, fw_lds_bytes<64>());
+    hipLaunchKernelGGL((attn_fwd5_kernel<64, 3>), dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
                        fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale);
     DTC_CHECK_LAUNCH();
     return 0;
