@@ -1683,8 +1683,11 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {
 
 // Finish the tail tiles: dW = beta*dW + sum_z slab[z] (z ascending), and their grad-norm partials (block
 // (tail tile, row group q) of 32 rows writes sq slot q of its tile, the slots the whole tile's waves
-// fill in the main kernel).  Grid (tail_tiles * 8), 1024 threads: 32 rows x 64 float4 columns.
-__global__ void __launch_bounds__(1024) wg_tail_reduce(WgBatch b) {
+// fill in the main kernel).  Grid (tail_tiles * 8), 256 threads: 32 rows x 64 float4 columns, 8 float4 per
+// thread, every load of a thread issued before its first add (1024-thread blocks of 2 float4 each ran 1.5
+// rounds of short-lived waves: 33 us for 75 MB at GPT-2 small).
+constexpr int WGT_THREADS = 256;
+__global__ void __launch_bounds__(WGT_THREADS) wg_tail_reduce(WgBatch b) {
   const int nmain = b.ntiles - b.tail_tiles;
   const int tt = blockIdx.x / 8, q = blockIdx.x % 8;
   const int lid = nmain + tt;
@@ -1694,13 +1697,13 @@ __global__ void __launch_bounds__(1024) wg_tail_reduce(WgBatch b) {
   const int m0 = (w.nfast ? t / tiles_n : t % tiles_m) * BIG, n0 = (w.nfast ? t % tiles_n : t / tiles_m) * BIG;
   const float* slab = b.tail_slab + (long)tt * b.tail_split * BIG * BIG;
   float ss = 0.f;
-  constexpr int IT = 32 * 64 / 1024;  // float4 per thread, all loads of a slab issued before any add
+  constexpr int IT = 32 * 64 / WGT_THREADS;  // float4 per thread, all loads of a slab issued before any add
   bool ok[IT];
   long so[IT], co[IT];
   f32x4 v[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int k = threadIdx.x + 1024 * i;
+    const int k = threadIdx.x + WGT_THREADS * i;
     const int r = q * 32 + k / 64, c = (k % 64) * 4;
     ok[i] = m0 + r < w.M && n0 + c < w.N;
     so[i] = (long)r * BIG + c;
@@ -1728,13 +1731,13 @@ __global__ void __launch_bounds__(1024) wg_tail_reduce(WgBatch b) {
       ss += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
     }
   if (!b.sq) return;
-  __shared__ float red[16];
+  __shared__ float red[WGT_THREADS / 64];
   ss = warp_sum(ss);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
   if (threadIdx.x == 0) {
     float tot = 0.f;
-    for (int w = 0; w < 16; ++w) tot += red[w];
+    for (int w = 0; w < WGT_THREADS / 64; ++w) tot += red[w];
     b.sq[(long)lid * (NT2 / 64) + q] = tot;
   }
 }
@@ -3353,7 +3356,7 @@ int dtc_wgrad_group(const WgBatch* in, hipStream_t st) {
   hipLaunchKernelGGL(gemm8p_group_kernel, dim3(t - tail + tail * b.tail_split), dim3(NT2), 0, st, b);
   DTC_CHECK_LAUNCH();
   if (tail) {
-    hipLaunchKernelGGL(wg_tail_reduce, dim3(tail * 8), dim3(1024), 0, st, b);
+    hipLaunchKernelGGL(wg_tail_reduce, dim3(tail * 8), dim3(WGT_THREADS), 0, st, b);
     DTC_CHECK_LAUNCH();
   }
   return 0;

@@ -214,9 +214,11 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
 }
 
 // out (beta*out +)= sum_p part[p*C + c], c in [0, C), the C columns cut into segments of `seg`
-// columns routed to o0 / o1 / o2.  Block = 16 columns x 16 partial groups (64-B row segments),
-// LDS tree over the groups — deterministic order, short per-thread chains (P/16 loads).
-constexpr int SR_COLS = 16, SR_GROUPS = 256 / SR_COLS;
+// columns routed to o0 / o1 / o2.  Block = 32 columns x 8 partial groups (whole 128-B row segments; 16
+// columns read half lines), LDS tree over the groups — deterministic order, P/8 loads per thread, 8 in
+// flight.  The batched TALL reduction (reduce_tasks_kernel) uses the same scheme: both paths stay bitwise
+// equal.
+constexpr int SR_COLS = 32, SR_GROUPS = 256 / SR_COLS;
 __global__ void __launch_bounds__(256) slab_reduce(const float* __restrict__ part, int P, int C, float* __restrict__ o0,
                                                    float* __restrict__ o1, float* __restrict__ o2, int seg, float beta) {
   const int tx = threadIdx.x % SR_COLS, ty = threadIdx.x / SR_COLS;
@@ -224,7 +226,7 @@ __global__ void __launch_bounds__(256) slab_reduce(const float* __restrict__ par
   DTC_ASSERT(P >= 1 && ty < SR_GROUPS && (long)blockIdx.x * SR_COLS < C);
   float s = 0.f;
   if (c < C) {
-#pragma unroll 4
+#pragma unroll 8
     for (int p = ty; p < P; p += SR_GROUPS) s += part[(long)p * C + c];
   }
   __shared__ float red[SR_GROUPS][SR_COLS];
@@ -287,7 +289,7 @@ __global__ void __launch_bounds__(256) colsum_stage1(const void* __restrict__ dy
 // graph node, paid ~9 times per layer.  Every output element is summed by one thread in a fixed
 // partial order (p ascending), so results are bitwise reproducible and equal the per-op path.
 //  WIDE  (few partials, many columns; split-K slabs): 1024 columns per block, f32x4 per thread.
-//  TALL  (many partials, few columns; LN / colsum partials): 16 columns x 16 partial groups per
+//  TALL  (many partials, few columns; LN / colsum partials): 32 columns x 8 partial groups per
 //        block, fixed-order LDS combine (the slab_reduce scheme).
 //  SUMSQ (grad-norm chunk): part[b] = weight * sum x^2 over a grid-stride share of the range.
 __global__ void __launch_bounds__(256) reduce_tasks_kernel(RedBatch batch) {
@@ -319,7 +321,7 @@ __global__ void __launch_bounds__(256) reduce_tasks_kernel(RedBatch batch) {
     const long c = (long)b * SR_COLS + tx;
     float s = 0.f;
     if (c < T.C) {
-#pragma unroll 4
+#pragma unroll 8
       for (int p = ty; p < T.P; p += SR_GROUPS) s += T.src[(long)p * T.pstride + c];
     }
     __shared__ float red[SR_GROUPS][SR_COLS];

@@ -23,6 +23,7 @@ drains everything at the end of backward.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List
 
 import torch
@@ -30,7 +31,7 @@ import torch
 from . import _native as N
 
 RED_WIDE, RED_TALL, RED_SUMSQ = 0, 1, 2
-_TALL_COLS = 16  # SR_COLS in csrc/norm_reduce.hip
+_TALL_COLS = 32  # SR_COLS in csrc/norm_reduce.hip
 _WIDE_COLS = 1024
 
 
@@ -46,6 +47,7 @@ class RedTask(ctypes.Structure):
 
 
 MAX_TASKS = 48  # RED_MAX_TASKS
+_TRACE = os.environ.get("DTC_RED_TRACE", "0") == "1"  # launch trace (diagnostic)
 
 
 class RedBatch(ctypes.Structure):
@@ -100,6 +102,10 @@ class GradReducer:
 
     # ------------------------------------------------------------------ launch
     def _launch(self, tasks):
+        if _TRACE:  # DTC_RED_TRACE=1: one line per launch (diagnostic)
+            names = {RED_WIDE: "wide", RED_TALL: "tall", RED_SUMSQ: "sumsq"}
+            print(f"[reduce flush {self.nflush}] " + " ".join(f"{names[t[0]]}(C={t[4]},P={t[6]},blk={t[7]})"
+                                                              for t in tasks), flush=True)
         L = N.lib()
         if not self._checked:
             assert L.dtc_red_task_bytes() == ctypes.sizeof(RedTask) and L.dtc_red_max_tasks() == MAX_TASKS
@@ -122,8 +128,11 @@ class GradReducer:
         ready = [t for (r, t) in self.sumsq if r < k]
         self.sumsq = [(r, t) for (r, t) in self.sumsq if r >= k]
         # long-running blocks first (they are dispatched first): norm chunks, then the many-partial
-        # (TALL) columns, then the short split-K (WIDE) blocks fill in behind them
-        tasks = sorted(ready + self.pending, key=lambda t: {RED_SUMSQ: 0, RED_TALL: 1, RED_WIDE: 2}[t[0]])
+        # (TALL) columns, then the short split-K (WIDE) blocks fill in behind them; within a kind the
+        # tasks with the most blocks first, so a flush of more than MAX_TASKS tasks leaves only the smallest
+        # to its second launch (the wte + wpe norm chunk was last: a 99-block launch of 48 tiny chunks,
+        # 18 us, ran before it)
+        tasks = sorted(ready + self.pending, key=lambda t: ({RED_SUMSQ: 0, RED_TALL: 1, RED_WIDE: 2}[t[0]], -t[7]))
         self.pending = []
         if tasks:
             self._launch(tasks)
