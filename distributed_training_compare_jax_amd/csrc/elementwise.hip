@@ -154,45 +154,60 @@ __device__ __forceinline__ void embed_piece_sums(int bx, int by, const uint32_t*
 // grid (n, ceil(D/256)), 64 threads; only the first key of each id does work.  Pieces of one id
 // start at its first key and at every piece boundary inside its run; they are fetched 8 at a time
 // (membership is monotone along the run) and added in order.
+// sq (optional, beta = 0 only): block (s, y) writes sq[s * gridDim.y + y] = its rows' sum of squares of the
+// FINAL dwte values (0 for the blocks that do no work), so the gradient norm needs no pass over the table:
+// every row no id touches is zero.
 __global__ void __launch_bounds__(64) embed_segment_sum(const uint32_t* __restrict__ keys, int n, int nb, int piece,
                                                         const float* __restrict__ P, float* __restrict__ dwte, int D,
-                                                        int accumulate) {
+                                                        int accumulate, float* __restrict__ sq) {
   const int s = blockIdx.x;
   const uint32_t id = keys[s] >> nb;
-  DTC_ASSERT(s < n && piece >= 1);
-  if (s > 0 && (keys[s - 1] >> nb) == id) return;  // not the first occurrence of this id
-  const int d = (blockIdx.y * 64 + threadIdx.x) * 4;
-  if (d >= D) return;
-  f32x4 acc = *(const f32x4*)(P + (long)s * D + d);
-  for (int q = (s / piece + 1) * piece; q < n; q += 8 * piece) {
-    bool in[8];
-    f32x4 t[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int qq = q + u * piece;
-      in[u] = qq < n && (keys[min(qq, n - 1)] >> nb) == id;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      t[u] = in[u] ? *(const f32x4*)(P + (long)(q + u * piece) * D + d) : f32x4{0.f, 0.f, 0.f, 0.f};
-    bool more = true;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (!in[u]) { more = false; break; }
-      acc += t[u];
-    }
-    if (!more) break;
+  DTC_ASSERT(s < n && piece >= 1 && !(sq && accumulate));
+  float* sq_slot = sq ? sq + (long)s * gridDim.y + blockIdx.y : nullptr;
+  if (s > 0 && (keys[s - 1] >> nb) == id) {  // not the first occurrence of this id (block-uniform)
+    if (sq_slot && threadIdx.x == 0) *sq_slot = 0.f;
+    return;
   }
-  float* o = dwte + (long)id * D + d;
-  if (accumulate) acc += *(const f32x4*)o;
-  *(f32x4*)o = acc;
+  const int d = (blockIdx.y * 64 + threadIdx.x) * 4;
+  float q2 = 0.f;  // this lane's sum of squares of the final values
+  if (d < D) {
+    f32x4 acc = *(const f32x4*)(P + (long)s * D + d);
+    for (int q = (s / piece + 1) * piece; q < n; q += 8 * piece) {
+      bool in[8];
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int qq = q + u * piece;
+        in[u] = qq < n && (keys[min(qq, n - 1)] >> nb) == id;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        t[u] = in[u] ? *(const f32x4*)(P + (long)(q + u * piece) * D + d) : f32x4{0.f, 0.f, 0.f, 0.f};
+      bool more = true;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (!in[u]) { more = false; break; }
+        acc += t[u];
+      }
+      if (!more) break;
+    }
+    float* o = dwte + (long)id * D + d;
+    if (accumulate) acc += *(const f32x4*)o;
+    *(f32x4*)o = acc;
+    q2 = acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2] + acc[3] * acc[3];
+  }
+  if (sq_slot) {  // every lane of the (one-wave) block reaches the sum
+    const float z = warp_sum(q2);
+    if (threadIdx.x == 0) *sq_slot = z;
+  }
 }
 
-__device__ __forceinline__ void wpe_bwd(long i, const float* __restrict__ dh, float* __restrict__ dwpe, int B, int T,
-                                        int D, float p, uint32_t seed, const int64_t* __restrict__ step, long row0,
-                                        int accumulate) {
+// returns the sum of squares of the dwpe values this thread wrote (0 past the end)
+__device__ __forceinline__ float wpe_bwd(long i, const float* __restrict__ dh, float* __restrict__ dwpe, int B, int T,
+                                         int D, float p, uint32_t seed, const int64_t* __restrict__ step, long row0,
+                                         int accumulate) {
   const int D4 = D / 4;
-  if (i >= (long)T * D4) return;
+  if (i >= (long)T * D4) return 0.f;
   int t = (int)(i / D4);
   int d = (int)(i % D4) * 4;
   DTC_ASSERT(D % 4 == 0 && t < T && d + 4 <= D && B >= 1);
@@ -203,6 +218,7 @@ __device__ __forceinline__ void wpe_bwd(long i, const float* __restrict__ dh, fl
   float* o = dwpe + (long)t * D + d;
   if (accumulate) acc += *(f32x4*)o;
   *(f32x4*)o = acc;
+  return acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2] + acc[3] * acc[3];
 }
 
 // The embedding backward's first launch: three independent jobs in one grid of 64-thread blocks, so the
@@ -216,7 +232,7 @@ __global__ void __launch_bounds__(64) embed_bwd_stage1(const uint32_t* __restric
                                                        float* __restrict__ P, float* __restrict__ dwte, long n4zero,
                                                        int nzero, float* __restrict__ dwpe, int B, int T, int D,
                                                        float p, uint32_t seed, const int64_t* __restrict__ step,
-                                                       long row0, int accumulate) {
+                                                       long row0, int accumulate, float* __restrict__ sq_wpe) {
   int b = blockIdx.x;
   if (b < nzero) {
     f32x4* z = (f32x4*)dwte;
@@ -230,7 +246,11 @@ __global__ void __launch_bounds__(64) embed_bwd_stage1(const uint32_t* __restric
     return;
   }
   b -= npieces * dblk;
-  wpe_bwd((long)b * 64 + threadIdx.x, dh, dwpe, B, T, D, p, seed, step, row0, accumulate);
+  const float q = wpe_bwd((long)b * 64 + threadIdx.x, dh, dwpe, B, T, D, p, seed, step, row0, accumulate);
+  if (sq_wpe) {  // one sum-of-squares slot per dwpe block (the norm's fused partials, beta = 0 only)
+    const float z = warp_sum(q);
+    if (threadIdx.x == 0) sq_wpe[b] = z;
+  }
 }
 
 // ---------------------------------------------------------------- cross-entropy
@@ -681,8 +701,12 @@ struct TrBatch {
 };
 
 __global__ void __launch_bounds__(256) transpose_batch_kernel(TrBatch batch) {
-  int t = 0;
-  while (t + 1 < batch.ntasks && (int)blockIdx.x >= batch.t[t + 1].blk0) ++t;
+  int t = 0, hi = batch.ntasks - 1;  // binary search over the ascending blk0
+  while (t < hi) {
+    const int mid = (t + hi + 1) >> 1;
+    if ((int)blockIdx.x >= batch.t[mid].blk0) t = mid;
+    else hi = mid - 1;
+  }
   const TrTask& T = batch.t[t];
   const int b = blockIdx.x - T.blk0;
   const int tcols = (T.cols + 63) / 64;
@@ -750,9 +774,17 @@ int dtc_embed_sort(const int* ids, int n, int V, uint32_t* keys, hipStream_t st)
 
 // dwte (+)= scatter(ids, dropout'(dh)), dwpe (+)= sum_b dropout'(dh); keys from dtc_embed_sort,
 // P = n*D fp32 scratch.  Bitwise deterministic.
+// sq (optional; accumulate == 0): dtc_embed_sq_slots(B, T, D) sum-of-squares partials of the final dwte / dwpe
+// values -- the gradient norm's share of the two tables without a pass over them (FusedAdamW fused partials)
+long dtc_embed_sq_slots(int B, int T, int D) {
+  const long dblk = (D / 4 + 63) / 64, nwpe = ((long)T * (D / 4) + 63) / 64;
+  return (long)B * T * dblk + nwpe;
+}
+
 int dtc_embed_bwd(const uint32_t* keys, const float* dh, float* dwte, float* dwpe, float* P, int B, int T, int D, int V,
-                  float p, long seed, const int64_t* step, long row0, int accumulate, hipStream_t st) {
+                  float p, long seed, const int64_t* step, long row0, int accumulate, float* sq, hipStream_t st) {
   if (D % 4) return 3001;
+  if (sq && accumulate) return 3005;
   const int n = B * T;
   if (n > SORT_MAX) return 3003;
   const int nb = dtc_embed_sort_bits(n);
@@ -767,9 +799,10 @@ int dtc_embed_bwd(const uint32_t* keys, const float* dh, float* dwte, float* dwp
   const long nblk = nzero + (long)npieces * dblk + nwpe;
   if (nblk > 0x7fffffffL) return 3004;
   hipLaunchKernelGGL(embed_bwd_stage1, dim3((unsigned)nblk), dim3(64), 0, st, keys, n, nb, piece, npieces, dblk, dh, P,
-                     dwte, n4, (int)nzero, dwpe, B, T, D, p, (uint32_t)seed, step, row0, accumulate);
+                     dwte, n4, (int)nzero, dwpe, B, T, D, p, (uint32_t)seed, step, row0, accumulate,
+                     sq ? sq + (long)n * dblk : nullptr);
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(embed_segment_sum, dim3(n, dblk), dim3(64), 0, st, keys, n, nb, piece, P, dwte, D, accumulate);
+  hipLaunchKernelGGL(embed_segment_sum, dim3(n, dblk), dim3(64), 0, st, keys, n, nb, piece, P, dwte, D, accumulate, sq);
   DTC_CHECK_LAUNCH();
   return 0;
 }

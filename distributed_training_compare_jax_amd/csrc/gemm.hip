@@ -1643,10 +1643,16 @@ __global__ void __launch_bounds__(NT2, 1) gemm8r_kernel(R8Args a, Epi e) {
 // Tail split (b.tail_tiles > 0): the grid's last blocks are K-pieces of the last tail_tiles logical tiles,
 // so the final, partly filled round of whole tiles (GPT-2 small: 1887 tiles = 7 rounds + 95) becomes
 // tail_split times as many blocks of 1/tail_split the length; wg_tail_reduce finishes those tiles.
+// entry of logical tile lid: binary search over the ascending tile0 (a linear scan was up to ~50 dependent
+// scalar loads of the kernel argument at every block's start)
 __device__ __forceinline__ const WgEntry& wg_entry(const WgBatch& b, int lid) {
-  int i = 0;
-  while (i + 1 < b.n && lid >= b.e[i + 1].tile0) ++i;
-  return b.e[i];
+  int lo = 0, hi = b.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (lid >= b.e[mid].tile0) lo = mid;
+    else hi = mid - 1;
+  }
+  return b.e[lo];
 }
 
 __global__ void __launch_bounds__(NT2, 1) gemm8p_group_kernel(WgBatch b) {

@@ -293,8 +293,14 @@ __global__ void __launch_bounds__(256) colsum_stage1(const void* __restrict__ dy
 //        block, fixed-order LDS combine (the slab_reduce scheme).
 //  SUMSQ (grad-norm chunk): part[b] = weight * sum x^2 over a grid-stride share of the range.
 __global__ void __launch_bounds__(256) reduce_tasks_kernel(RedBatch batch) {
-  int t = 0;
-  while (t + 1 < batch.ntasks && (int)blockIdx.x >= batch.t[t + 1].blk0) ++t;
+  // task of this block: binary search over the ascending blk0 (a linear scan cost up to 47 dependent scalar
+  // loads of the kernel argument per block: 18 us for a launch of 48 one-block norm chunks)
+  int t = 0, hi = batch.ntasks - 1;
+  while (t < hi) {
+    const int mid = (t + hi + 1) >> 1;
+    if ((int)blockIdx.x >= batch.t[mid].blk0) t = mid;
+    else hi = mid - 1;
+  }
   const RedTask& T = batch.t[t];
   const int b = blockIdx.x - T.blk0;
   DTC_ASSERT(t < batch.ntasks && b >= 0 && b < T.nblk && (int)blockIdx.x < batch.nblocks);

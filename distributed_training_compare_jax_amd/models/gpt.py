@@ -155,6 +155,8 @@ class GPTStage:
         self.wg_record = False
         self.wg_seen = None
         self.wg_sq: Optional[torch.Tensor] = None
+        # the embedding backward's Σ dwte² + Σ dwpe² partial slots (FusedAdamW fused partials), or None
+        self.emb_sq: Optional[torch.Tensor] = None
         self._wg_keys = None
         # LayerNorm fused into the layer GEMMs (ops/ln_fused.py), set up by enable_ln_fusion
         self.ln_sync: Optional[LF.LnSync] = None
@@ -311,7 +313,10 @@ class GPTStage:
         if self.sp and gathered is None:
             dh = self.tp.all_gather_rows(dh)  # every rank builds the identical wte / wpe grads
         f = self.flat
-        E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta, keys=keys)
+        sq = self.emb_sq
+        if sq is not None and (beta != 0.0 or gathered is not None or self.sp):
+            raise RuntimeError("fused embedding Σg² partials need one local embedding backward per step (beta 0)")
+        E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta, keys=keys, sq=sq)
 
     # ------------------------------------------------------------------ block
     def _await_params(self, key):

@@ -75,6 +75,7 @@ class Engine:
 
         # ---- batch geometry (reference: `batch` is the global batch, train_config_*.yaml:1)
         T = model_cfg.max_seq_len
+        self._D = model_cfg.d_model
         self.T = T
         self.global_batch = train_cfg.batch
         if self.global_batch % dp:
@@ -675,8 +676,26 @@ class Engine:
             for dw, m, n in st.wg_seen:
                 ranges.append(((dw.data_ptr() - base) // 4, dw.numel()))
                 tiles += G.wgrad_tiles(m, n)
-            st.use_wgrad_sumsq(self.opt.set_fused_sumsq(ranges, tiles * G.WG_SQ_SLOTS))
+            nwg = tiles * G.WG_SQ_SLOTS
+            # the embedding tables' Σg² from the embedding backward itself (its last kernel writes the final
+            # rows): no 154 MB norm pass over a table whose untouched rows are zero (GPT-2 small: -25 us/step)
+            emb = 0
+            if self._emb_fused_norm():
+                for name in ("wte", "wpe"):
+                    g = self.flat.g(name)
+                    ranges.append(((g.data_ptr() - base) // 4, g.numel()))
+                emb = E.embed_sq_slots(self.b_local, self.T, self._D)
+            part = self.opt.set_fused_sumsq(ranges, nwg + emb)
+            st.use_wgrad_sumsq(part[:nwg])
+            if emb:
+                st.emb_sq = part[nwg:]
         return self.loss
+
+    def _emb_fused_norm(self) -> bool:
+        """The embedding backward may write the wte / wpe share of Σg² itself: one local embedding backward
+        per step (no DP gather, no TP / sequence parallelism: norm weight 1), one sort window."""
+        return (self.layout.has_embed and self.mesh.tp == 1 and not self.embed_gather and not self.stage.sp
+                and self.b_local * self.T <= E.SORT_MAX)
 
     def loss_value(self) -> float:
         """Blocking read of the global mean loss (reference: float(np.asarray(loss)), train.py:82)."""

@@ -170,8 +170,8 @@ def test_deferred_optimizer_matches_immediate(cuda, monkeypatch):
 
 
 def test_fused_grad_norm_matches(cuda, monkeypatch):
-    """The grouped weight-gradient launch's per-tile Σ dW² (switched on after the first, eager step)
-    replaces ~3/4 of the norm pass: at every step (graph-replayed ones included) the engine's grad norm
+    """The grouped weight-gradient launch's per-tile Σ dW² and the embedding backward's per-block Σ dwte² /
+    Σ dwpe² (switched on after the first, eager step) replace most of the norm pass: at every step (graph-replayed ones included) the engine's grad norm
     equals the norm of the grads that step left behind, with and without the fusion.  (The two runs'
     losses agree only loosely: a last-bit difference in the clip factor flips bf16 mirror roundings.)"""
     runs = {}
@@ -188,6 +188,8 @@ def test_fused_grad_norm_matches(cuda, monkeypatch):
             assert norm == pytest.approx(g, rel=1e-5), (fused, len(out), norm, g)
             out.append((loss, norm))
         assert (eng.stage.wg_sq is not None) == (fused == "1")
+        # ... and the embedding backward's Σ dwte² + Σ dwpe² partials replace the norm pass over both tables
+        assert (eng.stage.emb_sq is not None) == (fused == "1")
         runs[fused] = out
         del eng
     assert runs["1"][0] == runs["0"][0]  # step 1 (eager, before the switch) is identical
