@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(64) embed_bwd_stage1(const uint32_t* __restric
 // index: for the part-major GEMM partials (srow 1, spart M) lanes 0-15 read 16 consecutive rows'
 // pairs (one 128-B line) per partial — the one-wave-per-row mapping read 8 B per line.  Two passes
 // (row max, then the rescaled sum), each combined over the 16 lanes in fixed order.
-constexpr int CC_ROWS = 16, CC_LANES = 16;
+constexpr int CC_ROWS = 16, CC_LANES = 16, CC_REG = 16;
 __global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__ part, int M, int P, long srow, long spart,
                                                        float* __restrict__ lse_out, float* __restrict__ rowstat) {
   const int r = threadIdx.x % CC_ROWS, pl = threadIdx.x / CC_ROWS;
@@ -268,10 +268,25 @@ __global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__
   DTC_ASSERT(P >= 1 && pl < CC_LANES && (long)blockIdx.x * CC_ROWS < M);
   __shared__ float red[CC_LANES][CC_ROWS];
   __shared__ float rmax[CC_ROWS];
+  // P <= CC_LANES * CC_REG (GPT-2 small: 197 lm_head tiles): every partial of the thread is loaded once, all
+  // loads in flight together, and the sum pass reads the registers (the two global passes were latency-bound:
+  // 21 us for 13 MB).  Same max / sum order as the two-pass form: bitwise identical.
+  const bool in_reg = P <= CC_LANES * CC_REG;
+  f32x2 qv[CC_REG];
   float mx = -INFINITY;
   if (row < M) {
+    if (in_reg) {
+#pragma unroll
+      for (int k = 0; k < CC_REG; ++k) {
+        const int p = pl + k * CC_LANES;
+        qv[k] = p < P ? *(const f32x2*)(part + (row * srow + p * spart) * 2) : f32x2{-INFINITY, 0.f};
+      }
+#pragma unroll
+      for (int k = 0; k < CC_REG; ++k) mx = fmaxf(mx, qv[k][0]);
+    } else {
 #pragma unroll 4
-    for (int p = pl; p < P; p += CC_LANES) mx = fmaxf(mx, part[(row * srow + p * spart) * 2]);
+      for (int p = pl; p < P; p += CC_LANES) mx = fmaxf(mx, part[(row * srow + p * spart) * 2]);
+    }
   }
   red[pl][r] = mx;
   __syncthreads();
@@ -285,10 +300,16 @@ __global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__
   mx = rmax[r];
   float s = 0.f;
   if (row < M) {
+    if (in_reg) {
+#pragma unroll
+      for (int k = 0; k < CC_REG; ++k)
+        if (qv[k][1] > 0.f) s += qv[k][1] * __expf(qv[k][0] - mx);
+    } else {
 #pragma unroll 4
-    for (int p = pl; p < P; p += CC_LANES) {
-      const f32x2 q = *(const f32x2*)(part + (row * srow + p * spart) * 2);
-      if (q[1] > 0.f) s += q[1] * __expf(q[0] - mx);
+      for (int p = pl; p < P; p += CC_LANES) {
+        const f32x2 q = *(const f32x2*)(part + (row * srow + p * spart) * 2);
+        if (q[1] > 0.f) s += q[1] * __expf(q[0] - mx);
+      }
     }
   }
   __syncthreads();

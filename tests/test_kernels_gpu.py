@@ -399,6 +399,28 @@ def test_adamw_matches_cpu(cuda):
     assert torch.equal(p, p2) and torch.equal(m, m2) and torch.equal(v, v2) and torch.equal(mirror, mir2)
 
 
+@pytest.mark.parametrize("R", [1, 197, 256, 300])
+def test_ce_combine_rows(cuda, R):
+    """Row (max, Σexp) partials of R vocab tiles / shards -> lse and loss against a float64 torch reference:
+    the register path (R <= 256: every partial loaded once) and the two-pass path (R > 256); empty partials
+    (Σexp = 0, max -inf: tiles past a row's valid vocab) must not contribute."""
+    from distributed_training_compare_jax_amd.ops import xent as X
+
+    M = 1000
+    g = torch.Generator().manual_seed(R)
+    mx = torch.randn(R, M, generator=g) * 4
+    se = torch.rand(R, M, generator=g) * 60 + 1
+    if R > 1:
+        mx[-1, :50], se[-1, :50] = -float("inf"), 0.0
+    st = torch.stack([mx, se], -1).contiguous()
+    lab = torch.randn(M, generator=g)
+    lse, loss = X.ce_finalize(st.to(cuda), lab.to(cuda), 0.5)
+    m64 = st[..., 0].double().max(0).values
+    ref = m64 + torch.log((st[..., 1].double() * torch.exp(st[..., 0].double() - m64)).sum(0))
+    assert torch.allclose(lse.cpu().double(), ref, rtol=0, atol=2e-5), (lse.cpu().double() - ref).abs().max()
+    assert float(loss.item()) == pytest.approx(float(0.5 * (ref - lab.double()).sum()), rel=1e-5)
+
+
 def test_batched_reducer_matches_per_op(cuda):
     """ops/reduce.py: wgrad split-K slabs, colsum and LN partials finished by one batched launch
     are bitwise equal to the per-op kernels; the grad-norm task matches torch."""
