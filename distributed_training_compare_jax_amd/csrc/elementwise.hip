@@ -159,9 +159,11 @@ __device__ __forceinline__ void embed_piece_sums(int bx, int by, const uint32_t*
 // every row no id touches is zero.
 __global__ void __launch_bounds__(64) embed_segment_sum(const uint32_t* __restrict__ keys, int n, int nb, int piece,
                                                         const float* __restrict__ P, float* __restrict__ dwte, int D,
-                                                        int accumulate, float* __restrict__ sq) {
+                                                        int accumulate, float* __restrict__ sq,
+                                                        uint32_t* __restrict__ keys_out) {
   const int s = blockIdx.x;
   const uint32_t id = keys[s] >> nb;
+  if (keys_out && blockIdx.y == 0 && threadIdx.x == 0) keys_out[s] = keys[s];  // the next call's prev_keys
   DTC_ASSERT(s < n && piece >= 1 && !(sq && accumulate));
   float* sq_slot = sq ? sq + (long)s * gridDim.y + blockIdx.y : nullptr;
   if (s > 0 && (keys[s - 1] >> nb) == id) {  // not the first occurrence of this id (block-uniform)
@@ -223,7 +225,8 @@ __device__ __forceinline__ float wpe_bwd(long i, const float* __restrict__ dh, f
 
 // The embedding backward's first launch: three independent jobs in one grid of 64-thread blocks, so the
 // latency-bound piece sums run alongside the bandwidth-bound table zeroing instead of after it:
-// [0, nzero) zero the dwte table (EB_ZCH float4 per block; beta = 0 only), then the piece-sum blocks
+// [0, nzero) zero the dwte table (EB_ZCH float4 per block; beta = 0 only; with prev_keys: one block per key of
+// the previous call, zeroing that id's row once -- the only rows that can be nonzero), then the piece-sum blocks
 // (pieces x dblk), then dwpe (one thread per (t, 4 channels)).  Was three launches, 53 us at GPT-2 small;
 // 36.8 us in this order (40.9 us with the piece sums first).
 constexpr int EB_ZCH = 64 * 32;
@@ -232,9 +235,17 @@ __global__ void __launch_bounds__(64) embed_bwd_stage1(const uint32_t* __restric
                                                        float* __restrict__ P, float* __restrict__ dwte, long n4zero,
                                                        int nzero, float* __restrict__ dwpe, int B, int T, int D,
                                                        float p, uint32_t seed, const int64_t* __restrict__ step,
-                                                       long row0, int accumulate, float* __restrict__ sq_wpe) {
+                                                       long row0, int accumulate, float* __restrict__ sq_wpe,
+                                                       const uint32_t* __restrict__ prev_keys) {
   int b = blockIdx.x;
   if (b < nzero) {
+    if (prev_keys) {  // sparse: zero the rows the previous call wrote (every other row is still zero)
+      const uint32_t id = prev_keys[b] >> nb;
+      if (b > 0 && (prev_keys[b - 1] >> nb) == id) return;  // not the id's first key (block-uniform)
+      f32x4* z = (f32x4*)(dwte + (long)id * D);
+      for (int e = threadIdx.x; e < D / 4; e += 64) z[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
     f32x4* z = (f32x4*)dwte;
     const long e0 = (long)b * EB_ZCH, e1 = min(n4zero, e0 + EB_ZCH);
     for (long e = e0 + threadIdx.x; e < e1; e += 64) z[e] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -260,7 +271,7 @@ __global__ void __launch_bounds__(64) embed_bwd_stage1(const uint32_t* __restric
 // index: for the part-major GEMM partials (srow 1, spart M) lanes 0-15 read 16 consecutive rows'
 // pairs (one 128-B line) per partial — the one-wave-per-row mapping read 8 B per line.  Two passes
 // (row max, then the rescaled sum), each combined over the 16 lanes in fixed order.
-constexpr int CC_ROWS = 16, CC_LANES = 16, CC_REG = 16;
+constexpr int CC_ROWS = 16, CC_LANES = 16, CC_REG = 56;
 __global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__ part, int M, int P, long srow, long spart,
                                                        float* __restrict__ lse_out, float* __restrict__ rowstat) {
   const int r = threadIdx.x % CC_ROWS, pl = threadIdx.x / CC_ROWS;
@@ -268,7 +279,8 @@ __global__ void __launch_bounds__(256) ce_combine_rows(const float* __restrict__
   DTC_ASSERT(P >= 1 && pl < CC_LANES && (long)blockIdx.x * CC_ROWS < M);
   __shared__ float red[CC_LANES][CC_ROWS];
   __shared__ float rmax[CC_ROWS];
-  // P <= CC_LANES * CC_REG (GPT-2 small: 197 lm_head tiles): every partial of the thread is loaded once, all
+  // P <= CC_LANES * CC_REG (GPT-2 small: 788 = 197 lm_head tiles x 4 wave columns): every partial of the thread
+  // is loaded once, all
   // loads in flight together, and the sum pass reads the registers (the two global passes were latency-bound:
   // 21 us for 13 MB).  Same max / sum order as the two-pass form: bitwise identical.
   const bool in_reg = P <= CC_LANES * CC_REG;
@@ -802,10 +814,14 @@ long dtc_embed_sq_slots(int B, int T, int D) {
   return (long)B * T * dblk + nwpe;
 }
 
+// prev_keys (optional, n entries, accumulate == 0 only): the keys of the previous call into this same dwte,
+// whose rows are the only nonzero ones -- zeroed sparsely instead of the whole V x D table (GPT-2 small: at
+// most 25 of 154 MB); prev_valid = 0 on the first call (full zeroing).  The call stores its own keys there.
 int dtc_embed_bwd(const uint32_t* keys, const float* dh, float* dwte, float* dwpe, float* P, int B, int T, int D, int V,
-                  float p, long seed, const int64_t* step, long row0, int accumulate, float* sq, hipStream_t st) {
+                  float p, long seed, const int64_t* step, long row0, int accumulate, float* sq, uint32_t* prev_keys,
+                  int prev_valid, hipStream_t st) {
   if (D % 4) return 3001;
-  if (sq && accumulate) return 3005;
+  if ((sq || prev_keys) && accumulate) return 3005;
   const int n = B * T;
   if (n > SORT_MAX) return 3003;
   const int nb = dtc_embed_sort_bits(n);
@@ -815,15 +831,17 @@ int dtc_embed_bwd(const uint32_t* keys, const float* dh, float* dwte, float* dwp
   const int npieces = (n + piece - 1) / piece;
   // zero the table (beta = 0) with kernel blocks (not a memset node) in the same launch as the piece sums
   const long n4 = accumulate ? 0 : (long)V * D / 4;
-  const long nzero = (n4 + EB_ZCH - 1) / EB_ZCH;
+  const bool sparse = prev_keys && prev_valid;
+  const long nzero = sparse ? n : (n4 + EB_ZCH - 1) / EB_ZCH;
   const long nwpe = ((long)T * (D / 4) + 63) / 64;
   const long nblk = nzero + (long)npieces * dblk + nwpe;
   if (nblk > 0x7fffffffL) return 3004;
   hipLaunchKernelGGL(embed_bwd_stage1, dim3((unsigned)nblk), dim3(64), 0, st, keys, n, nb, piece, npieces, dblk, dh, P,
                      dwte, n4, (int)nzero, dwpe, B, T, D, p, (uint32_t)seed, step, row0, accumulate,
-                     sq ? sq + (long)n * dblk : nullptr);
+                     sq ? sq + (long)n * dblk : nullptr, sparse ? prev_keys : nullptr);
   DTC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(embed_segment_sum, dim3(n, dblk), dim3(64), 0, st, keys, n, nb, piece, P, dwte, D, accumulate, sq);
+  hipLaunchKernelGGL(embed_segment_sum, dim3(n, dblk), dim3(64), 0, st, keys, n, nb, piece, P, dwte, D, accumulate, sq,
+                     prev_keys);
   DTC_CHECK_LAUNCH();
   return 0;
 }

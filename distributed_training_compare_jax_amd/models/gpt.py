@@ -157,6 +157,10 @@ class GPTStage:
         self.wg_sq: Optional[torch.Tensor] = None
         # the embedding backward's Σ dwte² + Σ dwpe² partial slots (FusedAdamW fused partials), or None
         self.emb_sq: Optional[torch.Tensor] = None
+        # the previous embedding backward's sort keys (its rows are the only nonzero ones of the wte grad), or
+        # None: full-table zeroing every step (set by the engine where one local backward writes the table)
+        self.emb_prev: Optional[torch.Tensor] = None
+        self._emb_prev_valid = False
         self._wg_keys = None
         # LayerNorm fused into the layer GEMMs (ops/ln_fused.py), set up by enable_ln_fusion
         self.ln_sync: Optional[LF.LnSync] = None
@@ -316,7 +320,13 @@ class GPTStage:
         sq = self.emb_sq
         if sq is not None and (beta != 0.0 or gathered is not None or self.sp):
             raise RuntimeError("fused embedding Σg² partials need one local embedding backward per step (beta 0)")
-        E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta, keys=keys, sq=sq)
+        prev = self.emb_prev
+        if prev is not None and (beta != 0.0 or gathered is not None or self.sp):
+            raise RuntimeError("sparse wte zeroing needs one local embedding backward per step (beta 0)")
+        E.embed_bwd(ids, dh, f.g("wte"), f.g("wpe"), self.cfg.dropout, self.seed, step, row0, beta, keys=keys, sq=sq,
+                    prev_keys=prev, prev_valid=self._emb_prev_valid)
+        if prev is not None:
+            self._emb_prev_valid = True  # from the next call on only the rows written here are zeroed
 
     # ------------------------------------------------------------------ block
     def _await_params(self, key):

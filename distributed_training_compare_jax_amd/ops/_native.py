@@ -154,7 +154,7 @@ def _declare(lib):
         "dtc_cu_hog": ([i, l, i, vp, vp], i),
         "dtc_embed_sort_bits": ([i], i),
         "dtc_embed_sort": ([vp, i, i, vp, vp], i),
-        "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp, vp], i),
+        "dtc_embed_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, f, l, vp, l, i, vp, vp, i, vp], i),
         "dtc_embed_sq_slots": ([i, i, i], l),
         "dtc_attn_fwd": ([vp, vp, vp, i, i, i, i, l, f, vp], i),
         "dtc_attn_bwd": ([vp, vp, vp, vp, vp, i, i, i, i, i, f, vp, l, vp], i),

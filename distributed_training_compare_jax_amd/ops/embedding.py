@@ -81,13 +81,17 @@ def embed_sq_slots(B: int, T: int, D: int) -> int:
 
 
 def embed_bwd(ids: torch.Tensor, dh: torch.Tensor, dwte: torch.Tensor, dwpe: torch.Tensor, p: float, seed: int,
-              step: torch.Tensor, row0: int, beta: float = 0.0, keys: torch.Tensor = None, sq: torch.Tensor = None):
+              step: torch.Tensor, row0: int, beta: float = 0.0, keys: torch.Tensor = None, sq: torch.Tensor = None,
+              prev_keys: torch.Tensor = None, prev_valid: bool = False):
     """dwte (β·)+= scatter_add(ids, dropout'(dh)); dwpe (β·)+= Σ_b dropout'(dh).
 
     GPU path is bitwise deterministic (sorted segment sums, no float atomics; see
     ``csrc/elementwise.hip``); ``keys`` = :func:`embed_sort_keys` of ``ids`` if precomputed.
     ``sq`` (GPU, beta = 0, one sort window): :func:`embed_sq_slots` fp32 partials whose sum is Σ dwte² + Σ dwpe²
-    of the new grads (the gradient norm's share of both tables without reading them again)."""
+    of the new grads (the gradient norm's share of both tables without reading them again).
+    ``prev_keys`` (GPU, beta = 0, one sort window): int32 [B*T] that holds the previous call's sort keys for this
+    same ``dwte`` (``prev_valid``) -- only their rows are zeroed instead of the whole table -- and receives this
+    call's keys."""
     B, T = ids.shape
     D = dh.shape[1]
     if not ids.is_cuda:
@@ -104,6 +108,8 @@ def embed_bwd(ids: torch.Tensor, dh: torch.Tensor, dwte: torch.Tensor, dwpe: tor
     if sq is not None:
         assert beta == 0.0 and B * T <= SORT_MAX and sq.dtype == torch.float32 and sq.is_contiguous()
         assert sq.numel() == embed_sq_slots(B, T, dh.shape[1]), (sq.numel(), B, T)
+    if prev_keys is not None:
+        assert beta == 0.0 and B * T <= SORT_MAX and prev_keys.numel() == B * T and prev_keys.dtype == torch.int32
     if B * T > SORT_MAX:  # sort capacity of one workgroup: accumulate row chunks in order
         rows = max(1, SORT_MAX // T)
         for r0 in range(0, B, rows):
@@ -117,7 +123,8 @@ def embed_bwd(ids: torch.Tensor, dh: torch.Tensor, dwte: torch.Tensor, dwpe: tor
     P = torch.empty(B * T, D, dtype=torch.float32, device=dh.device)
     N.check(N.lib().dtc_embed_bwd(keys.data_ptr(), dh.data_ptr(), dwte.data_ptr(), dwpe.data_ptr(), P.data_ptr(), B,
                                   T, D, dwte.shape[0], p, seed, step.data_ptr(), row0, 1 if beta != 0.0 else 0,
-                                  N.ptr(sq), N.stream_ptr(ids.device)), "dtc_embed_bwd")
+                                  N.ptr(sq), N.ptr(prev_keys), 1 if prev_valid else 0, N.stream_ptr(ids.device)),
+            "dtc_embed_bwd")
 
 
 SORT_MAX = 32768  # keys one LDS bitonic sort handles (csrc/elementwise.hip)

@@ -226,6 +226,10 @@ class Engine:
                                         and os.environ.get("DTC_FUSED_NORM", "1") == "1")
             elif self.embed_gather:
                 self.opt.set_chunks([self.buckets.reduce_end, self.flat.numel])
+        if on_gpu and pp == 1 and self._emb_fused_norm():
+            # one local embedding backward per step writes the wte grad: zero only the rows the previous step
+            # wrote instead of the 154 MB table (GPT-2 small)
+            self.stage.emb_prev = torch.zeros(self.b_local * self.T, dtype=torch.int32, device=self.device)
 
         # ---- static device-side inputs/outputs (graph replay reads/writes these)
         D = model_cfg.d_model
@@ -692,10 +696,11 @@ class Engine:
         return self.loss
 
     def _emb_fused_norm(self) -> bool:
-        """The embedding backward may write the wte / wpe share of Σg² itself: one local embedding backward
-        per step (no DP gather, no TP / sequence parallelism: norm weight 1), one sort window."""
-        return (self.layout.has_embed and self.mesh.tp == 1 and not self.embed_gather and not self.stage.sp
-                and self.b_local * self.T <= E.SORT_MAX)
+        """The embedding backward alone writes the wte / wpe grads, once per step, and they are final there: dp 1
+        (no all-reduce or gather of them), no TP / sequence parallelism (norm weight 1), one sort window.  Then it
+        may write the tables' share of Σg² itself and zero only the wte rows its previous call wrote."""
+        return (self.layout.has_embed and not self.dp_comm and self.mesh.tp == 1 and not self.embed_gather
+                and not self.stage.sp and self.b_local * self.T <= E.SORT_MAX)
 
     def loss_value(self) -> float:
         """Blocking read of the global mean loss (reference: float(np.asarray(loss)), train.py:82)."""

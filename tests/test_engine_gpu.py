@@ -186,10 +186,16 @@ def test_fused_grad_norm_matches(cuda, monkeypatch):
             loss, norm = eng.loss_value(), eng.opt.grad_norm()
             g = eng.flat.grads.double().norm().item()  # tp = 1: every norm weight is 1
             assert norm == pytest.approx(g, rel=1e-5), (fused, len(out), norm, g)
+            # sparse wte-grad zeroing (only the previous step's rows): every row this step's ids miss is zero
+            dwte = eng.flat.g("wte")
+            miss = torch.ones(dwte.shape[0], dtype=torch.bool, device=dwte.device)
+            miss[eng.ids.reshape(-1).long()] = False
+            assert int(dwte[miss].abs().max().item() == 0.0) == 1, (fused, len(out))
             out.append((loss, norm))
         assert (eng.stage.wg_sq is not None) == (fused == "1")
         # ... and the embedding backward's Σ dwte² + Σ dwpe² partials replace the norm pass over both tables
         assert (eng.stage.emb_sq is not None) == (fused == "1")
+        assert eng.stage.emb_prev is not None and eng.stage._emb_prev_valid
         runs[fused] = out
         del eng
     assert runs["1"][0] == runs["0"][0]  # step 1 (eager, before the switch) is identical
