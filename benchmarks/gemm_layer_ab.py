@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default="")
-    ap.add_argument("--variants", default="", help="comma list of plan variants: n8, n8w3, n8w4, n8k768, r8, r8f, r8nn, nor8, r8ilv, s192")
+    ap.add_argument("--variants", default="", help="comma list of plan variants: n8, n8w3, n8w4, n8k768, r8, r8f, r8nn, nor8")
     ap.add_argument("--cold", action="store_true",
                     help="write a 512 MB buffer before every call (operands come from HBM, as in the step)")
     a = ap.parse_args()
@@ -117,26 +117,21 @@ def main():
     # 128 x 64CB kernel for multi-round problems too (DTC_GEMM8N bit 4), "n8w4" = with 128 x 256 tiles
     L = N.lib()
     # "n8k768": one-round gemm8n problems down to K = 768 (the out_proj forward / dgrad)
-    # "s192": one-round NT fp32 problems as 256 x 192 split-K 2 tiles (DTC_SPLIT192)
     # "r8": the mixed-width 256-row plan (DTC_GEMM8R=1, bf16 epilogues), "r8f": also fp32 outputs (=3)
     r8_default = L.dtc_gemm_set_r8(0)
     variants = {"ours": (3, 0, 1024, r8_default)}
     for v in [x for x in a.variants.split(",") if x]:
         variants[v] = {"n8": (7, 0, 1024, 0), "n8w3": (7, 3, 1024, 0), "n8w4": (7, 4, 1024, 0),
                        "n8k768": (3, 0, 768, 0), "r8": (3, 0, 1024, 1), "r8f": (3, 0, 1024, 3),
-                       "r8nn": (3, 0, 1024, 5), "nor8": (3, 0, 1024, 0), "r8ilv": None,
-                       "s192": (3, 0, 1024, r8_default, None, 1)}[v]
+                       "r8nn": (3, 0, 1024, 5), "nor8": (3, 0, 1024, 0), "r8ilv": None}[v]
 
     ilv_default = L.dtc_gemm_set_r8_ilv(0)
     L.dtc_gemm_set_r8_ilv(ilv_default)
     if "r8ilv" in variants:
         variants["r8ilv"] = variants["ours"] + (1,)
-    split192_default = L.dtc_gemm_set_split192(0)
-    variants["ours"] = variants["ours"] + (None, split192_default)
 
     def use(v):
-        L.dtc_gemm_set_r8_ilv(v[4] if len(v) > 4 and v[4] is not None else ilv_default)
-        L.dtc_gemm_set_split192(v[5] if len(v) > 5 else split192_default)
+        L.dtc_gemm_set_r8_ilv(v[4] if len(v) > 4 else ilv_default)
         L.dtc_gemm_set_n8(v[0])
         L.dtc_gemm_set_n8_cb(v[1])
         L.dtc_gemm_set_n8_mink(v[2])

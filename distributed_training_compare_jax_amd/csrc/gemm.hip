@@ -2220,7 +2220,7 @@ __global__ void __launch_bounds__(NT2, 1) ce_dgrad256_kernel(CeDgradArgs a) {
 
 // C = beta*C + sum_z slab[z]   (fp32, deterministic order)
 __global__ void splitk_reduce(const float* __restrict__ slab, int split, long MN, float* __restrict__ C, long ldc,
-                              int N, float beta, const float* __restrict__ bias) {
+                              int N, float beta) {
   long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i4 >= MN) return;
   DTC_ASSERT(N % 4 == 0 && i4 + 4 <= MN);
@@ -2231,7 +2231,6 @@ __global__ void splitk_reduce(const float* __restrict__ slab, int split, long MN
     f32x4 t = *(const f32x4*)(slab + z * MN + i4);
     s += t;
   }
-  if (bias) s += *(const f32x4*)(bias + n);
   float* c = C + m * ldc + n;
   if (beta != 0.f) {
     f32x4 old = *(const f32x4*)c;
@@ -2741,7 +2740,7 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
         long MN = (long)a.M * a.N;
         int blocks = (int)((MN / 4 + 255) / 256);
         hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, p.split, MN,
-                           (float*)a.C, a.ldc, a.N, a.beta, (const float*)nullptr);
+                           (float*)a.C, a.ldc, a.N, a.beta);
         DTC_CHECK_LAUNCH();
       }
       return 0;
@@ -2762,7 +2761,7 @@ int launch_t(const GemmArgs& a, const Plan& p, hipStream_t st) {
     long MN = (long)a.M * a.N;
     int blocks = (int)((MN / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, p.split, MN,
-                       (float*)a.C, a.ldc, a.N, a.beta, (const float*)nullptr);
+                       (float*)a.C, a.ldc, a.N, a.beta);
     DTC_CHECK_LAUNCH();
   }
   return 0;
@@ -2874,18 +2873,10 @@ int launch_big(const GemmArgs& a, int split, hipStream_t st) {
     long MN = (long)a.M * a.N;
     int blocks = (int)((MN / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, (const float*)a.workspace, split, MN,
-                       (float*)a.C, a.ldc, a.N, a.beta, (const float*)a.bias);
+                       (float*)a.C, a.ldc, a.N, a.beta);
     DTC_CHECK_LAUNCH();
   }
   return 0;
-}
-
-// DTC_SPLIT192 (default 0): one-round NT fp32 problems whose 256 x 192 grid split-K 2 is exactly one block per CU
-// (GPT-2 small: the fc2 forward, the fc1 / qkv dgrads, M/256 x N/192 x 2 = 32 x 4 x 2) on gemm8p instead of gemm8n
-static int g_split192 = [] { const char* v = getenv("DTC_SPLIT192"); return v ? atoi(v) : 0; }();
-static bool split192(int layout, int M, int N, int K) {
-  if (!g_split192 || layout != 0 || K % 64 || K < 1024 || K >= 16384 || N % 192 || M % BIG) return false;
-  return (long)(M / BIG) * (N / 192) * 2 == cu_count() && (long)(M / BIG) * ((N + BIG - 1) / BIG) * 2 < cu_count();
 }
 
 // ---- gemm8r plans (layer GEMMs on 256-row tiles of two widths, one launch) ---------------------------
@@ -3147,7 +3138,7 @@ int launch_w(const GemmArgs& a, int split, hipStream_t st) {
   if (split > 1 && !a.defer_reduce) {
     long MN = (long)a.M * a.N;
     hipLaunchKernelGGL(splitk_reduce, dim3((int)((MN / 4 + 255) / 256)), dim3(256), 0, st, (const float*)a.workspace, split,
-                       MN, (float*)a.C, a.ldc, a.N, a.beta, (const float*)nullptr);
+                       MN, (float*)a.C, a.ldc, a.N, a.beta);
     DTC_CHECK_LAUNCH();
   }
   return 0;
@@ -3230,7 +3221,7 @@ int dtc_ce_dgrad(const bf16* logits, long ldl, const float* lse, const int* labe
   DTC_CHECK_LAUNCH();
   const long MN = (long)M * N;
   hipLaunchKernelGGL(splitk_reduce, dim3((int)((MN / 4 + 255) / 256)), dim3(256), 0, st, (const float*)ws, split, MN,
-                     dx, (long)N, N, 0.f, (const float*)nullptr);
+                     dx, (long)N, N, 0.f);
   DTC_CHECK_LAUNCH();
   return 0;
 }
@@ -3284,7 +3275,7 @@ int dtc_gemm_wgrad_fuses_colsum(int M, int N, int K) {
 
 long dtc_gemm_workspace_bytes(int layout, int M, int N, int K) {
   Plan p = make_plan(M, N, K, layout == 2 ? 1 : (layout == 1 ? 2 : 0));
-  const int bs = split192(layout, M, N, K) ? 2 : big_split(layout, M, N, K);
+  const int bs = big_split(layout, M, N, K);
   int split = bs ? bs : p.split;
   if (layout == 2 && !bs) split = std::max(split, dmaw_plan(2, M, N, K, EPI_STORE, true, false).split);
   return split > 1 ? (long)split * M * N * 4 : 0;
@@ -3308,12 +3299,6 @@ int dtc_gemm_set_n8(int mask) {
 int dtc_gemm_set_big_cb3(int on) {
   const int old = g_big_cb3;
   g_big_cb3 = on;
-  return old;
-}
-
-int dtc_gemm_set_split192(int on) {
-  const int old = g_split192;
-  g_split192 = on;
   return old;
 }
 
@@ -3402,8 +3387,6 @@ int dtc_gemm(const GemmArgs* a, hipStream_t st) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int epi = a->epi;
   const bool f32 = a->c_f32 != 0;
-  if (epi == EPI_STORE && f32 && !a->colsum && a->alpha == 1.f && a->beta == 0.f && split192(a->layout, a->M, a->N, a->K))
-    return launch_big<true, true, EPI_STORE, true>(*a, 2, st);
   if (a->layout <= 1 && !a->colsum && a->alpha == 1.f && a->beta == 0.f &&
       !n8_cb(a->layout, a->M, a->N, a->K, epi)) {
     const R8Plan pl = r8_plan(a->layout, a->M, a->N, a->K, epi, f32);

@@ -120,7 +120,6 @@ def _declare(lib):
         "dtc_gemm_set_r8_ilv": ([i], i),
         "dtc_gemm_set_big_cb3": ([i], i),
         "dtc_gemm_set_n8_mink": ([i], i),
-        "dtc_gemm_set_split192": ([i], i),
         "dtc_gemm_set_wgrad256": ([i], i),
         "dtc_wgrad_group": ([ctypes.POINTER(WgBatch), vp], i),
         "dtc_wg_entry_bytes": ([], i),
