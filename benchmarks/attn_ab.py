@@ -64,7 +64,12 @@ def main():
         torch.cuda.synchronize()
         print(f"fwd 2 waves/SIMD vs default (3): max |do| {(o.float() - o6.float()).abs().max().item():.3e} "
               f"max |dlse| {(lse - lse6).abs().max().item():.3e}", flush=True)
+        o7, lse7 = A.attn_fwd(qkv, H, flags=64)
+        torch.cuda.synchronize()
+        print(f"fwd heavy-first vs CU-balanced (default) order: max |do| {(o.float() - o7.float()).abs().max().item():.3e} "
+              f"max |dlse| {(lse - lse7).abs().max().item():.3e}", flush=True)
         variants = {"fwd (default, 3 waves/SIMD)": lambda: A.attn_fwd(qkv, H),
+                    "fwd heavy-first order": lambda: A.attn_fwd(qkv, H, flags=64),
                     "fwd (2 waves/SIMD, round 5)": lambda: A.attn_fwd(qkv, H, flags=32),
                     "fwd (round 4: 32 q/wave)": lambda: A.attn_fwd(qkv, H, flags=16),
                     "fwd (16 q/wave chunk)": lambda: A.attn_fwd(qkv, H, flags=4),

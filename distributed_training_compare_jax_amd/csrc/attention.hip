@@ -15,6 +15,7 @@
 // one workgroup per 64-key block sweeping the queries; dQ with one workgroup per 64-query
 // block sweeping the keys.  P is recomputed from the saved LSE.
 #include "common.h"
+#include <vector>
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -883,10 +884,21 @@ __global__ void __launch_bounds__(FW_THREADS, 2) attn_fwd32_kernel(const bf16* _
 // share a CU (768 blocks = one round at GPT-2 small) and the extra wave per SIMD covers the tile's serial
 // QK^T -> softmax -> PV chain: 27.21 -> 26.54 us per layer, bitwise identical (profiles/r6_attn_fwd_wps3.log;
 // 4 waves/SIMD spills 38 VGPRs).  flags bit 5 = the 2-wave form (A/B).
+// CU-balanced block order of a grid that is exactly one round (every block resident from the start): block
+// bid runs on XCD bid % 8 as that XCD's k = bid / 8-th block, and blocks k, k + C, k + 2C, ... of an XCD
+// (C = CUs per XCD) share a CU.  The host assigns the query blocks to those CU slots by longest-processing-
+// time-first (per-CU causal work within 1 unit instead of 17 vs 10 units of the heavy-first order at GPT-2
+// small): q[k] = query block, j[k] = which of its (b, h) on this XCD (bh = 8 j + XCD).  n = 0: heavy-first.
+constexpr int FW_ORDER_MAX = 256;
+struct FwOrder {
+  int n;
+  unsigned char q[FW_ORDER_MAX], j[FW_ORDER_MAX];
+};
+
 template <int HD, int WPS = 3>
 __global__ void __launch_bounds__(FW_THREADS, WPS) attn_fwd5_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ o,
                                                                float* __restrict__ lse, int B, int T, int H,
-                                                               float scale) {
+                                                               float scale, FwOrder ord) {
   static_assert(HD == 64, "round-5 forward: head_dim 64");
   constexpr int HC = HD / 16, HB = HD / 32;
   using L = FwLds<HD>;
@@ -895,8 +907,17 @@ __global__ void __launch_bounds__(FW_THREADS, WPS) attn_fwd5_kernel(const bf16* 
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nqb = (T + FW_QROWS - 1) / FW_QROWS, nbh = B * H;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / nbh);
-  const int bh = blockIdx.x % nbh, b = bh / H, h = bh % H;
+  int qblk, bh;
+  if (ord.n) {
+    const int k = (int)blockIdx.x >> 3;
+    DTC_ASSERT(k < ord.n);
+    qblk = ord.q[k];
+    bh = 8 * ord.j[k] + ((int)blockIdx.x & 7);
+  } else {
+    qblk = nqb - 1 - (int)(blockIdx.x / nbh);
+    bh = blockIdx.x % nbh;
+  }
+  const int b = bh / H, h = bh % H;
   DTC_ASSERT(qblk >= 0 && b < B && h < H);
   const long ts = 3L * H * HD;
   const bf16* Qb = qkv + (long)b * T * ts + (0 * H + h) * HD;
@@ -2056,6 +2077,40 @@ int dtc_attn_stamps(unsigned long long* host, long n) {
 #endif
 }
 
+// The CU-balanced order (FwOrder) for nqb query blocks x nbh (b, h) at WPS blocks per CU, or n = 0 when the
+// grid is not exactly one round of 8 equal XCDs.  Longest-processing-time-first per XCD: the query blocks,
+// heaviest first, each to the least-loaded CU with a free slot; CU c's s-th block becomes k = s * C + c.
+static FwOrder fw_order(int nqb, int nbh, int wps) {
+  static int cached_key = -1;
+  static FwOrder cached;
+  const int key = (nqb << 20) | (nbh << 4) | wps;
+  if (key == cached_key) return cached;
+  FwOrder ord{};
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 0;
+  const int C = cus / 8, per_xcd = nbh / 8 * nqb;
+  if (cus % 8 == 0 && nbh % 8 == 0 && C > 0 && per_xcd == C * wps && per_xcd <= FW_ORDER_MAX && nqb <= 255 &&
+      nbh / 8 <= 255) {
+    std::vector<int> load(C, 0), cnt(C, 0), used(nqb, 0);
+    for (int q = nqb - 1; q >= 0; --q)
+      for (int i = 0; i < nbh / 8; ++i) {
+        int c = -1;
+        for (int t = 0; t < C; ++t)
+          if (cnt[t] < wps && (c < 0 || load[t] < load[c])) c = t;
+        const int k = cnt[c] * C + c;
+        ord.q[k] = (unsigned char)q;
+        ord.j[k] = (unsigned char)used[q]++;
+        load[c] += q + 1;
+        ++cnt[c];
+      }
+    ord.n = per_xcd;
+  }
+  cached_key = key;
+  cached = ord;
+  return ord;
+}
+
 int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int HD, long flags, float scale,
                  hipStream_t st) {
   if (use_resident(T, HD)) {
@@ -2072,15 +2127,21 @@ int dtc_attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int T, int H, int 
   // bit 2 = the 16-row chunked kernel
   if (HD == 64 && (flags & 32) && !(flags & 16) && !(flags & 4) && attn_chunk_enabled()) {
     allow_lds(attn_fwd5_kernel<64, 2>, fw_lds_bytes<64>());
+    FwOrder ord;
+    ord.n = 0;
     hipLaunchKernelGGL((attn_fwd5_kernel<64, 2>), dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
-                       fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale);
+                       fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale, ord);
     DTC_CHECK_LAUNCH();
     return 0;
   }
   if (HD == 64 && !(flags & 16) && !(flags & 4) && attn_chunk_enabled()) {
     allow_lds(attn_fwd5_kernel<64, 3>, fw_lds_bytes<64>());
-    hipLaunchKernelGGL((attn_fwd5_kernel<64, 3>), dim3(B * H * ((T + FW_QROWS - 1) / FW_QROWS)), dim3(FW_THREADS),
-                       fw_lds_bytes<64>(), st, qkv, o, lse, B, T, H, scale);
+    const int nqb = (T + FW_QROWS - 1) / FW_QROWS;
+    // CU-balanced block order (default; flags bit 6 = the heavy-first order, A/B): 25.8 -> 24.2-24.5 us per
+    // GPT-2-small layer, bitwise identical (profiles/r6_attn_order_ab*.log)
+    const FwOrder ord = (flags & 64) ? FwOrder{} : fw_order(nqb, B * H, 3);
+    hipLaunchKernelGGL((attn_fwd5_kernel<64, 3>), dim3(B * H * nqb), dim3(FW_THREADS), fw_lds_bytes<64>(), st, qkv, o,
+                       lse, B, T, H, scale, ord);
     DTC_CHECK_LAUNCH();
     return 0;
   }

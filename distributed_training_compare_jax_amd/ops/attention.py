@@ -26,7 +26,8 @@ def attn_fwd(qkv: torch.Tensor, n_heads: int, scale: float | None = None, flags:
     """qkv [B,T,3*H*hd] → (o [B,T,H*hd], lse [B,H,T] fp32, natural-log units).  ``flags`` (A/B switches of
     ``dtc_attn_fwd``): bit 0 the resident kernel's plain wave → query-group order; bit 2 the 16-row chunked
     kernel; bit 4 the round-4 32-row kernel; bit 5 the round-5 forward at 2 waves per SIMD (the default
-    runs it at 3)."""
+    runs it at 3); bit 6 its heavy-first block order (the default assigns query blocks to CU slots
+    longest-processing-time-first)."""
     B, T, C3 = qkv.shape
     hd = C3 // (3 * n_heads)
     scale = scale if scale is not None else hd ** -0.5

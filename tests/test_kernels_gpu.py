@@ -287,6 +287,24 @@ def test_attention_fwd32_vs_chunk_and_reference(cuda, B, T, H, spike):
     assert torch.equal(d8, A.attn_bwd(qkv, o, lse, do, H, flags=8))
 
 
+def test_attention_fwd_balanced_order_bitwise(cuda):
+    """GPT-2 small shape (B8 T1024 H12: 768 blocks = one round at 3 per CU): the CU-balanced block order
+    (default) computes every (query block, b, h) exactly once, bitwise equal to the heavy-first order (flags
+    bit 6) and to the 2-waves-per-SIMD form (bit 5, heavy-first)."""
+    B, T, H, hd = 8, 1024, 12, 64
+    qkv = _r(B, T, 3 * H * hd, seed=44)
+    o, lse = A.attn_fwd(qkv, H)
+    o6, lse6 = A.attn_fwd(qkv, H, flags=64)
+    o5, lse5 = A.attn_fwd(qkv, H, flags=32)
+    assert torch.equal(o, o6) and torch.equal(lse, lse6)
+    assert torch.equal(o, o5) and torch.equal(lse, lse5)
+    # one head of one sequence against the fp32 reference (the order only moves whole blocks)
+    one = qkv[:1].view(1, T, 3, H, hd)[:, :, :, :1].reshape(1, T, 3 * hd)
+    oc, lsec = A.attn_fwd(one.cpu().float(), 1)
+    _close(o[:1, :, :hd].cpu(), oc, 2e-2, "attn_bal_o")
+    _close(lse[:1, :1].cpu(), lsec, 1e-3, "attn_bal_lse")
+
+
 @pytest.mark.parametrize("B,T,H", [(2, 512, 4), (1, 200, 3), (2, 64, 2)])
 def test_attention_bwd_fused_matches_two_round(cuda, B, T, H):
     """The fused single-round backward and the two-round resident kernels compute the same
